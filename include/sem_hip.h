@@ -1,0 +1,169 @@
+/*
+ * sem_hip.h -- C ABI of the MI355X spectral-element operator engine
+ * (libsem_hip.so, built from spectralelementmethod_amd/csrc/).
+ *
+ * The reference (nchisholm/SpectralElementMethod) has no FFI: its hot path is
+ * Python/NumPy classes.  Each entry point below replaces one piece of that
+ * path; the reference interface it stands in for is cited per function
+ * (paths relative to the reference checkout).  INTEGRATION.md shows the
+ * ctypes binding a maintainer adds on the reference side.
+ *
+ * Conventions
+ *   - n = p + 1 GLL nodes per direction; element-local nodal arrays are
+ *     [n][n] in lexicographic (xi0, xi1) order, C-contiguous, float64
+ *     (sem/basis_functions.py:647, sem/mapping.py:113).
+ *   - element->node map: uint32 [n_elem][n][n] (sem/discrete.py:1044).
+ *   - DOF index = dpn * node + comp (sem/discrete.py:567-574).
+ *   - Pointers named d_* are DEVICE pointers (caller-owned, e.g. PyTorch
+ *     tensors); pointers named h_* are host pointers.
+ *   - Every int-returning call returns SEM_OK (0) or a negative SEM_E_* code;
+ *     sem_last_error() gives a thread-local message.
+ *   - Work is enqueued on the caller's stream (hipStream_t passed as void*;
+ *     NULL = the legacy default stream).  sem_apply and the vector kernels
+ *     allocate nothing and do not synchronise (graph-capturable).
+ */
+#ifndef SEM_HIP_H
+#define SEM_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (mapped to the reference's Python exceptions) ---- */
+#define SEM_OK 0
+#define SEM_E_INVALID (-1)      /* ValueError      (sem/discrete.py:134, sem/basis_functions.py:358) */
+#define SEM_E_NOTIMPL (-2)      /* NotImplementedError (sem/basis_functions.py:366-369, sem/mapping.py:110-111) */
+#define SEM_E_DETJ (-3)         /* AssertionError detJ > 0 (sem/mapping.py:117) */
+#define SEM_E_HIP (-4)          /* HIP runtime failure */
+#define SEM_E_STATE (-5)        /* call order violated (e.g. apply before geometry) */
+
+/* ---- operator kinds ---- */
+#define SEM_OP_POISSON 0        /* scalar Laplacian Lse, examples/poisson.py:168-193 */
+#define SEM_OP_AXISYM_STOKES 1  /* [Lve.w ; E2e.psi - Me.w], squirmer-axisymmetric.py:193-254,278-295 (Re=0) */
+
+/* number of geometric factors per local node for an operator kind (3 or 7) */
+int sem_op_ncomp(int op_kind);
+
+const char* sem_last_error(void);
+const char* sem_version(void);
+
+/* ------------------------------------------------------------------ */
+/* Host-side basis data (C twins of the reference's 1-D basis layer)   */
+/* ------------------------------------------------------------------ */
+
+/* GLL nodes, barycentric and quadrature weights for 1 <= p <= 16, unfolded
+ * from the stored non-negative half exactly as LagrangeGaussLobatto.__init__
+ * (sem/basis_functions.py:349-393).  Orders 1..10 are the reference's
+ * basis-data.hdf5 values; 11..16 come from its generator
+ * sem/basis_data.py:19-109.  Each output has p+1 entries. */
+int sem_gll_table(int p, double* h_nodes, double* h_bary, double* h_quad);
+
+/* First-derivative matrix D1 (n*n, row-major) from nodes and barycentric
+ * weights: BarycentricLagrange.__init__ (sem/basis_functions.py:213-219). */
+int sem_diff_matrix(int n, const double* h_nodes, const double* h_bary, double* h_D);
+
+/* Lagrange basis evaluated at points: B[i][j] = l_j(x_i) (n_x*n, row-major),
+ * BarycentricLagrange.__call__ (sem/basis_functions.py:226-255). */
+int sem_lagrange_eval(int n, const double* h_nodes, const double* h_bary,
+                      int64_t n_x, const double* h_x, double* h_B);
+
+/* Equispaced interpolation matrix V_eq (= B at linspace(-1,1,n),
+ * sem/basis_functions.py:221-224) and its inverse (the lu_solve of
+ * TensorProduct.compute_coeffs_grid_eq, sem/basis_functions.py:599-624). */
+int sem_interp_eq_matrix(int n, const double* h_nodes, const double* h_bary,
+                         double* h_Veq, double* h_Veq_inv);
+
+/* C twins of sem/bary_interp.c:10-36 (legeval) and :39-90
+ * (barycentric_lagrange, 2 <= n <= 17 here; the reference's table stops at
+ * n = 9).  Interpolating exactly at a node returns the nodal value. */
+double sem_legeval(double x, unsigned n);
+double sem_barycentric_lagrange(const double* h_f, unsigned n, double x);
+
+/* ------------------------------------------------------------------ */
+/* Operator context (one per GPU)                                      */
+/* ------------------------------------------------------------------ */
+typedef struct sem_ctx sem_ctx;
+
+/* Replaces DOFManager(mesh, dofs_per_node, basis) bookkeeping
+ * (sem/discrete.py:81-124) for the batched operator path. */
+int sem_ctx_create(sem_ctx** out, int p, int64_t n_elem, int64_t n_node, int dpn, int device);
+void sem_ctx_destroy(sem_ctx* ctx);
+
+/* Basis of the operator: D (n*n, host) and 1-D quadrature weights w (n,
+ * host): TensorProductQS.get_D1_matrices() / quad_rule.weights
+ * (sem/basis_functions.py:156-162, sem/quadratures.py:246-252). */
+int sem_set_basis(sem_ctx* ctx, const double* h_D, const double* h_w);
+
+/* Element->node map (device, uint32 [n_elem][n][n]): the per-element
+ * FiniteElement.node_ind gather/scatter index (sem/discrete.py:658-663,
+ * 810-812).  The library keeps a repacked copy (coalesced per wavefront)
+ * plus the list of element-boundary nodes; synchronises `stream`. */
+int sem_set_map(sem_ctx* ctx, const uint32_t* d_e2n, void* stream);
+
+/* Geometry from mesh nodes (device, float64 [2][n_node]) for op_kind:
+ * x_phys = V_eq^-1 X V_eq^-T (Mapping._compute_x_phys, sem/mapping.py:98-103),
+ * J = gradient(x_phys) (sem/mapping.py:105-114), det/inverse
+ * (sem/linalg.py:105-115), detJxW (sem/discrete.py:594-597) and the operator's
+ * per-node factors (Poisson 3, axisymmetric 7).  h_Veq_inv is n*n host.
+ * Returns SEM_E_DETJ if any detJ <= 0 (count in *n_bad_nodes if non-NULL). */
+int sem_geom_from_nodes(sem_ctx* ctx, const double* d_nodes, const double* h_Veq_inv,
+                        int op_kind, int64_t* n_bad_nodes, void* stream);
+
+/* Reference-layout geometry fields for FiniteElement properties
+ * (x_phys [E][2][n][n], J and invJ [E][2][2][n][n], detJ and detJxW
+ * [E][n][n]; any output may be NULL).  sem/discrete.py:582-597. */
+int sem_geom_fields(sem_ctx* ctx, const double* d_nodes, const double* h_Veq_inv,
+                    double* d_x_phys, double* d_J, double* d_invJ, double* d_detJ,
+                    double* d_detJxW, void* stream);
+
+/* Install precomputed per-node factors (device, [n_elem][ncomp][n][n]). */
+int sem_set_geom(sem_ctx* ctx, const double* d_G, int op_kind, void* stream);
+
+/* Global operator action y (=|+=) K u over all elements: the element loop
+ * finite_elements() -> einsum('pqrs,rs', Op, u[loc]) -> y[loc] +=
+ * (sem/discrete.py:189-209; examples/squirmer-axisymmetric.py:286,293;
+ * examples/poisson.py:168-193), matrix-free by sum factorisation.
+ * u, y: device float64 of length dpn*n_node.  accumulate = 0 overwrites y. */
+int sem_apply(sem_ctx* ctx, int op_kind, const double* d_u, double* d_y, int accumulate,
+              void* stream);
+
+/* Diagonal of the assembled operator (Jacobi preconditioner for the
+ * assembled Poisson solve; diag(Lse) summed through the map). */
+int sem_diag(sem_ctx* ctx, int op_kind, double* d_diag, void* stream);
+
+/* Batched tensor-product operator on device arrays [batch][n][n]:
+ * out[b][m][q] = sum_{r,s} A0[m][r] A1[q][s] in[b][r][s]; A0/A1 are n*n host
+ * matrices, NULL meaning identity.  TensorProduct.deriv / gradient
+ * (D(x)I, I(x)D; sem/basis_functions.py:626-650), compute_coeffs_grid_eq
+ * (V_eq^-1 (x) V_eq^-1; :599-624), interpolate_on_grid_eq (:539-569). */
+int sem_tensor_apply(int n, int64_t batch, const double* h_A0, const double* h_A1,
+                     const double* d_in, double* d_out, void* stream);
+
+/* det_inv_2x2 (sem/linalg.py:105-115) over n points: d_mat [2][2][n] ->
+ * d_det [n], d_inv [2][2][n]. */
+int sem_det_inv_2x2(int64_t n, const double* d_mat, double* d_det, double* d_inv, void* stream);
+
+/* ------------------------------------------------------------------ */
+/* Device vector helpers (multi-GPU interface exchange, CG)            */
+/* ------------------------------------------------------------------ */
+/* dst[i] = src[idx[i]] */
+int sem_gather(const double* d_src, const uint32_t* d_idx, int64_t n, double* d_dst, void* stream);
+/* dst[idx[i]] += src[i]  (idx entries unique) */
+int sem_scatter_add(double* d_dst, const uint32_t* d_idx, int64_t n, const double* d_src,
+                    void* stream);
+
+/* Matrix-free preconditioned CG for K x = b on the free DOFs
+ * (mask[i] != 0 => Dirichlet DOF: x[i] fixed, row/col removed), Jacobi
+ * preconditioner.  Replaces DOFManagerSC.solve (sem/discrete.py:502-528).
+ * x holds the Dirichlet values and the initial guess on entry.  Synchronises
+ * `stream` once per iteration for the convergence test. */
+int sem_pcg_solve(sem_ctx* ctx, int op_kind, const double* d_b, double* d_x,
+                  const uint8_t* d_dirichlet, double rtol, int max_iter,
+                  int* iters, double* final_relres, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SEM_HIP_H */

@@ -1,0 +1,44 @@
+"""Build libsem_hip.so in-tree with hipcc for gfx950 (no JIT cache, no torch
+extension machinery: the library exposes a plain C ABI, include/sem_hip.h)."""
+import os
+import subprocess
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG_DIR, "csrc")
+LIB_NAME = "libsem_hip.so"
+LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
+SOURCES = ["sem_device.hip", "sem_basis.cpp"]
+DEPS = SOURCES + ["sem_internal.h", "gll_table.h"]
+ARCH = os.environ.get("SEM_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc():
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    cand = os.path.join(rocm, "bin", "hipcc")
+    return cand if os.path.exists(cand) else "hipcc"
+
+
+def needs_rebuild():
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    deps = [os.path.join(CSRC, d) for d in DEPS]
+    deps.append(os.path.join(os.path.dirname(PKG_DIR), "include", "sem_hip.h"))
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force=False, verbose=True):
+    if not force and not needs_rebuild():
+        return LIB_PATH
+    cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-fPIC", "-shared", "-std=c++17",
+           "-munsafe-fp-atomics", "-Wall", "-Wno-unused-result",
+           *[os.path.join(CSRC, s) for s in SOURCES], "-o", LIB_PATH + ".tmp"]
+    if verbose:
+        print("[sem build]", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    build(force=True)

@@ -1,0 +1,25 @@
+// Internal declarations shared by the host (sem_basis.cpp) and device
+// (sem_device.hip) halves of libsem_hip.so.
+#pragma once
+#include <cstdint>
+#include <string>
+
+#include "../../include/sem_hip.h"
+
+#define SEM_MAX_ORDER 16
+#define SEM_MAXN (SEM_MAX_ORDER + 1)
+
+namespace sem {
+
+// thread-local error message behind sem_last_error()
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+
+// host basis helpers (sem_basis.cpp)
+int gll_table(int p, double* nodes, double* bary, double* quad);
+void diff_matrix(int n, const double* nodes, const double* bary, double* D);
+void lagrange_eval(int n, const double* nodes, const double* bary, int64_t nx, const double* x,
+                   double* B);
+int invert(int n, const double* A, double* Ainv);
+
+}  // namespace sem

@@ -1,0 +1,70 @@
+"""Synthetic meshes for tests and benchmarks.
+
+The reference ships only Gmsh ``.geo`` sources (examples/meshes/*.geo) and
+no ``.msh``; gmsh is absent here.  These generators produce the same kind of
+mesh in memory, following the in-memory fixture pattern of
+tests/test_discrete.py:19-33 (nodes via np.mgrid, x-major global ids):
+
+* ``structured_square``: [-1,1]^2 with nex x ney quads of order p and
+  equispaced element nodes (Gmsh high-order node placement), optional warp
+  x,y += a sin(pi x) sin(pi y) for non-constant Jacobians
+  (examples/meshes/square.geo:1-15 stand-in).
+* ``annulus``: curved half-annulus in (rho, z), r in [r0, r1],
+  theta in [th0, pi - th0] (examples/meshes/donut.geo:1-22 stand-in).
+
+Both return ``nodes`` float64 [2, n_nodes] and ``e2n`` uint32 [E, n, n]
+(lexicographic (xi0, xi1), sem/discrete.py:1044).
+"""
+import numpy as np
+
+
+def _element_map(n_a, n_b, p, stride):
+    """e2n[ea*n_b + eb, i, j] = (ea*p + i)*stride + eb*p + j."""
+    n = p + 1
+    ea = np.arange(n_a, dtype=np.int64)[:, None, None, None]
+    eb = np.arange(n_b, dtype=np.int64)[None, :, None, None]
+    i = np.arange(n, dtype=np.int64)[None, None, :, None]
+    j = np.arange(n, dtype=np.int64)[None, None, None, :]
+    ids = (ea * p + i) * stride + eb * p + j
+    return ids.reshape(n_a * n_b, n, n).astype(np.uint32)
+
+
+def structured_square(nex, ney, p, warp=0.0, x0=-1.0, x1=1.0, y0=-1.0, y1=1.0):
+    """Structured quad mesh.  Node (ix, iy) -> id ix*Ny + iy with
+    Ny = ney*p + 1; element (ex, ey) -> id ex*ney + ey.  A strip of element
+    columns [ex0, ex1) therefore owns the contiguous node range
+    [ex0*p*Ny, (ex1*p + 1)*Ny)."""
+    Nx, Ny = nex * p + 1, ney * p + 1
+    if Nx * Ny >= 2 ** 32:
+        raise ValueError("mesh too large for a uint32 element map")
+    x = np.linspace(x0, x1, Nx)
+    y = np.linspace(y0, y1, Ny)
+    X, Y = np.meshgrid(x, y, indexing="ij")
+    if warp:
+        s = warp * np.sin(np.pi * X) * np.sin(np.pi * Y)
+        X = X + s
+        Y = Y + s
+    nodes = np.stack([X.ravel(), Y.ravel()])
+    return nodes, _element_map(nex, ney, p, Ny)
+
+
+def annulus(nth, nr, p, r0=1.0, r1=4.0, th0=0.05, th1=np.pi - 0.05):
+    """Curved annulus: xi0 <-> theta, xi1 <-> r (positive Jacobian).
+    Node (it, ir) -> id it*Nr + ir."""
+    Nt, Nr = nth * p + 1, nr * p + 1
+    th = np.linspace(th0, th1, Nt)
+    r = np.linspace(r0, r1, Nr)
+    TH, R = np.meshgrid(th, r, indexing="ij")
+    nodes = np.stack([(R * np.sin(TH)).ravel(), (R * np.cos(TH)).ravel()])
+    return nodes, _element_map(nth, nr, p, Nr)
+
+
+def square_dirichlet_left_bottom(nodes, tol=1e-12):
+    """Essential-BC mask and values of the restated Poisson example:
+    u = 0.2((x+1) + (y+1)) on the left and bottom edges
+    (examples/poisson.py:137-140)."""
+    x, y = nodes
+    on = (np.abs(x + 1) < tol) | (np.abs(y + 1) < tol)
+    vals = np.zeros(x.shape)
+    vals[on] = 0.2 * ((x[on] + 1) + (y[on] + 1))
+    return on, vals

@@ -1,0 +1,252 @@
+"""Device operator context: the batched replacement of the reference's
+per-element Python loop.
+
+The reference applies an operator by iterating ``DOFManager.finite_elements``
+(sem/discrete.py:189-209), building each element's dense operator with
+einsums (examples/poisson.py:168-193; examples/squirmer-axisymmetric.py:
+193-254), multiplying it into the element's slice of the global vector
+(``np.einsum('pqrs,rs', Op, u[loc])``, squirmer:286,293) and adding the
+result back through ``FiniteElement.node_ind`` (sem/discrete.py:658-663).
+
+``SEMOperator`` owns one ``sem_ctx`` of libsem_hip.so on one GPU and does the
+same computation for all elements in one kernel launch, matrix-free by sum
+factorisation.  There is no CPU path: constructing it without the built
+library or without a GPU raises.
+"""
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib
+from .basis_functions import LagrangeGaussLobatto, TensorProductQS
+
+POISSON = _lib.OP_POISSON
+AXISYM_STOKES = _lib.OP_AXISYM_STOKES
+_KIND_NAMES = {"poisson": POISSON, "laplace": POISSON, "stiffness": POISSON,
+               "axisym_stokes": AXISYM_STOKES, "stokes_axisym": AXISYM_STOKES}
+
+
+def op_kind(kind):
+    if isinstance(kind, str):
+        try:
+            return _KIND_NAMES[kind.lower()]
+        except KeyError:
+            raise ValueError("unknown operator kind %r" % kind)
+    if kind not in (POISSON, AXISYM_STOKES):
+        raise ValueError("unknown operator kind %r" % kind)
+    return int(kind)
+
+
+def _device_index(device):
+    if device is None:
+        if not torch.cuda.is_available():
+            raise RuntimeError("SEMOperator needs a GPU (no HIP device visible)")
+        return torch.cuda.current_device()
+    device = torch.device(device)
+    if device.type != "cuda":
+        raise ValueError("SEMOperator runs on a HIP device, got %s" % device)
+    return device.index if device.index is not None else torch.cuda.current_device()
+
+
+def _basis_arrays(p, basis):
+    if basis is None:
+        b1 = LagrangeGaussLobatto(p)
+        basis = TensorProductQS(b1, b1)
+    D = np.ascontiguousarray(basis.get_D1_matrices()[0], dtype=np.float64)
+    D1 = basis.get_D1_matrices()[1]
+    if not np.array_equal(D, D1):
+        raise NotImplementedError("anisotropic tensor bases are not supported by the kernels")
+    w = np.ascontiguousarray(basis.quad_rule.weights[0], dtype=np.float64)
+    sub = basis._subbases[0]
+    Vinv = np.ascontiguousarray(sub._interp_eq_inv, dtype=np.float64)
+    return basis, D, w, Vinv
+
+
+class SEMOperator(object):
+    """Matrix-free spectral-element operators on one GPU.
+
+    Parameters
+    ----------
+    p : int
+        Polynomial order (1..16).
+    e2n : array-like uint32 [n_elem, p+1, p+1]
+        Element -> global node map (lexicographic, sem/discrete.py:1044).
+    nodes : array-like float64 [2, n_node]
+        Mesh node coordinates (equispaced within each element).
+    dofs_per_node : int
+        1 for the Poisson operator, 2 (interleaved psi, omega) for the
+        axisymmetric Stokes block.
+    basis : TensorProductQS, optional
+    device : torch.device or str, optional
+    """
+
+    def __init__(self, p, e2n, nodes, dofs_per_node=1, basis=None, device=None):
+        self._lib = _lib.load()
+        self.p = int(p)
+        self.n = self.p + 1
+        self.dpn = int(dofs_per_node)
+        dev = _device_index(device)
+        self.device = torch.device("cuda", dev)
+        self.basis, self.D, self.w, self.Vinv = _basis_arrays(self.p, basis)
+        e2n_t = self._to_map(e2n)
+        if e2n_t.dim() != 3 or tuple(e2n_t.shape[1:]) != (self.n, self.n):
+            raise ValueError("e2n must have shape [E, %d, %d]" % (self.n, self.n))
+        nodes_t = torch.as_tensor(nodes, dtype=torch.float64)
+        if nodes_t.dim() != 2 or nodes_t.shape[0] != 2:
+            raise ValueError("nodes must have shape [2, n_node]")
+        self.n_elem = int(e2n_t.shape[0])
+        self.n_node = int(nodes_t.shape[1])
+        self.ndof = self.dpn * self.n_node
+        with torch.cuda.device(self.device):
+            self.e2n = e2n_t.to(self.device).contiguous()
+            self.nodes = nodes_t.to(self.device).contiguous()
+            ctx = C.c_void_p()
+            _lib.check(self._lib.sem_ctx_create(C.byref(ctx), self.p, self.n_elem, self.n_node,
+                                                self.dpn, dev))
+            self._ctx = ctx
+            _lib.check(self._lib.sem_set_basis(ctx, _lib.dptr(self.D), _lib.dptr(self.w)))
+            _lib.check(self._lib.sem_set_map(ctx, _lib.tptr(self.e2n), _lib.stream_ptr()))
+        self._geom_ready = set()
+
+    @staticmethod
+    def _to_map(e2n):
+        if isinstance(e2n, torch.Tensor):
+            if e2n.dtype == torch.int32:
+                return e2n
+            if e2n.dtype == torch.uint32:
+                return e2n.view(torch.int32)
+            e2n = e2n.cpu().numpy()
+        a = np.ascontiguousarray(e2n)
+        if a.dtype != np.uint32:
+            if a.size and (a.min() < 0 or a.max() >= 2 ** 32):
+                raise ValueError("element map entries must fit uint32")
+            a = a.astype(np.uint32)
+        return torch.from_numpy(a.view(np.int32))
+
+    # ------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self._lib.sem_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _stream(self, stream):
+        return _lib.stream_ptr(stream)
+
+    # ------------------------------------------------------------------
+    def compute_geometry(self, kind=POISSON, stream=None):
+        """Per-node geometric factors for ``kind`` from the mesh nodes
+        (Mapping: sem/mapping.py:98-119; detJxW: sem/discrete.py:594-597).
+        Raises AssertionError when detJ <= 0 anywhere (sem/mapping.py:117)."""
+        kind = op_kind(kind)
+        bad = C.c_int64(0)
+        with torch.cuda.device(self.device):
+            _lib.check(self._lib.sem_geom_from_nodes(self._ctx, _lib.tptr(self.nodes),
+                                                     _lib.dptr(self.Vinv), kind, C.byref(bad),
+                                                     self._stream(stream)))
+        self._geom_ready.add(kind)
+        return self
+
+    def set_geometry(self, G, kind=POISSON, stream=None):
+        """Install user factors [E, ncomp, n, n] (device or host)."""
+        kind = op_kind(kind)
+        ncomp = self._lib.sem_op_ncomp(kind)
+        G = torch.as_tensor(G, dtype=torch.float64).to(self.device).contiguous()
+        if tuple(G.shape) != (self.n_elem, ncomp, self.n, self.n):
+            raise ValueError("G must have shape [%d, %d, %d, %d]" % (self.n_elem, ncomp, self.n,
+                                                                     self.n))
+        with torch.cuda.device(self.device):
+            _lib.check(self._lib.sem_set_geom(self._ctx, _lib.tptr(G), kind, self._stream(stream)))
+            torch.cuda.current_stream().synchronize()
+        self._geom_ready.add(kind)
+        return self
+
+    def geometry_fields(self, stream=None):
+        """Reference-layout x_phys [E,2,n,n], J/invJ [E,2,2,n,n],
+        detJ/detJxW [E,n,n] as device tensors (FiniteElement properties,
+        sem/discrete.py:582-597)."""
+        E, n = self.n_elem, self.n
+        kw = dict(dtype=torch.float64, device=self.device)
+        out = dict(x_phys=torch.empty(E, 2, n, n, **kw), J=torch.empty(E, 2, 2, n, n, **kw),
+                   invJ=torch.empty(E, 2, 2, n, n, **kw), detJ=torch.empty(E, n, n, **kw),
+                   detJxW=torch.empty(E, n, n, **kw))
+        with torch.cuda.device(self.device):
+            _lib.check(self._lib.sem_geom_fields(
+                self._ctx, _lib.tptr(self.nodes), _lib.dptr(self.Vinv), _lib.tptr(out["x_phys"]),
+                _lib.tptr(out["J"]), _lib.tptr(out["invJ"]), _lib.tptr(out["detJ"]),
+                _lib.tptr(out["detJxW"]), self._stream(stream)))
+        return out
+
+    # ------------------------------------------------------------------
+    def _vec(self, v, name):
+        if not isinstance(v, torch.Tensor):
+            v = torch.as_tensor(np.ascontiguousarray(v, dtype=np.float64))
+        if v.dtype != torch.float64:
+            raise TypeError("%s must be float64" % name)
+        if v.device != self.device:
+            v = v.to(self.device)
+        if not v.is_contiguous():
+            v = v.contiguous()
+        if v.numel() != self.ndof:
+            raise ValueError("%s has %d entries, expected ndof = %d" % (name, v.numel(), self.ndof))
+        return v
+
+    def apply(self, u, out=None, kind=POISSON, accumulate=False, stream=None):
+        """out (=|+=) K u for all elements in one launch (device tensors)."""
+        kind = op_kind(kind)
+        if kind not in self._geom_ready:
+            self.compute_geometry(kind, stream=stream)
+        is_np = not isinstance(u, torch.Tensor)
+        u = self._vec(u, "u")
+        if out is None:
+            out = torch.empty_like(u)
+            accumulate = False
+        elif not (isinstance(out, torch.Tensor) and out.dtype == torch.float64
+                  and out.device == self.device and out.is_contiguous()
+                  and out.numel() == self.ndof):
+            raise TypeError("out must be a contiguous float64 tensor of %d entries on %s"
+                            % (self.ndof, self.device))
+        with torch.cuda.device(self.device):
+            _lib.check(self._lib.sem_apply(self._ctx, kind, _lib.tptr(u), _lib.tptr(out),
+                                           1 if accumulate else 0, self._stream(stream)))
+        if is_np:
+            return out.cpu().numpy()
+        return out
+
+    def diag(self, kind=POISSON, stream=None):
+        kind = op_kind(kind)
+        if kind not in self._geom_ready:
+            self.compute_geometry(kind, stream=stream)
+        d = torch.empty(self.ndof, dtype=torch.float64, device=self.device)
+        with torch.cuda.device(self.device):
+            _lib.check(self._lib.sem_diag(self._ctx, kind, _lib.tptr(d), self._stream(stream)))
+        return d
+
+    def pcg_solve(self, rhs, x, dirichlet, rtol=1e-13, max_iter=20000, kind=POISSON,
+                  stream=None):
+        """Solve K x = rhs on the free DOFs (``dirichlet`` True => x fixed)
+        with Jacobi-preconditioned CG on the device.  ``x`` (device tensor) is
+        updated in place and returned with (iterations, relative residual)."""
+        kind = op_kind(kind)
+        if kind not in self._geom_ready:
+            self.compute_geometry(kind, stream=stream)
+        rhs = self._vec(rhs, "rhs")
+        if not isinstance(x, torch.Tensor) or x.device != self.device:
+            raise TypeError("x must be a device tensor on %s" % self.device)
+        x = self._vec(x, "x")
+        mask = torch.as_tensor(dirichlet, dtype=torch.bool).to(self.device).to(torch.uint8)
+        if mask.numel() != self.ndof:
+            raise ValueError("dirichlet mask must have ndof entries")
+        its = C.c_int(0)
+        rel = C.c_double(0.0)
+        with torch.cuda.device(self.device):
+            _lib.check(self._lib.sem_pcg_solve(self._ctx, kind, _lib.tptr(rhs), _lib.tptr(x),
+                                               _lib.tptr(mask), float(rtol), int(max_iter),
+                                               C.byref(its), C.byref(rel), self._stream(stream)))
+        return x, its.value, rel.value
