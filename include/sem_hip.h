@@ -125,9 +125,18 @@ int sem_set_geom(sem_ctx* ctx, const double* d_G, int op_kind, void* stream);
  * finite_elements() -> einsum('pqrs,rs', Op, u[loc]) -> y[loc] +=
  * (sem/discrete.py:189-209; examples/squirmer-axisymmetric.py:286,293;
  * examples/poisson.py:168-193), matrix-free by sum factorisation.
- * u, y: device float64 of length dpn*n_node.  accumulate = 0 overwrites y. */
-int sem_apply(sem_ctx* ctx, int op_kind, const double* d_u, double* d_y, int accumulate,
+ * u, y: device float64 of length dpn*n_node.
+ * flags: 0 overwrites y (shared entries are zeroed first by a small list
+ * kernel); SEM_APPLY_ACCUMULATE adds into y; SEM_APPLY_SKIP_ZERO (overwrite
+ * mode only) states that the caller already ran sem_zero_shared on y. */
+#define SEM_APPLY_ACCUMULATE 1
+#define SEM_APPLY_SKIP_ZERO 2
+int sem_apply(sem_ctx* ctx, int op_kind, const double* d_u, double* d_y, int flags,
               void* stream);
+
+/* Zero the entries of y that the overwrite-mode kernel does not store
+ * (element-boundary and unreferenced nodes; all dpn components). */
+int sem_zero_shared(sem_ctx* ctx, double* d_y, void* stream);
 
 /* Diagonal of the assembled operator (Jacobi preconditioner for the
  * assembled Poisson solve; diag(Lse) summed through the map). */
@@ -150,6 +159,8 @@ int sem_det_inv_2x2(int64_t n, const double* d_mat, double* d_det, double* d_inv
 /* ------------------------------------------------------------------ */
 /* dst[i] = src[idx[i]] */
 int sem_gather(const double* d_src, const uint32_t* d_idx, int64_t n, double* d_dst, void* stream);
+/* dst[i] += src[i] */
+int sem_vec_add(double* d_dst, const double* d_src, int64_t n, void* stream);
 /* dst[idx[i]] += src[i]  (idx entries unique) */
 int sem_scatter_add(double* d_dst, const uint32_t* d_idx, int64_t n, const double* d_src,
                     void* stream);

@@ -23,6 +23,9 @@ SEM_E_STATE = -5
 OP_POISSON = 0
 OP_AXISYM_STOKES = 1
 
+APPLY_ACCUMULATE = 1
+APPLY_SKIP_ZERO = 2
+
 # every symbol include/sem_hip.h declares, with (restype, argtypes)
 _i64 = C.c_int64
 _dp = C.POINTER(C.c_double)
@@ -45,6 +48,8 @@ SIGNATURES = {
     "sem_geom_fields": (C.c_int, [_vp, _vp, _dp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "sem_set_geom": (C.c_int, [_vp, _vp, C.c_int, _vp]),
     "sem_apply": (C.c_int, [_vp, C.c_int, _vp, _vp, C.c_int, _vp]),
+    "sem_zero_shared": (C.c_int, [_vp, _vp, _vp]),
+    "sem_vec_add": (C.c_int, [_vp, _vp, _i64, _vp]),
     "sem_diag": (C.c_int, [_vp, C.c_int, _vp, _vp]),
     "sem_tensor_apply": (C.c_int, [C.c_int, _i64, _dp, _dp, _vp, _vp, _vp]),
     "sem_det_inv_2x2": (C.c_int, [_i64, _vp, _vp, _vp, _vp]),

@@ -652,6 +652,12 @@ __global__ void k_gather(const double* __restrict__ src, const uint32_t* __restr
     dst[t] = src[idx[t]];
 }
 
+__global__ void k_vec_add(double* __restrict__ dst, const double* __restrict__ src, int64_t n) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n;
+       t += (int64_t)gridDim.x * blockDim.x)
+    dst[t] += src[t];
+}
+
 __global__ void k_scatter_add(double* __restrict__ dst, const uint32_t* __restrict__ idx,
                               int64_t n, const double* __restrict__ src) {
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n;
@@ -1119,8 +1125,21 @@ int sem_set_geom(sem_ctx* c, const double* d_G, int op_kind, void* stream) {
   return SEM_OK;
 }
 
-int sem_apply(sem_ctx* c, int op_kind, const double* u, double* y, int accumulate, void* stream) {
+int sem_zero_shared(sem_ctx* c, double* y, void* stream) {
+  if (!c || !y) return fail(SEM_E_INVALID, "null argument");
+  if (!c->d_mapP) return fail(SEM_E_STATE, "map must be set");
+  DeviceGuard g(c->device);
+  if (c->n_zero)
+    hipLaunchKernelGGL(k_zero_list, dim3(grid_for(c->n_zero, BLOCK, 4096)), dim3(BLOCK), 0,
+                       S(stream), y, c->d_zero, c->n_zero, c->dpn);
+  HIP_TRY(hipGetLastError());
+  return SEM_OK;
+}
+
+int sem_apply(sem_ctx* c, int op_kind, const double* u, double* y, int flags, void* stream) {
   if (!c || !u || !y) return fail(SEM_E_INVALID, "null argument");
+  if (flags & ~(SEM_APPLY_ACCUMULATE | SEM_APPLY_SKIP_ZERO))
+    return fail(SEM_E_INVALID, "unknown sem_apply flags");
   int rc;
   if ((rc = check_op(c, op_kind))) return rc;
   if (!c->have_basis || !c->d_mapP) return fail(SEM_E_STATE, "basis and map must be set");
@@ -1128,10 +1147,19 @@ int sem_apply(sem_ctx* c, int op_kind, const double* u, double* y, int accumulat
     return fail(SEM_E_STATE, "geometry for this operator has not been computed");
   DeviceGuard g(c->device);
   hipStream_t st = S(stream);
-  if (!accumulate && c->n_zero)
+  const int accumulate = flags & SEM_APPLY_ACCUMULATE;
+  if (!accumulate && !(flags & SEM_APPLY_SKIP_ZERO) && c->n_zero)
     hipLaunchKernelGGL(k_zero_list, dim3(grid_for(c->n_zero, BLOCK, 4096)), dim3(BLOCK), 0, st, y,
                        c->d_zero, c->n_zero, c->dpn);
   SEM_DISPATCH_N(c->n, launch_apply_n, c, op_kind, u, y, accumulate, st);
+  HIP_TRY(hipGetLastError());
+  return SEM_OK;
+}
+
+int sem_vec_add(double* dst, const double* src, int64_t n, void* stream) {
+  if (n < 0 || (n && (!dst || !src))) return fail(SEM_E_INVALID, "bad arguments");
+  if (!n) return SEM_OK;
+  hipLaunchKernelGGL(k_vec_add, dim3(grid_for(n)), dim3(BLOCK), 0, S(stream), dst, src, n);
   HIP_TRY(hipGetLastError());
   return SEM_OK;
 }

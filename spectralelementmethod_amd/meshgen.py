@@ -48,6 +48,27 @@ def structured_square(nex, ney, p, warp=0.0, x0=-1.0, x1=1.0, y0=-1.0, y1=1.0):
     return nodes, _element_map(nex, ney, p, Ny)
 
 
+def structured_strip(nex, ney, p, ex0, ex1, warp=0.0):
+    """Element columns [ex0, ex1) of ``structured_square(nex, ney, p, warp)``
+    with nodes renumbered locally: local id = global id - ex0*p*Ny.  The
+    coordinates are slices of the same global linspace, so a node on a strip
+    boundary has bit-identical coordinates in both neighbouring strips.
+    Returns nodes [2, n_local], e2n [E_local, n, n], node_offset."""
+    if not (0 <= ex0 < ex1 <= nex):
+        raise ValueError("bad strip [%d, %d) of %d columns" % (ex0, ex1, nex))
+    Nx, Ny = nex * p + 1, ney * p + 1
+    ix0, ix1 = ex0 * p, ex1 * p + 1
+    x = np.linspace(-1.0, 1.0, Nx)[ix0:ix1]
+    y = np.linspace(-1.0, 1.0, Ny)
+    X, Y = np.meshgrid(x, y, indexing="ij")
+    if warp:
+        s = warp * np.sin(np.pi * X) * np.sin(np.pi * Y)
+        X = X + s
+        Y = Y + s
+    nodes = np.stack([X.ravel(), Y.ravel()])
+    return nodes, _element_map(ex1 - ex0, ney, p, Ny), ix0 * Ny
+
+
 def annulus(nth, nr, p, r0=1.0, r1=4.0, th0=0.05, th1=np.pi - 0.05):
     """Curved annulus: xi0 <-> theta, xi1 <-> r (positive Jacobian).
     Node (it, ir) -> id it*Nr + ir."""
