@@ -146,6 +146,8 @@ def main():
                                                           time.time() - t0))
     op = SEMOperator(p, e2n, nodes, dofs_per_node=dpn, device=dev)
     op.compute_geometry(kind)
+    plan = op.plan_info()
+    log("rank %d: plan %s" % (rank, plan))
     del nodes, e2n
     xchg = InterfaceExchange(part.neighbors, dpn, dev) if world > 1 else None
     log("rank %d: operator ready (%.1fs)" % (rank, time.time() - t0))
@@ -230,6 +232,8 @@ def main():
             "single GPU",
             "kernel_ms_avg": kern_avg_s * 1e3, "kernel_ms_min": float(np.min(kern_ms)),
             "gflops_kernel": F / kern_avg_s / 1e9,
+            "scatter_plan": {k: plan[k] for k in ("colours", "groups_per_colour", "zero_list",
+                                                  "atomic_groups")},
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

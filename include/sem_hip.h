@@ -102,6 +102,12 @@ int sem_set_basis(sem_ctx* ctx, const double* h_D, const double* h_w);
  * plus the list of element-boundary nodes; synchronises `stream`. */
 int sem_set_map(sem_ctx* ctx, const uint32_t* d_e2n, void* stream);
 
+/* Setup plan of the last sem_set_map (diagnostics): info[0] groups (one
+ * wavefront of elements each), [1] zero-list length, [2] atomic-fallback
+ * groups, [3] mesh conforming (0/1), [4] elements per group, [5] colour
+ * classes, [6..] groups per class.  Writes min(n_info, 15) values. */
+int sem_plan_info(sem_ctx* ctx, int64_t* info, int n_info);
+
 /* Geometry from mesh nodes (device, float64 [2][n_node]) for op_kind:
  * x_phys = V_eq^-1 X V_eq^-T (Mapping._compute_x_phys, sem/mapping.py:98-103),
  * J = gradient(x_phys) (sem/mapping.py:105-114), det/inverse

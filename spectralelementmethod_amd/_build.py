@@ -8,7 +8,7 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_NAME = "libsem_hip.so"
 LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
 SOURCES = ["sem_device.hip", "sem_basis.cpp"]
-DEPS = SOURCES + ["sem_internal.h", "gll_table.h"]
+DEPS = SOURCES + ["sem_internal.h", "sem_kernels.h", "gll_table.h"]
 ARCH = os.environ.get("SEM_OFFLOAD_ARCH", "gfx950")
 
 

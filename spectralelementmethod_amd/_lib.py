@@ -44,6 +44,7 @@ SIGNATURES = {
     "sem_ctx_destroy": (None, [_vp]),
     "sem_set_basis": (C.c_int, [_vp, _dp, _dp]),
     "sem_set_map": (C.c_int, [_vp, _vp, _vp]),
+    "sem_plan_info": (C.c_int, [_vp, C.POINTER(_i64), C.c_int]),
     "sem_geom_from_nodes": (C.c_int, [_vp, _vp, _dp, C.c_int, C.POINTER(_i64), _vp]),
     "sem_geom_fields": (C.c_int, [_vp, _vp, _dp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "sem_set_geom": (C.c_int, [_vp, _vp, C.c_int, _vp]),

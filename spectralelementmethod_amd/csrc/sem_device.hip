@@ -1,35 +1,21 @@
-// Device half of libsem_hip.so: the operator context, the geometry kernel,
-// the matrix-free operator kernels and the C ABI that launches them.
-//
-// Hot path (BASELINE.json north_star):
-//   for every element e:  u_e = u[map[e]]                       (gather)
-//                         d0 = D u_e,  d1 = u_e D^T              (D(x)I, I(x)D)
-//                         w0 = G00 d0 + G01 d1, w1 = G01 d0 + G11 d1
-//                         y_e = D^T w0 + w1 D                    (transposed pass)
-//                         y[map[e]] += y_e                       (scatter-add)
-// which equals the reference's per-element dense action
-// einsum('pqrs,rs', Lse, u[loc]) (examples/poisson.py:168-193,
-// examples/squirmer-axisymmetric.py:286) to rounding.
-//
-// CDNA4 mapping: one wavefront owns EPW = floor(64 / n)
-// elements, lane = (element slot, line j).  Contractions along the lane's own
-// column/row run in registers with D read as wave-uniform scalars (kernel
-// arguments -> SGPRs); the two transposes go through a wave-private LDS tile,
-// so no workgroup barrier is ever needed.  The element map and the geometric
-// factors are repacked at setup into [group][row][lane] order so that every
-// wave-instruction streams one contiguous run of HBM.
+// Device half of libsem_hip.so: the operator context, the setup planner
+// (map packing, group colouring, write codes) and the C ABI that launches
+// the kernels of sem_kernels.h.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
 
 #include "sem_internal.h"
+#include "sem_kernels.h"
 
 using sem::fail;
+using namespace semk;
 
 #define HIP_TRY(expr)                                                                  \
   do {                                                                                 \
@@ -40,522 +26,11 @@ using sem::fail;
 
 namespace {
 
-constexpr int WAVE = 64;
-constexpr int BLOCK = 256;
-constexpr int WAVES_PER_BLOCK = BLOCK / WAVE;
-
 inline int epw_of(int n) { return WAVE / n; }
 
-template <int N>
-struct DMat {
-  double v[N * N];
-};
-
-// Ordering point for LDS traffic between lanes of ONE wavefront (a wave's LDS
-// operations complete in issue order; this only stops the compiler moving
-// them across the exchange).
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__device__ __forceinline__ void atomic_add_f64(double* p, double v) {
-  unsafeAtomicAdd(p, v);  // global_atomic_add_f64, no return
-}
-
-// ---------------------------------------------------------------------------
-// Poisson stiffness action
-// ---------------------------------------------------------------------------
-// Packed layouts (built by k_pack_map / k_geometry):
-//   mapP[g][r][k*N + j]        = map[g*EPW + k][r][j]
-//   GP  [g][c][r][k*N + j]     = factor c at node (r, j) of element g*EPW + k
-// with LW = EPW*N values per (g, r).  Padding elements map to node 0 with
-// zero factors and are masked at the scatter.
-template <int N, bool ALL_ATOMIC>
-__global__ void __launch_bounds__(BLOCK)
-    k_poisson_apply(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
-                    const double* __restrict__ u, double* __restrict__ y, int64_t n_groups,
-                    int64_t n_elem, int accumulate, const DMat<N> D) {
-  constexpr int EPW = WAVE / N;
-  constexpr int LW = EPW * N;
-  constexpr int SLOTS = (WAVE + N - 1) / N;   // every lane owns a tile slot
-  constexpr int RS = (N % 2) ? N + 1 : N;     // 16-B aligned rows
-  constexpr int ES = N * RS;
-  __shared__ __attribute__((aligned(16))) double lds[WAVES_PER_BLOCK * SLOTS * ES];
-
-  const int wave = threadIdx.x / WAVE;
-  const int lane = threadIdx.x % WAVE;
-  const int64_t g = (int64_t)blockIdx.x * WAVES_PER_BLOCK + wave;
-  if (g >= n_groups) return;  // whole wavefront leaves; no block barriers below
-  const int k = lane / N;
-  const int j = lane - k * N;
-  const bool in_wave = lane < LW;
-  const bool active = in_wave && (g * EPW + k < n_elem);
-  double* L = lds + (wave * SLOTS + k) * ES;
-
-  const uint32_t* mp = mapP + g * (int64_t)(N * LW) + lane;
-  const double* gp = GP + g * (int64_t)(3 * N * LW) + lane;
-
-  uint32_t gid[N];
-  double uc[N];
-#pragma unroll
-  for (int r = 0; r < N; ++r) gid[r] = in_wave ? mp[r * LW] : 0u;
-#pragma unroll
-  for (int r = 0; r < N; ++r) uc[r] = in_wave ? u[gid[r]] : 0.0;
-
-  // column j: d0[m][j] = sum_r D[m][r] u[r][j]     (TensorProduct.deriv dim 0)
-  double d0[N];
-#pragma unroll
-  for (int m = 0; m < N; ++m) {
-    double a = 0.0;
-#pragma unroll
-    for (int r = 0; r < N; ++r) a = fma(D.v[m * N + r], uc[r], a);
-    d0[m] = a;
-  }
-#pragma unroll
-  for (int r = 0; r < N; ++r) L[r * RS + j] = uc[r];
-  wave_sync();
-
-  // row i = j: d1[i][q] = sum_s D[q][s] u[i][s]     (TensorProduct.deriv dim 1)
-  double t[N];
-  {
-    double ur[RS];
-    const double2* row = reinterpret_cast<const double2*>(L + j * RS);
-#pragma unroll
-    for (int s = 0; s < RS / 2; ++s) {
-      const double2 v = row[s];
-      ur[2 * s] = v.x;
-      ur[2 * s + 1] = v.y;
-    }
-#pragma unroll
-    for (int q = 0; q < N; ++q) {
-      double a = 0.0;
-#pragma unroll
-      for (int s = 0; s < N; ++s) a = fma(D.v[q * N + s], ur[s], a);
-      t[q] = a;
-    }
-  }
-  wave_sync();
-  {
-    double2* row = reinterpret_cast<double2*>(L + j * RS);
-#pragma unroll
-    for (int s = 0; s < N / 2; ++s) row[s] = make_double2(t[2 * s], t[2 * s + 1]);
-    if (N % 2) L[j * RS + N - 1] = t[N - 1];
-  }
-  wave_sync();
-
-  // column j: geometric factors, w0/w1, and ya = D^T w0 along xi0
-  double ya[N];
-  double w1[N];
-  {
-    double w0[N];
-#pragma unroll
-    for (int m = 0; m < N; ++m) {
-      const double d1 = L[m * RS + j];
-      const double g00 = gp[(0 * N + m) * LW];
-      const double g01 = gp[(1 * N + m) * LW];
-      const double g11 = gp[(2 * N + m) * LW];
-      w0[m] = fma(g00, d0[m], g01 * d1);
-      w1[m] = fma(g01, d0[m], g11 * d1);
-    }
-#pragma unroll
-    for (int p = 0; p < N; ++p) {
-      double a = 0.0;
-#pragma unroll
-      for (int m = 0; m < N; ++m) a = fma(D.v[m * N + p], w0[m], a);
-      ya[p] = a;
-    }
-  }
-  wave_sync();
-#pragma unroll
-  for (int m = 0; m < N; ++m) L[m * RS + j] = w1[m];
-  wave_sync();
-
-  // row i = j: yb[i][q] = sum_n D[n][q] w1[i][n]
-  {
-    double wr[RS];
-    const double2* row = reinterpret_cast<const double2*>(L + j * RS);
-#pragma unroll
-    for (int s = 0; s < RS / 2; ++s) {
-      const double2 v = row[s];
-      wr[2 * s] = v.x;
-      wr[2 * s + 1] = v.y;
-    }
-#pragma unroll
-    for (int q = 0; q < N; ++q) {
-      double a = 0.0;
-#pragma unroll
-      for (int nn = 0; nn < N; ++nn) a = fma(D.v[nn * N + q], wr[nn], a);
-      t[q] = a;
-    }
-  }
-  wave_sync();
-  {
-    double2* row = reinterpret_cast<double2*>(L + j * RS);
-#pragma unroll
-    for (int s = 0; s < N / 2; ++s) row[s] = make_double2(t[2 * s], t[2 * s + 1]);
-    if (N % 2) L[j * RS + N - 1] = t[N - 1];
-  }
-  wave_sync();
-
-  // column j: y[p][j] = ya[p] + yb[p][j]; scatter-add through the map.
-  // Element-boundary nodes may be shared -> atomic; interior nodes of a
-  // conforming mesh belong to this element only -> plain store.
-  if (active) {
-    const bool edge_col = (j == 0) || (j == N - 1);
-#pragma unroll
-    for (int p = 0; p < N; ++p) {
-      const double v = ya[p] + L[p * RS + j];
-      double* dst = y + gid[p];
-      if (ALL_ATOMIC || p == 0 || p == N - 1 || edge_col) {
-        atomic_add_f64(dst, v);
-      } else if (accumulate) {
-        *dst += v;
-      } else {
-        *dst = v;
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Axisymmetric Stokes block (Re = 0), dpn = 2 interleaved (psi, omega):
-//   y[2k]   = Lve.omega      = stiff_rho(omega) + (W/rho) omega
-//   y[2k+1] = E2e.psi - Me.omega = stiff_rho(psi) + 2W(iJ00 d0 + iJ10 d1)psi - rho^2 W omega
-// (examples/squirmer-axisymmetric.py:193-227, 253-254, 278-295)
-// factors per node: 0 G00rho 1 G01rho 2 G11rho 3 b0=2W iJ00 4 b1=2W iJ10 5 c=W/rho 6 m=rho^2 W
-// ---------------------------------------------------------------------------
-template <int N, bool ALL_ATOMIC>
-__global__ void __launch_bounds__(BLOCK)
-    k_axisym_apply(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
-                   const double* __restrict__ u, double* __restrict__ y, int64_t n_groups,
-                   int64_t n_elem, int accumulate, const DMat<N> D) {
-  constexpr int EPW = WAVE / N;
-  constexpr int LW = EPW * N;
-  constexpr int SLOTS = (WAVE + N - 1) / N;
-  constexpr int RS = (N % 2) ? N + 1 : N;
-  constexpr int ES = 2 * N * RS;  // two fields per tile
-  __shared__ __attribute__((aligned(16))) double lds[WAVES_PER_BLOCK * SLOTS * ES];
-
-  const int wave = threadIdx.x / WAVE;
-  const int lane = threadIdx.x % WAVE;
-  const int64_t g = (int64_t)blockIdx.x * WAVES_PER_BLOCK + wave;
-  if (g >= n_groups) return;
-  const int k = lane / N;
-  const int j = lane - k * N;
-  const bool in_wave = lane < LW;
-  const bool active = in_wave && (g * EPW + k < n_elem);
-  double* LP = lds + (wave * SLOTS + k) * ES;  // psi tile
-  double* LO = LP + N * RS;                     // omega tile
-
-  const uint32_t* mp = mapP + g * (int64_t)(N * LW) + lane;
-  const double* gp = GP + g * (int64_t)(7 * N * LW) + lane;
-  const double2* u2 = reinterpret_cast<const double2*>(u);
-
-  uint32_t gid[N];
-  double ps[N], om[N];
-#pragma unroll
-  for (int r = 0; r < N; ++r) gid[r] = in_wave ? mp[r * LW] : 0u;
-#pragma unroll
-  for (int r = 0; r < N; ++r) {
-    const double2 v = in_wave ? u2[gid[r]] : make_double2(0.0, 0.0);
-    ps[r] = v.x;
-    om[r] = v.y;
-  }
-  double d0p[N], d0o[N];
-#pragma unroll
-  for (int m = 0; m < N; ++m) {
-    double a = 0.0, b = 0.0;
-#pragma unroll
-    for (int r = 0; r < N; ++r) {
-      a = fma(D.v[m * N + r], ps[r], a);
-      b = fma(D.v[m * N + r], om[r], b);
-    }
-    d0p[m] = a;
-    d0o[m] = b;
-  }
-#pragma unroll
-  for (int r = 0; r < N; ++r) {
-    LP[r * RS + j] = ps[r];
-    LO[r * RS + j] = om[r];
-  }
-  wave_sync();
-  // row phase: d1 for both fields
-  {
-    double tp[N], to[N];
-    double rp[RS], ro[RS];
-    const double2* rowp = reinterpret_cast<const double2*>(LP + j * RS);
-    const double2* rowo = reinterpret_cast<const double2*>(LO + j * RS);
-#pragma unroll
-    for (int s = 0; s < RS / 2; ++s) {
-      const double2 a = rowp[s], b = rowo[s];
-      rp[2 * s] = a.x;
-      rp[2 * s + 1] = a.y;
-      ro[2 * s] = b.x;
-      ro[2 * s + 1] = b.y;
-    }
-#pragma unroll
-    for (int q = 0; q < N; ++q) {
-      double a = 0.0, b = 0.0;
-#pragma unroll
-      for (int s = 0; s < N; ++s) {
-        a = fma(D.v[q * N + s], rp[s], a);
-        b = fma(D.v[q * N + s], ro[s], b);
-      }
-      tp[q] = a;
-      to[q] = b;
-    }
-    wave_sync();
-#pragma unroll
-    for (int q = 0; q < N; ++q) {
-      LP[j * RS + q] = tp[q];
-      LO[j * RS + q] = to[q];
-    }
-  }
-  wave_sync();
-  // column phase: factors, pointwise terms, ya along xi0
-  double yap[N], yao[N], w1p[N], w1o[N];
-  {
-    double w0p[N], w0o[N];
-#pragma unroll
-    for (int m = 0; m < N; ++m) {
-      const double d1p = LP[m * RS + j];
-      const double d1o = LO[m * RS + j];
-      const double g00 = gp[(0 * N + m) * LW];
-      const double g01 = gp[(1 * N + m) * LW];
-      const double g11 = gp[(2 * N + m) * LW];
-      const double b0 = gp[(3 * N + m) * LW];
-      const double b1 = gp[(4 * N + m) * LW];
-      const double c = gp[(5 * N + m) * LW];
-      const double mm = gp[(6 * N + m) * LW];
-      w0p[m] = fma(g00, d0p[m], g01 * d1p);
-      w1p[m] = fma(g01, d0p[m], g11 * d1p);
-      w0o[m] = fma(g00, d0o[m], g01 * d1o);
-      w1o[m] = fma(g01, d0o[m], g11 * d1o);
-      // pointwise (test index = node (m, j)): psi row gets 2W gx(psi) - rho^2 W omega,
-      // omega row gets (W/rho) omega
-      d0p[m] = fma(b0, d0p[m], fma(b1, d1p, -mm * om[m]));
-      d0o[m] = c * om[m];
-    }
-#pragma unroll
-    for (int p = 0; p < N; ++p) {
-      double a = 0.0, b = 0.0;
-#pragma unroll
-      for (int m = 0; m < N; ++m) {
-        a = fma(D.v[m * N + p], w0p[m], a);
-        b = fma(D.v[m * N + p], w0o[m], b);
-      }
-      yap[p] = a + d0p[p];
-      yao[p] = b + d0o[p];
-    }
-  }
-  wave_sync();
-#pragma unroll
-  for (int m = 0; m < N; ++m) {
-    LP[m * RS + j] = w1p[m];
-    LO[m * RS + j] = w1o[m];
-  }
-  wave_sync();
-  {
-    double tp[N], to[N];
-    double rp[RS], ro[RS];
-    const double2* rowp = reinterpret_cast<const double2*>(LP + j * RS);
-    const double2* rowo = reinterpret_cast<const double2*>(LO + j * RS);
-#pragma unroll
-    for (int s = 0; s < RS / 2; ++s) {
-      const double2 a = rowp[s], b = rowo[s];
-      rp[2 * s] = a.x;
-      rp[2 * s + 1] = a.y;
-      ro[2 * s] = b.x;
-      ro[2 * s + 1] = b.y;
-    }
-#pragma unroll
-    for (int q = 0; q < N; ++q) {
-      double a = 0.0, b = 0.0;
-#pragma unroll
-      for (int nn = 0; nn < N; ++nn) {
-        a = fma(D.v[nn * N + q], rp[nn], a);
-        b = fma(D.v[nn * N + q], ro[nn], b);
-      }
-      tp[q] = a;
-      to[q] = b;
-    }
-    wave_sync();
-#pragma unroll
-    for (int q = 0; q < N; ++q) {
-      LP[j * RS + q] = tp[q];
-      LO[j * RS + q] = to[q];
-    }
-  }
-  wave_sync();
-  if (active) {
-    const bool edge_col = (j == 0) || (j == N - 1);
-#pragma unroll
-    for (int p = 0; p < N; ++p) {
-      // row 2k <- omega equation (Lve.omega), row 2k+1 <- psi equation
-      const double vo = yao[p] + LO[p * RS + j];
-      const double vp = yap[p] + LP[p * RS + j];
-      double* dst = y + 2 * (int64_t)gid[p];
-      if (ALL_ATOMIC || p == 0 || p == N - 1 || edge_col) {
-        atomic_add_f64(dst, vo);
-        atomic_add_f64(dst + 1, vp);
-      } else {
-        double2* d2 = reinterpret_cast<double2*>(dst);
-        if (accumulate) {
-          double2 o = *d2;
-          *d2 = make_double2(o.x + vo, o.y + vp);
-        } else {
-          *d2 = make_double2(vo, vp);
-        }
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Geometry: nodes -> x_phys -> J -> det/inv -> W -> operator factors.
-// Thread per local node, EPB elements per block, LDS staging (setup path).
-// ---------------------------------------------------------------------------
-template <int N>
-struct GeomShape {
-  static constexpr int NN = N * N;
-  static constexpr int EPB = (NN >= 256) ? 1 : 256 / NN;
-  static constexpr int THREADS = ((EPB * NN + 63) / 64) * 64;
-};
-
-template <int N>
-__global__ void __launch_bounds__(GeomShape<N>::THREADS)
-    k_geometry(const double* __restrict__ nodes, int64_t n_node, const uint32_t* __restrict__ e2n,
-               int64_t n_elem, const double* __restrict__ gVinv, const double* __restrict__ gD,
-               const double* __restrict__ gw, int op_kind, double* __restrict__ GP,
-               double* __restrict__ xph, double* __restrict__ Jo, double* __restrict__ iJo,
-               double* __restrict__ dJo, double* __restrict__ dJW,
-               unsigned long long* __restrict__ n_bad) {
-  using S = GeomShape<N>;
-  constexpr int NN = S::NN;
-  constexpr int EPB = S::EPB;
-  constexpr int EPW = WAVE / N;
-  constexpr int LW = EPW * N;
-  __shared__ double sV[NN], sD[NN], sw[N];
-  __shared__ double sx[EPB][2][NN], st[EPB][2][NN];
-  const int tid = threadIdx.x;
-  for (int i = tid; i < NN; i += blockDim.x) {
-    sV[i] = gVinv[i];
-    sD[i] = gD[i];
-  }
-  if (tid < N) sw[tid] = gw[tid];
-  const int el = tid / NN;
-  const int node = tid - el * NN;
-  const int m = node / N;
-  const int nq = node - m * N;
-  const int64_t e = (int64_t)blockIdx.x * EPB + el;
-  const bool act = (el < EPB) && (e < n_elem);
-  if (act) {
-    const uint32_t gi = e2n[e * NN + node];
-    sx[el][0][node] = nodes[gi];
-    sx[el][1][node] = nodes[n_node + gi];
-  }
-  __syncthreads();
-  // x_phys = Vinv X Vinv^T   (compute_coeffs_grid_eq: dim 0 then dim 1),
-  // evaluated on coordinates relative to the element's node (0,0): the map
-  // is translation invariant (V_eq reproduces constants) and J = D x_phys
-  // then no longer cancels the O(1) offset against O(h) variations.
-  double x0[2] = {0.0, 0.0};
-  if (act) {
-    x0[0] = sx[el][0][0];
-    x0[1] = sx[el][1][0];
-    for (int c = 0; c < 2; ++c) {
-      double a = 0.0;
-      for (int i = 0; i < N; ++i) a = fma(sV[m * N + i], sx[el][c][i * N + nq] - x0[c], a);
-      st[el][c][node] = a;
-    }
-  }
-  __syncthreads();
-  double xp[2] = {0.0, 0.0};
-  if (act) {
-    for (int c = 0; c < 2; ++c) {
-      double a = 0.0;
-      for (int jj = 0; jj < N; ++jj) a = fma(sV[nq * N + jj], st[el][c][m * N + jj], a);
-      xp[c] = a;
-    }
-  }
-  __syncthreads();
-  if (act) {
-    sx[el][0][node] = xp[0];
-    sx[el][1][node] = xp[1];
-  }
-  __syncthreads();
-  if (!act) return;
-  // J[c][d] = d x_c / d xi_d (TensorProduct.gradient, swapaxes(0,1))
-  double J[2][2];
-  for (int c = 0; c < 2; ++c) {
-    double a = 0.0, b = 0.0;
-    for (int r = 0; r < N; ++r) {
-      a = fma(sD[m * N + r], sx[el][c][r * N + nq], a);
-      b = fma(sD[nq * N + r], sx[el][c][m * N + r], b);
-    }
-    J[c][0] = a;
-    J[c][1] = b;
-  }
-  // det_inv_2x2 (sem/linalg.py:105-115)
-  const double det = J[0][0] * J[1][1] - J[0][1] * J[1][0];
-  const double rdet = 1.0 / det;
-  const double iJ00 = J[1][1] * rdet, iJ01 = -J[0][1] * rdet;
-  const double iJ10 = -J[1][0] * rdet, iJ11 = J[0][0] * rdet;
-  // detJxW via TensorQuadratureRule.xweight (sem/quadratures.py:268-275)
-  const double W = det * sw[m] * sw[nq];
-  if (!(det > 0.0)) atomicAdd(n_bad, 1ull);
-  const int64_t base = e * NN + node;
-  const double xabs0 = xp[0] + x0[0];
-  const double xabs1 = xp[1] + x0[1];
-  if (xph) {
-    xph[(e * 2 + 0) * NN + node] = xabs0;
-    xph[(e * 2 + 1) * NN + node] = xabs1;
-  }
-  if (Jo) {
-    Jo[(e * 4 + 0) * NN + node] = J[0][0];
-    Jo[(e * 4 + 1) * NN + node] = J[0][1];
-    Jo[(e * 4 + 2) * NN + node] = J[1][0];
-    Jo[(e * 4 + 3) * NN + node] = J[1][1];
-  }
-  if (iJo) {
-    iJo[(e * 4 + 0) * NN + node] = iJ00;
-    iJo[(e * 4 + 1) * NN + node] = iJ01;
-    iJo[(e * 4 + 2) * NN + node] = iJ10;
-    iJo[(e * 4 + 3) * NN + node] = iJ11;
-  }
-  if (dJo) dJo[base] = det;
-  if (dJW) dJW[base] = W;
-  if (GP) {
-    const int64_t gg = e / EPW;
-    const int kk = (int)(e - gg * EPW);
-    const int ncomp = (op_kind == SEM_OP_POISSON) ? 3 : 7;
-    double* o = GP + gg * (int64_t)(ncomp * N * LW) + m * LW + kk * N + nq;
-    const double A00 = iJ00 * iJ00 + iJ01 * iJ01;
-    const double A01 = iJ00 * iJ10 + iJ01 * iJ11;
-    const double A11 = iJ10 * iJ10 + iJ11 * iJ11;
-    if (op_kind == SEM_OP_POISSON) {
-      o[0 * N * LW] = W * A00;
-      o[1 * N * LW] = W * A01;
-      o[2 * N * LW] = W * A11;
-    } else {
-      const double rho = xabs0;
-      const double rW = rho * W;
-      o[0 * N * LW] = rW * A00;
-      o[1 * N * LW] = rW * A01;
-      o[2 * N * LW] = rW * A11;
-      o[3 * N * LW] = 2.0 * W * iJ00;
-      o[4 * N * LW] = 2.0 * W * iJ10;
-      o[5 * N * LW] = W / rho;
-      o[6 * N * LW] = rW * rho;
-    }
-  }
-}
-
-// user-supplied factors [E][ncomp][n][n] -> packed
+// user-supplied factors [E][ncomp][n][n] -> packed (group order via gpos)
 __global__ void k_pack_geom(const double* __restrict__ G, int64_t n_elem, int n, int ncomp,
-                            int epw, double* __restrict__ GP) {
+                            int epw, const int* __restrict__ gpos, double* __restrict__ GP) {
   const int64_t nn = (int64_t)n * n;
   const int64_t total = n_elem * ncomp * nn;
   const int lw = epw * n;
@@ -566,46 +41,10 @@ __global__ void k_pack_geom(const double* __restrict__ G, int64_t n_elem, int n,
     const int c = (int)(rem / nn);
     const int node = (int)(rem - c * nn);
     const int r = node / n, jj = node - r * n;
-    const int64_t gg = e / epw;
-    const int kk = (int)(e - gg * epw);
+    const int64_t grp = e / epw;
+    const int kk = (int)(e - grp * epw);
+    const int64_t gg = gpos[grp];
     GP[((gg * ncomp + c) * n + r) * lw + kk * n + jj] = G[t];
-  }
-}
-
-__global__ void k_pack_map(const uint32_t* __restrict__ e2n, int64_t n_elem, int n, int epw,
-                           int64_t n_groups, uint32_t* __restrict__ mapP) {
-  const int lw = epw * n;
-  const int64_t total = n_groups * n * lw;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t gg = t / (n * lw);
-    const int rem = (int)(t - gg * n * lw);
-    const int r = rem / lw;
-    const int lane = rem - r * lw;
-    const int kk = lane / n, jj = lane - kk * n;
-    const int64_t e = gg * epw + kk;
-    mapP[t] = (e < n_elem) ? e2n[(e * n + r) * n + jj] : 0u;
-  }
-}
-
-// reference counts: cnt[node] = total references, bnd[node] = 1 if referenced
-// as an element-boundary local node
-__global__ void k_node_refs(const uint32_t* __restrict__ e2n, int64_t n_elem, int n,
-                            int64_t n_node, unsigned* __restrict__ cnt,
-                            unsigned char* __restrict__ bnd, unsigned* __restrict__ n_oob) {
-  const int64_t nn = (int64_t)n * n;
-  const int64_t total = n_elem * nn;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t gi = e2n[t];
-    if ((int64_t)gi >= n_node) {
-      atomicAdd(n_oob, 1u);
-      continue;
-    }
-    const int node = (int)(t % nn);
-    const int r = node / n, jj = node - r * n;
-    atomicAdd(cnt + gi, 1u);
-    if (r == 0 || r == n - 1 || jj == 0 || jj == n - 1) bnd[gi] = 1;
   }
 }
 
@@ -621,9 +60,9 @@ __global__ void k_zero_list(double* __restrict__ y, const uint32_t* __restrict__
 // diag of the Poisson element operator, summed through the map:
 // K_e[pq,pq] = sum_m D[m][p]^2 G00[m][q] + sum_n D[n][q]^2 G11[p][n] + 2 D[p][p] D[q][q] G01[p][q]
 __global__ void k_poisson_diag(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
-                               const double* __restrict__ gD, int n, int epw, int64_t n_elem,
-                               double* __restrict__ diag) {
-  __shared__ double sD[SEM_MAXN * SEM_MAXN];
+                               const int* __restrict__ gpos, const double* __restrict__ gD, int n,
+                               int epw, int64_t n_elem, double* __restrict__ diag) {
+  __shared__ double sD[MAXN * MAXN];
   for (int i = threadIdx.x; i < n * n; i += blockDim.x) sD[i] = gD[i];
   __syncthreads();
   const int lw = epw * n;
@@ -633,14 +72,15 @@ __global__ void k_poisson_diag(const uint32_t* __restrict__ mapP, const double* 
     const int64_t e = t / (n * n);
     const int node = (int)(t - e * n * n);
     const int p = node / n, q = node - p * n;
-    const int64_t gg = e / epw;
-    const int kk = (int)(e - gg * epw);
+    const int64_t grp = e / epw;
+    const int kk = (int)(e - grp * epw);
+    const int64_t gg = gpos[grp];
     const double* G = GP + gg * (int64_t)(3 * n * lw) + kk * n;
     double s = 0.0;
     for (int m = 0; m < n; ++m) s += sD[m * n + p] * sD[m * n + p] * G[(0 * n + m) * lw + q];
     for (int nn = 0; nn < n; ++nn) s += sD[nn * n + q] * sD[nn * n + q] * G[(2 * n + p) * lw + nn];
     s += 2.0 * sD[p * n + p] * sD[q * n + q] * G[(1 * n + p) * lw + q];
-    const uint32_t gi = mapP[(gg * n + p) * lw + kk * n + q];
+    const uint32_t gi = mapP[(gg * n + p) * lw + kk * n + q] & GID_MASK;
     atomic_add_f64(diag + gi, s);
   }
 }
@@ -680,7 +120,7 @@ __device__ double block_sum(double v) {
   return s;
 }
 
-// partial[b] = sum a[i]*b[i] over the block's grid-stride slice (two dots at once)
+// partial[b] = sum a*b (and c*d) over the block's grid-stride slice
 __global__ void __launch_bounds__(BLOCK) k_dot2(const double* __restrict__ a,
                                                 const double* __restrict__ b,
                                                 const double* __restrict__ c,
@@ -764,8 +204,8 @@ __global__ void k_update_p(double* __restrict__ p, const double* __restrict__ z,
 __global__ void k_tensor_apply(int n, int64_t batch, const double* __restrict__ gA0,
                                const double* __restrict__ gA1, const double* __restrict__ in,
                                double* __restrict__ out) {
-  __shared__ double sA0[SEM_MAXN * SEM_MAXN], sA1[SEM_MAXN * SEM_MAXN];
-  __shared__ double tile[SEM_MAXN * SEM_MAXN];
+  __shared__ double sA0[MAXN * MAXN], sA1[MAXN * MAXN];
+  __shared__ double tile[MAXN * MAXN];
   const int nn = n * n;
   for (int i = threadIdx.x; i < nn; i += blockDim.x) {
     const int r = i / n, c = i - r * n;
@@ -817,6 +257,8 @@ inline int grid_for(int64_t n, int per_block = BLOCK, int cap = 8192) {
 // ---------------------------------------------------------------------------
 // context
 // ---------------------------------------------------------------------------
+constexpr int MAX_COLOURS = 8;  // + one trailing all-atomic class
+
 struct sem_ctx {
   int p = 0, n = 0, dpn = 1, device = 0;
   int64_t n_elem = 0, n_node = 0;
@@ -828,11 +270,14 @@ struct sem_ctx {
   double* d_D = nullptr;
   double* d_w = nullptr;
   double* d_Vinv = nullptr;
-  uint32_t* d_mapP = nullptr;
+  uint32_t* d_mapP = nullptr;   // packed coded map, launch (colour) order
+  int* d_gpos = nullptr;         // natural group -> packed position
   const uint32_t* d_e2n = nullptr;
-  uint32_t* d_zero = nullptr;  // nodes whose y entries are not fully overwritten
+  uint32_t* d_zero = nullptr;    // y entries no kernel stores first (unreferenced / first-atomic)
   int64_t n_zero = 0;
-  bool interior_unique = true;
+  std::vector<int64_t> colour_start;  // packed group ranges, one launch each
+  int64_t n_atomic_groups = 0;
+  bool conforming = true;
   double* d_GP[2] = {nullptr, nullptr};
   // CG scratch
   double* d_cg = nullptr;
@@ -867,21 +312,17 @@ DMat<N> make_dmat(const double* h) {
 template <int N>
 int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc, hipStream_t st) {
   const DMat<N> D = make_dmat<N>(c->hD);
-  const int grid = (int)((c->n_groups + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
-  if (op_kind == SEM_OP_POISSON) {
-    if (c->interior_unique)
-      hipLaunchKernelGGL((k_poisson_apply<N, false>), dim3(grid), dim3(BLOCK), 0, st, c->d_mapP,
-                         c->d_GP[0], u, y, c->n_groups, c->n_elem, acc, D);
+  const size_t nc = c->colour_start.size() - 1;
+  for (size_t k = 0; k < nc; ++k) {
+    const int64_t g0 = c->colour_start[k], g1 = c->colour_start[k + 1];
+    if (g1 <= g0) continue;
+    const int grid = (int)((g1 - g0 + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    if (op_kind == SEM_OP_POISSON)
+      hipLaunchKernelGGL((k_poisson_apply<N>), dim3(grid), dim3(BLOCK), 0, st, c->d_mapP,
+                         c->d_GP[0], u, y, g0, g1, acc, D);
     else
-      hipLaunchKernelGGL((k_poisson_apply<N, true>), dim3(grid), dim3(BLOCK), 0, st, c->d_mapP,
-                         c->d_GP[0], u, y, c->n_groups, c->n_elem, acc, D);
-  } else {
-    if (c->interior_unique)
-      hipLaunchKernelGGL((k_axisym_apply<N, false>), dim3(grid), dim3(BLOCK), 0, st, c->d_mapP,
-                         c->d_GP[1], u, y, c->n_groups, c->n_elem, acc, D);
-    else
-      hipLaunchKernelGGL((k_axisym_apply<N, true>), dim3(grid), dim3(BLOCK), 0, st, c->d_mapP,
-                         c->d_GP[1], u, y, c->n_groups, c->n_elem, acc, D);
+      hipLaunchKernelGGL((k_axisym_apply<N>), dim3(grid), dim3(BLOCK), 0, st, c->d_mapP,
+                         c->d_GP[1], u, y, g0, g1, acc, D);
   }
   return SEM_OK;
 }
@@ -892,29 +333,29 @@ void launch_geom_n(sem_ctx* c, const double* nodes, int op_kind, double* GP, dou
   using Sh = GeomShape<N>;
   const int grid = (int)((c->n_elem + Sh::EPB - 1) / Sh::EPB);
   hipLaunchKernelGGL((k_geometry<N>), dim3(grid), dim3(Sh::THREADS), 0, st, nodes, c->n_node,
-                     c->d_e2n, c->n_elem, c->d_Vinv, c->d_D, c->d_w, op_kind, GP, xph, J, iJ, dJ,
-                     dJW, c->d_bad);
+                     c->d_e2n, c->n_elem, c->d_Vinv, c->d_D, c->d_w, op_kind, c->d_gpos, GP, xph,
+                     J, iJ, dJ, dJW, c->d_bad);
 }
 
-#define SEM_DISPATCH_N(n, FN, ...)                          \
-  switch (n) {                                              \
-    case 2: FN<2>(__VA_ARGS__); break;                      \
-    case 3: FN<3>(__VA_ARGS__); break;                      \
-    case 4: FN<4>(__VA_ARGS__); break;                      \
-    case 5: FN<5>(__VA_ARGS__); break;                      \
-    case 6: FN<6>(__VA_ARGS__); break;                      \
-    case 7: FN<7>(__VA_ARGS__); break;                      \
-    case 8: FN<8>(__VA_ARGS__); break;                      \
-    case 9: FN<9>(__VA_ARGS__); break;                      \
-    case 10: FN<10>(__VA_ARGS__); break;                    \
-    case 11: FN<11>(__VA_ARGS__); break;                    \
-    case 12: FN<12>(__VA_ARGS__); break;                    \
-    case 13: FN<13>(__VA_ARGS__); break;                    \
-    case 14: FN<14>(__VA_ARGS__); break;                    \
-    case 15: FN<15>(__VA_ARGS__); break;                    \
-    case 16: FN<16>(__VA_ARGS__); break;                    \
-    case 17: FN<17>(__VA_ARGS__); break;                    \
-    default: break;                                         \
+#define SEM_DISPATCH_N(n, FN, ...)       \
+  switch (n) {                           \
+    case 2: FN<2>(__VA_ARGS__); break;   \
+    case 3: FN<3>(__VA_ARGS__); break;   \
+    case 4: FN<4>(__VA_ARGS__); break;   \
+    case 5: FN<5>(__VA_ARGS__); break;   \
+    case 6: FN<6>(__VA_ARGS__); break;   \
+    case 7: FN<7>(__VA_ARGS__); break;   \
+    case 8: FN<8>(__VA_ARGS__); break;   \
+    case 9: FN<9>(__VA_ARGS__); break;   \
+    case 10: FN<10>(__VA_ARGS__); break; \
+    case 11: FN<11>(__VA_ARGS__); break; \
+    case 12: FN<12>(__VA_ARGS__); break; \
+    case 13: FN<13>(__VA_ARGS__); break; \
+    case 14: FN<14>(__VA_ARGS__); break; \
+    case 15: FN<15>(__VA_ARGS__); break; \
+    case 16: FN<16>(__VA_ARGS__); break; \
+    case 17: FN<17>(__VA_ARGS__); break; \
+    default: break;                      \
   }
 
 int check_op(sem_ctx* c, int op_kind) {
@@ -941,6 +382,173 @@ int ensure_gp(sem_ctx* c, int op_kind) {
   return SEM_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Setup planner (host, once per map).
+//   1. groups = EPW consecutive elements (one wavefront each);
+//   2. greedy colouring of groups so that groups of one colour share no node
+//      (per-node colour bitmask; groups needing > MAX_COLOURS colours, and
+//      every group of a non-conforming mesh, go to a final atomic class);
+//   3. launch order = colour-major; gpos[g] = packed position of group g;
+//   4. write codes in launch order: first writer of a node -> STORE, later
+//      writers -> RMW, the duplicate of a node shared by the elements on two
+//      neighbouring lanes of one group (same row, lanes L and L+1) -> SKIP with
+//      MERGE on lane L; any other in-group duplicate turns the group atomic;
+//   5. zero list = unreferenced nodes + nodes whose first writer is atomic.
+// ---------------------------------------------------------------------------
+struct Plan {
+  std::vector<uint32_t> mapP;
+  std::vector<int> gpos;
+  std::vector<int64_t> colour_start;
+  std::vector<uint32_t> zero;
+  int64_t n_atomic_groups = 0;
+  bool conforming = true;
+};
+
+int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node, int n, Plan& P) {
+  const int epw = WAVE / n, lw = epw * n, nn = n * n;
+  const int64_t n_groups = (n_elem + epw - 1) / epw;
+  auto is_bnd = [n](int r, int jj) { return r == 0 || r == n - 1 || jj == 0 || jj == n - 1; };
+  // references and conformity (interior local nodes must be unique)
+  std::vector<uint32_t> cnt(n_node, 0);
+  for (int64_t t = 0; t < n_elem * nn; ++t) {
+    if (e2n[t] >= n_node) return fail(SEM_E_INVALID, "element map references node >= n_node");
+    cnt[e2n[t]]++;
+  }
+  bool conforming = true;
+  for (int64_t e = 0; e < n_elem && conforming; ++e)
+    for (int r = 1; r < n - 1 && conforming; ++r)
+      for (int jj = 1; jj < n - 1; ++jj)
+        if (cnt[e2n[e * nn + r * n + jj]] != 1) {
+          conforming = false;
+          break;
+        }
+  P.conforming = conforming;
+  auto shared_local = [&](int r, int jj) { return !conforming || is_bnd(r, jj); };
+  // colouring
+  std::vector<uint8_t> cmask(n_node, 0);
+  std::vector<int> colour(n_groups);
+  for (int64_t g = 0; g < n_groups; ++g) {
+    int c = MAX_COLOURS;
+    if (conforming) {
+      uint32_t forb = 0;
+      for (int k = 0; k < epw; ++k) {
+        const int64_t e = g * epw + k;
+        if (e >= n_elem) break;
+        for (int r = 0; r < n; ++r)
+          for (int jj = 0; jj < n; ++jj)
+            if (is_bnd(r, jj)) forb |= cmask[e2n[e * nn + r * n + jj]];
+      }
+      for (int q = 0; q < MAX_COLOURS; ++q)
+        if (!(forb & (1u << q))) {
+          c = q;
+          break;
+        }
+      if (c < MAX_COLOURS)
+        for (int k = 0; k < epw; ++k) {
+          const int64_t e = g * epw + k;
+          if (e >= n_elem) break;
+          for (int r = 0; r < n; ++r)
+            for (int jj = 0; jj < n; ++jj)
+              if (is_bnd(r, jj)) cmask[e2n[e * nn + r * n + jj]] |= (uint8_t)(1u << c);
+        }
+    }
+    colour[g] = c;
+  }
+  std::vector<uint8_t>().swap(cmask);
+  // launch order
+  std::vector<int64_t> count(MAX_COLOURS + 2, 0);
+  for (int64_t g = 0; g < n_groups; ++g) count[colour[g] + 1]++;
+  P.colour_start.assign(MAX_COLOURS + 2, 0);
+  for (int q = 0; q <= MAX_COLOURS; ++q) P.colour_start[q + 1] = P.colour_start[q] + count[q + 1];
+  std::vector<int64_t> order(n_groups);
+  {
+    std::vector<int64_t> fill(P.colour_start.begin(), P.colour_start.end() - 1);
+    P.gpos.assign(n_groups, 0);
+    for (int64_t g = 0; g < n_groups; ++g) {
+      const int64_t q = fill[colour[g]]++;
+      order[q] = g;
+      P.gpos[g] = (int)q;
+    }
+  }
+  // write codes
+  P.mapP.assign((size_t)n_groups * n * lw, 0u);
+  std::vector<uint8_t> written(n_node, 0);
+  std::vector<int> lastg(n_node, -1);
+  std::vector<int> lastpos(n_node, -1);
+  std::vector<int> dup_of(n * lw);
+  P.n_atomic_groups = 0;
+  for (int64_t q = 0; q < n_groups; ++q) {
+    const int64_t g = order[q];
+    uint32_t* out = P.mapP.data() + q * (int64_t)n * lw;
+    bool atomic_group = colour[g] >= MAX_COLOURS;
+    // pass 1: in-group duplicates; only the (row r, lanes L, L+1) pattern merges
+    if (!atomic_group) {
+      for (int r = 0; r < n && !atomic_group; ++r)
+        for (int lane = 0; lane < lw; ++lane) {
+          const int pos = r * lw + lane;
+          dup_of[pos] = -1;
+          const int k = lane / n, jj = lane - k * n;
+          const int64_t e = g * epw + k;
+          if (e >= n_elem) continue;
+          const uint32_t gid = e2n[e * nn + r * n + jj];
+          if (lastg[gid] == (int)g) {
+            const int prev = lastpos[gid];
+            if (prev == pos - 1 && jj == 0 && (prev % lw) % n == n - 1 && dup_of[prev] < 0) {
+              dup_of[pos] = prev;
+            } else {
+              atomic_group = true;
+              break;
+            }
+          }
+          lastg[gid] = (int)g;
+          lastpos[gid] = pos;
+        }
+      // reset stamps so pass 2 and later groups are unaffected
+      for (int k = 0; k < epw; ++k) {
+        const int64_t e = g * epw + k;
+        if (e >= n_elem) break;
+        for (int t = 0; t < nn; ++t) lastg[e2n[e * nn + t]] = -1;
+      }
+    }
+    if (atomic_group) P.n_atomic_groups++;
+    // pass 2: codes
+    for (int r = 0; r < n; ++r)
+      for (int lane = 0; lane < lw; ++lane) {
+        const int pos = r * lw + lane;
+        const int k = lane / n, jj = lane - k * n;
+        const int64_t e = g * epw + k;
+        if (e >= n_elem) {
+          out[pos] = W_SKIP << CODE_SHIFT;
+          continue;
+        }
+        const uint32_t gid = e2n[e * nn + r * n + jj];
+        uint32_t code;
+        if (!shared_local(r, jj)) {
+          code = W_STORE;  // conforming interior node: sole writer
+        } else if (atomic_group) {
+          code = W_ATOMIC;
+          if (!written[gid]) {
+            P.zero.push_back(gid);
+            written[gid] = 1;
+          }
+        } else if (dup_of[pos] >= 0) {
+          code = W_SKIP;
+          out[dup_of[pos]] |= W_MERGE << CODE_SHIFT;
+        } else if (written[gid]) {
+          code = W_RMW;
+        } else {
+          code = W_STORE;
+          written[gid] = 1;
+        }
+        out[pos] = gid | (code << CODE_SHIFT);
+      }
+  }
+  for (int64_t i = 0; i < n_node; ++i)
+    if (cnt[i] == 0) P.zero.push_back((uint32_t)i);
+  std::sort(P.zero.begin(), P.zero.end());
+  return SEM_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -954,7 +562,8 @@ int sem_ctx_create(sem_ctx** out, int p, int64_t n_elem, int64_t n_node, int dpn
                                    std::to_string(SEM_MAX_ORDER));
   if (n_elem < 1 || n_node < 1 || dpn < 1 || dpn > 2)
     return fail(SEM_E_INVALID, "bad sizes (n_elem, n_node >= 1, dpn in {1,2})");
-  if (n_node > 0xFFFFFFFFll) return fail(SEM_E_INVALID, "n_node exceeds uint32 map range");
+  if (n_node > (int64_t)GID_MASK)
+    return fail(SEM_E_INVALID, "n_node exceeds the per-GPU limit of 2^29 - 1 nodes");
   DeviceGuard g(device);
   sem_ctx* c = new sem_ctx();
   c->p = p;
@@ -966,6 +575,10 @@ int sem_ctx_create(sem_ctx** out, int p, int64_t n_elem, int64_t n_node, int dpn
   c->epw = epw_of(c->n);
   c->lw = c->epw * c->n;
   c->n_groups = (n_elem + c->epw - 1) / c->epw;
+  if (c->n_groups > 0x7FFFFFFFll) {
+    delete c;
+    return fail(SEM_E_INVALID, "too many elements");
+  }
   hipError_t e1 = hipMalloc(&c->d_D, SEM_MAXN * SEM_MAXN * sizeof(double));
   hipError_t e2 = hipMalloc(&c->d_w, SEM_MAXN * sizeof(double));
   hipError_t e3 = hipMalloc(&c->d_Vinv, SEM_MAXN * SEM_MAXN * sizeof(double));
@@ -986,6 +599,7 @@ void sem_ctx_destroy(sem_ctx* c) {
   (void)hipFree(c->d_w);
   (void)hipFree(c->d_Vinv);
   (void)hipFree(c->d_mapP);
+  (void)hipFree(c->d_gpos);
   (void)hipFree(c->d_zero);
   (void)hipFree(c->d_GP[0]);
   (void)hipFree(c->d_GP[1]);
@@ -1012,57 +626,49 @@ int sem_set_map(sem_ctx* c, const uint32_t* d_e2n, void* stream) {
   DeviceGuard g(c->device);
   hipStream_t st = S(stream);
   const int n = c->n;
-  c->d_e2n = d_e2n;
-  if (!c->d_mapP) HIP_TRY(hipMalloc(&c->d_mapP, (size_t)c->n_groups * n * c->lw * sizeof(uint32_t)));
-  hipLaunchKernelGGL(k_pack_map, dim3(grid_for(c->n_groups * n * c->lw)), dim3(BLOCK), 0, st,
-                     d_e2n, c->n_elem, n, c->epw, c->n_groups, c->d_mapP);
-  HIP_TRY(hipGetLastError());
-  // node classification: which y entries are not overwritten by a unique
-  // interior store (element-boundary nodes and unreferenced nodes).
-  unsigned* d_cnt = nullptr;
-  unsigned char* d_bnd = nullptr;
-  unsigned* d_oob = nullptr;
-  HIP_TRY(hipMalloc(&d_cnt, c->n_node * sizeof(unsigned)));
-  HIP_TRY(hipMalloc(&d_bnd, c->n_node));
-  HIP_TRY(hipMalloc(&d_oob, sizeof(unsigned)));
-  HIP_TRY(hipMemsetAsync(d_cnt, 0, c->n_node * sizeof(unsigned), st));
-  HIP_TRY(hipMemsetAsync(d_bnd, 0, c->n_node, st));
-  HIP_TRY(hipMemsetAsync(d_oob, 0, sizeof(unsigned), st));
-  hipLaunchKernelGGL(k_node_refs, dim3(grid_for(c->n_elem * n * n)), dim3(BLOCK), 0, st, d_e2n,
-                     c->n_elem, n, c->n_node, d_cnt, d_bnd, d_oob);
-  std::vector<unsigned> cnt(c->n_node);
-  std::vector<unsigned char> bnd(c->n_node);
-  unsigned oob = 0;
-  HIP_TRY(hipMemcpyAsync(cnt.data(), d_cnt, c->n_node * sizeof(unsigned), hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipMemcpyAsync(bnd.data(), d_bnd, c->n_node, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipMemcpyAsync(&oob, d_oob, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+  std::vector<uint32_t> h((size_t)c->n_elem * n * n);
+  HIP_TRY(hipMemcpyAsync(h.data(), d_e2n, h.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
-  (void)hipFree(d_cnt);
-  (void)hipFree(d_bnd);
-  (void)hipFree(d_oob);
-  if (oob) return fail(SEM_E_INVALID, "element map references node >= n_node");
-  std::vector<uint32_t> zero;
-  bool unique = true;
-  for (int64_t i = 0; i < c->n_node; ++i) {
-    if (bnd[i] || cnt[i] == 0) {
-      zero.push_back((uint32_t)i);
-    } else if (cnt[i] != 1) {
-      unique = false;  // an element-interior node referenced twice: non-conforming
-    }
-  }
-  c->interior_unique = unique;
-  if (!unique) {
-    // every entry goes through atomics: zero all nodes
-    zero.resize(c->n_node);
-    for (int64_t i = 0; i < c->n_node; ++i) zero[i] = (uint32_t)i;
-  }
+  Plan P;
+  int rc = build_plan(h, c->n_elem, c->n_node, n, P);
+  if (rc) return rc;
+  std::vector<uint32_t>().swap(h);
+  c->d_e2n = d_e2n;
+  (void)hipFree(c->d_mapP);
+  (void)hipFree(c->d_gpos);
   (void)hipFree(c->d_zero);
+  c->d_mapP = nullptr;
+  c->d_gpos = nullptr;
   c->d_zero = nullptr;
-  c->n_zero = (int64_t)zero.size();
+  HIP_TRY(hipMalloc(&c->d_mapP, P.mapP.size() * sizeof(uint32_t)));
+  HIP_TRY(hipMemcpy(c->d_mapP, P.mapP.data(), P.mapP.size() * sizeof(uint32_t),
+                    hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&c->d_gpos, P.gpos.size() * sizeof(int)));
+  HIP_TRY(hipMemcpy(c->d_gpos, P.gpos.data(), P.gpos.size() * sizeof(int), hipMemcpyHostToDevice));
+  c->n_zero = (int64_t)P.zero.size();
   if (c->n_zero) {
-    HIP_TRY(hipMalloc(&c->d_zero, zero.size() * sizeof(uint32_t)));
-    HIP_TRY(hipMemcpy(c->d_zero, zero.data(), zero.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&c->d_zero, P.zero.size() * sizeof(uint32_t)));
+    HIP_TRY(hipMemcpy(c->d_zero, P.zero.data(), P.zero.size() * sizeof(uint32_t),
+                      hipMemcpyHostToDevice));
   }
+  c->colour_start = P.colour_start;
+  c->n_atomic_groups = P.n_atomic_groups;
+  c->conforming = P.conforming;
+  // geometry factors were packed for the previous order
+  (void)hipFree(c->d_GP[0]);
+  (void)hipFree(c->d_GP[1]);
+  c->d_GP[0] = c->d_GP[1] = nullptr;
+  return SEM_OK;
+}
+
+int sem_plan_info(sem_ctx* c, int64_t* info, int n_info) {
+  if (!c || !info || n_info < 1) return fail(SEM_E_INVALID, "bad arguments");
+  const int64_t nc = c->colour_start.empty() ? 0 : (int64_t)c->colour_start.size() - 1;
+  int64_t vals[6 + MAX_COLOURS + 1] = {c->n_groups, c->n_zero, c->n_atomic_groups,
+                                       c->conforming ? 1 : 0, c->epw, nc};
+  for (int64_t q = 0; q < nc && q <= MAX_COLOURS; ++q)
+    vals[6 + q] = c->colour_start[q + 1] - c->colour_start[q];
+  for (int i = 0; i < n_info && i < 6 + MAX_COLOURS + 1; ++i) info[i] = vals[i];
   return SEM_OK;
 }
 
@@ -1113,13 +719,14 @@ int sem_geom_fields(sem_ctx* c, const double* d_nodes, const double* h_Vinv, dou
 
 int sem_set_geom(sem_ctx* c, const double* d_G, int op_kind, void* stream) {
   if (!c || !d_G) return fail(SEM_E_INVALID, "null argument");
+  if (!c->d_gpos) return fail(SEM_E_STATE, "sem_set_map must precede sem_set_geom");
   DeviceGuard g(c->device);
   int rc;
   if ((rc = check_op(c, op_kind))) return rc;
   if ((rc = ensure_gp(c, op_kind))) return rc;
   const int ncomp = sem_op_ncomp(op_kind);
   hipLaunchKernelGGL(k_pack_geom, dim3(grid_for(c->n_elem * ncomp * c->n * c->n)), dim3(BLOCK), 0,
-                     S(stream), d_G, c->n_elem, c->n, ncomp, c->epw,
+                     S(stream), d_G, c->n_elem, c->n, ncomp, c->epw, c->d_gpos,
                      c->d_GP[op_kind == SEM_OP_POISSON ? 0 : 1]);
   HIP_TRY(hipGetLastError());
   return SEM_OK;
@@ -1174,7 +781,7 @@ int sem_diag(sem_ctx* c, int op_kind, double* d_diag, void* stream) {
   hipStream_t st = S(stream);
   HIP_TRY(hipMemsetAsync(d_diag, 0, c->n_node * sizeof(double), st));
   hipLaunchKernelGGL(k_poisson_diag, dim3(grid_for(c->n_elem * c->n * c->n)), dim3(BLOCK), 0, st,
-                     c->d_mapP, c->d_GP[0], c->d_D, c->n, c->epw, c->n_elem, d_diag);
+                     c->d_mapP, c->d_GP[0], c->d_gpos, c->d_D, c->n, c->epw, c->n_elem, d_diag);
   HIP_TRY(hipGetLastError());
   return SEM_OK;
 }
@@ -1232,76 +839,71 @@ int sem_pcg_solve(sem_ctx* c, int op_kind, const double* b, double* x, const uin
   const int64_t n = c->n_node;
   if (c->cg_len != n) {
     (void)hipFree(c->d_cg);
-    HIP_TRY(hipMalloc(&c->d_cg, 4 * n * sizeof(double)));
+    c->d_cg = nullptr;
+    c->cg_len = 0;
+    HIP_TRY(hipMalloc(&c->d_cg, 5 * n * sizeof(double)));
     c->cg_len = n;
   }
   double* r = c->d_cg;
   double* z = r + n;
   double* p = z + n;
   double* q = p + n;
-  // Jacobi diagonal (allocated per solve; setup cost)
-  double* d_diag = nullptr;
-  HIP_TRY(hipMalloc(&d_diag, n * sizeof(double)));
+  double* d_diag = q + n;
   int rc = sem_diag(c, op_kind, d_diag, stream);
-  if (rc) {
-    (void)hipFree(d_diag);
-    return rc;
-  }
+  if (rc) return rc;
   double* partial = c->d_red;
   double* scal = c->d_red + 2 * RED_BLOCKS;  // [alpha, beta, dot0, dot1]
   const int gb = grid_for(n, BLOCK, RED_BLOCKS);
-  auto dot2 = [&](const double* a1, const double* b1, const double* a2, const double* b2,
-                  double* out2) -> int {
+  double h[2];
+  auto dot2 = [&](const double* a1, const double* b1, const double* a2, const double* b2) -> int {
     hipLaunchKernelGGL(k_dot2, dim3(gb), dim3(BLOCK), 0, st, a1, b1, a2, b2, n, partial);
     hipLaunchKernelGGL(k_finish2, dim3(1), dim3(BLOCK), 0, st, partial, gb, scal + 2);
-    HIP_TRY(hipMemcpyAsync(out2, scal + 2, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(h, scal + 2, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     return SEM_OK;
   };
   // r = b - K x on free rows
-  if ((rc = sem_apply(c, op_kind, x, r, 0, stream))) goto done;
+  if ((rc = sem_apply(c, op_kind, x, r, 0, stream))) return rc;
   hipLaunchKernelGGL(k_residual, dim3(grid_for(n)), dim3(BLOCK), 0, st, b, r, mask, n);
   hipLaunchKernelGGL(k_precond, dim3(grid_for(n)), dim3(BLOCK), 0, st, r, d_diag, mask, n, z);
   HIP_TRY(hipMemcpyAsync(p, z, n * sizeof(double), hipMemcpyDeviceToDevice, st));
-  {
-    double h[2];
-    if ((rc = dot2(r, z, r, r, h))) goto done;
-    double rz = h[0];
-    const double r0 = std::sqrt(h[1]);
-    double res = r0;
-    int it = 0;
-    if (r0 == 0.0) {
-      if (iters) *iters = 0;
-      if (relres) *relres = 0.0;
-      goto done;
-    }
-    while (it < max_iter && res > rtol * r0) {
-      if ((rc = sem_apply(c, op_kind, p, q, 0, stream))) goto done;
-      hipLaunchKernelGGL(k_mask, dim3(grid_for(n)), dim3(BLOCK), 0, st, q, mask, n);
-      if ((rc = dot2(p, q, nullptr, nullptr, h))) goto done;
-      const double alpha = rz / h[0];
-      double hs[2] = {alpha, 0.0};
-      HIP_TRY(hipMemcpyAsync(scal, hs, 2 * sizeof(double), hipMemcpyHostToDevice, st));
-      hipLaunchKernelGGL(k_update_xr, dim3(grid_for(n)), dim3(BLOCK), 0, st, x, r, p, q, scal, n);
-      hipLaunchKernelGGL(k_precond, dim3(grid_for(n)), dim3(BLOCK), 0, st, r, d_diag, mask, n, z);
-      if ((rc = dot2(r, z, r, r, h))) goto done;
-      const double beta = h[0] / rz;
-      rz = h[0];
-      res = std::sqrt(h[1]);
-      hs[0] = alpha;
-      hs[1] = beta;
-      HIP_TRY(hipMemcpyAsync(scal, hs, 2 * sizeof(double), hipMemcpyHostToDevice, st));
-      hipLaunchKernelGGL(k_update_p, dim3(grid_for(n)), dim3(BLOCK), 0, st, p, z, scal, n);
-      ++it;
-    }
-    HIP_TRY(hipStreamSynchronize(st));
-    if (iters) *iters = it;
-    if (relres) *relres = res / r0;
-    if (res > rtol * r0) rc = fail(SEM_E_INVALID, "PCG did not converge");
+  if ((rc = dot2(r, z, r, r))) return rc;
+  double rz = h[0];
+  const double r0 = std::sqrt(h[1]);
+  double res = r0;
+  int it = 0;
+  if (r0 == 0.0) {
+    if (iters) *iters = 0;
+    if (relres) *relres = 0.0;
+    return SEM_OK;
   }
-done:
-  (void)hipFree(d_diag);
-  return rc;
+  double hs[2];
+  while (it < max_iter && res > rtol * r0) {
+    if ((rc = sem_apply(c, op_kind, p, q, 0, stream))) return rc;
+    hipLaunchKernelGGL(k_mask, dim3(grid_for(n)), dim3(BLOCK), 0, st, q, mask, n);
+    if ((rc = dot2(p, q, nullptr, nullptr))) return rc;
+    const double alpha = rz / h[0];
+    hs[0] = alpha;
+    hs[1] = 0.0;
+    HIP_TRY(hipMemcpyAsync(scal, hs, 2 * sizeof(double), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_update_xr, dim3(grid_for(n)), dim3(BLOCK), 0, st, x, r, p, q, scal, n);
+    hipLaunchKernelGGL(k_precond, dim3(grid_for(n)), dim3(BLOCK), 0, st, r, d_diag, mask, n, z);
+    if ((rc = dot2(r, z, r, r))) return rc;
+    const double beta = h[0] / rz;
+    rz = h[0];
+    res = std::sqrt(h[1]);
+    hs[0] = alpha;
+    hs[1] = beta;
+    HIP_TRY(hipMemcpyAsync(scal, hs, 2 * sizeof(double), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_update_p, dim3(grid_for(n)), dim3(BLOCK), 0, st, p, z, scal, n);
+    HIP_TRY(hipStreamSynchronize(st));  // hs is reused by the next iteration's copy
+    ++it;
+  }
+  HIP_TRY(hipStreamSynchronize(st));
+  if (iters) *iters = it;
+  if (relres) *relres = res / r0;
+  if (res > rtol * r0) return fail(SEM_E_INVALID, "PCG did not converge");
+  return SEM_OK;
 }
 
 }  // extern "C"

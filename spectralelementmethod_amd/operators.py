@@ -139,6 +139,15 @@ class SEMOperator(object):
     def _stream(self, stream):
         return _lib.stream_ptr(stream)
 
+    def plan_info(self):
+        """Setup plan of the scatter (see include/sem_hip.h sem_plan_info)."""
+        info = (C.c_int64 * 15)()
+        _lib.check(self._lib.sem_plan_info(self._ctx, info, 15))
+        v = list(info)
+        return dict(groups=v[0], zero_list=v[1], atomic_groups=v[2], conforming=bool(v[3]),
+                    elements_per_group=v[4], colours=v[5],
+                    groups_per_colour=[x for x in v[6:6 + v[5]]])
+
     # ------------------------------------------------------------------
     def compute_geometry(self, kind=POISSON, stream=None):
         """Per-node geometric factors for ``kind`` from the mesh nodes
