@@ -408,15 +408,57 @@ def gen_axisym():
     print("axisym_action.npz")
 
 
-def main():
+def gen_geometry():
+    """Node orderings of sem/geometry.py (NCube hierarchical order :197-212,
+    exterior/interior sets) and the DOFManagerSC condensation permutation
+    (sem/discrete.py:314-359) on a small mesh."""
+    from sem.geometry import Quadrilateral
+    from sem.discrete import DOFManagerSC, DOFManager
+    out = {}
+    for shp in [(2, 2), (3, 3), (5, 5), (9, 9), (17, 17), (5, 6), (4, 7)]:
+        q = Quadrilateral(*shp)
+        key = "%dx%d" % shp
+        out["hier_" + key] = q.hierarchical_node_order
+        out["next_" + key] = np.array(q.n_exterior_nodes)
+        out["nsub_" + key] = np.array([q.n_sub_geometries(d) for d in range(3)])
+    nodes, e2n = structured_square(3, 2, 4, 0.0)
+    for rcm in (False, True):
+        mesh = ref_mesh(nodes, e2n)
+        _, tb = ref_basis(4)
+        dm = DOFManagerSC(mesh, 1, tb, rcm_order=rcm)
+        out["sc_nodes_rcm%d" % rcm] = mesh.nodes.copy()
+        out["sc_e2n_rcm%d" % rcm] = mesh_map(mesh)
+        out["sc_next_rcm%d" % rcm] = np.array(dm.ndof_exterior)
+        fe = next(dm.finite_elements())
+        out["sc_gdof_hier_rcm%d" % rcm] = np.stack(
+            [f.global_dof_ind_hier for f in dm.finite_elements()])
+        out["sc_ldof_hier_rcm%d" % rcm] = fe.loc_dof_ind_hier
+    mesh = ref_mesh(nodes, e2n)
+    _, tb = ref_basis(4)
+    DOFManager(mesh, 1, tb, rcm_order=True)
+    out["rcm_nodes"] = mesh.nodes.copy()
+    out["rcm_e2n"] = mesh_map(mesh)
+    np.savez_compressed(os.path.join(OUT, "geometry.npz"), **out)
+    print("geometry.npz")
+
+
+GENERATORS = {"gll": gen_gll, "tensor_ops": gen_tensor_ops, "poisson_action": gen_poisson_action,
+              "poisson_solution": gen_poisson_solution, "axisym": gen_axisym,
+              "geometry": gen_geometry}
+
+
+def main(names=None):
     _TABLES.update(decode_basis_hdf5())
     install_runtime_shims()
-    gen_gll()
-    gen_tensor_ops()
-    gen_poisson_action()
-    gen_poisson_solution()
-    gen_axisym()
+    for name in (names or list(GENERATORS)):
+        if name != "gll" and len(_TABLES) < 16:
+            # extended-order tables are needed by every generator
+            import sem.basis_data as bd
+            for p in range(11, MAX_ORDER_EXT + 1):
+                nodes, bary, qw = bd.gauss_legendre_lobatto(p + 1)
+                _TABLES[p] = np.array([[float(v) for v in mat] for mat in (nodes, bary, qw)])
+        GENERATORS[name]()
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:] or None)

@@ -1,0 +1,109 @@
+"""GPU tests of the reference-shaped facade (spectralelementmethod_amd.discrete):
+the reference's own call pattern -- build a Mesh, a DOFManager with its
+default RCM numbering, iterate finite_elements(x_phys=True, Jacobian=True),
+apply the stiffness operator, solve the assembled Poisson problem -- against
+goldens produced by running the reference."""
+import numpy as np
+import pytest
+
+from conftest import rel_l2
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def _mesh(p, nex, ney, warp):
+    from spectralelementmethod_amd import meshgen
+    from spectralelementmethod_amd.discrete import Mesh
+    nodes, e2n = meshgen.structured_square(nex, ney, p, warp)
+    return Mesh.from_arrays(nodes, e2n)
+
+
+def test_dofmanager_rcm_stiffness_action(poisson_action):
+    """DOFManager(mesh, 1, basis) with the default RCM order reproduces the
+    reference numbering, and stiffness_action matches its action."""
+    from spectralelementmethod_amd.basis_functions import gll_basis_2d
+    from spectralelementmethod_amd.discrete import DOFManager
+    name = "p8_8x8w_rcm"
+    mesh = _mesh(8, 8, 8, 0.05)
+    dm = DOFManager(mesh, 1, gll_basis_2d(8))
+    assert np.array_equal(mesh.element_map(), poisson_action[name + "_e2n"])
+    y = dm.stiffness_action(poisson_action[name + "_u"])
+    assert rel_l2(y, poisson_action[name + "_y"]) < 1e-12
+
+
+def test_finite_element_fields(poisson_action):
+    from spectralelementmethod_amd.basis_functions import gll_basis_2d
+    from spectralelementmethod_amd.discrete import DOFManager
+    name = "p8_8x8w"
+    dm = DOFManager(_mesh(8, 8, 8, 0.05), 1, gll_basis_2d(8), rcm_order=False)
+    fes = list(dm.finite_elements(x_phys=True, Jacobian=True))
+    for key, attr in (("x_phys", "x_phys"), ("J", "J"), ("invJ", "invJ"), ("detJxW", "detJxW")):
+        got = np.stack([getattr(fe, attr) for fe in fes])
+        assert rel_l2(got, poisson_action[name + "_geom_" + key]) < 1e-12, key
+    got = np.stack([fe.mapping.detJ for fe in fes])
+    assert rel_l2(got, poisson_action[name + "_geom_detJ"]) < 1e-12
+    # FiniteElement.integrate of 1 sums to the area of the square
+    assert abs(sum(fe.integrate(np.ones((9, 9))) for fe in fes) - 4.0) < 1e-12
+    # physical gradient of x is (1, 0)
+    fe = fes[5]
+    g = fe.gradient(fe.x_phys[0])
+    assert np.abs(g[0] - 1).max() < 1e-10 and np.abs(g[1]).max() < 1e-10
+
+
+def test_dofmanager_sc_solve_poisson(poisson_solution):
+    """DOFManagerSC numbering + matrix-free PCG == the reference's
+    static-condensation solve (sem/discrete.py:502-528), to 1e-10."""
+    from spectralelementmethod_amd.basis_functions import gll_basis_2d
+    from spectralelementmethod_amd.discrete import DOFManagerSC
+    for name, (p, nex, ney, warp) in (("p4_8x8", (4, 8, 8, 0.0)),
+                                      ("p8_4x4w", (8, 4, 4, 0.05))):
+        fx = poisson_solution
+        mesh = _mesh(p, nex, ney, warp)
+        dm = DOFManagerSC(mesh, 1, gll_basis_2d(p))
+        assert np.array_equal(mesh.element_map(), fx[name + "_e2n"])
+        assert dm.ndof_exterior == int(fx[name + "_n_ext"])
+        x, y = mesh.nodes
+        on_ebc = ((np.abs(x + 1) < 1e-12) | (np.abs(y + 1) < 1e-12))
+        dof = np.zeros(dm.ndof)
+        dof[on_ebc] = 0.2 * ((x[on_ebc] + 1) + (y[on_ebc] + 1))
+        dof, its, rel = dm.solve_poisson(fx[name + "_rhs"], dof, on_ebc[:dm.ndof_exterior])
+        assert rel_l2(dof, fx[name + "_soln"]) < 1e-10, (name, its, rel)
+
+
+def test_axisym_operator_action(axisym_action):
+    from spectralelementmethod_amd.basis_functions import gll_basis_2d
+    from spectralelementmethod_amd.discrete import DOFManager, Mesh
+    name = "p6_4x8"
+    mesh = Mesh.from_arrays(axisym_action[name + "_nodes"], axisym_action[name + "_e2n"])
+    dm = DOFManager(mesh, 2, gll_basis_2d(6), rcm_order=False)
+    y = dm.operator_action("axisym_stokes", axisym_action[name + "_soln"])
+    assert rel_l2(y, axisym_action[name + "_block"]) < 1e-12
+
+
+def test_values_at_nodes_and_det_inv():
+    from spectralelementmethod_amd.basis_functions import gll_basis_2d
+    from spectralelementmethod_amd.discrete import DOFManager
+    from spectralelementmethod_amd.linalg import det_inv_2x2
+    dm = DOFManager(_mesh(4, 3, 3, 0.0), 1, gll_basis_2d(4), rcm_order=False)
+    # a bilinear field's GLL coefficients = its values at the GLL points;
+    # at the (equispaced) mesh nodes it must equal x*y there
+    fes = list(dm.finite_elements(x_phys=True))
+    coeffs = np.zeros(dm.ndof)
+    for fe in fes:
+        coeffs[fe.node_ind] = fe.x_phys[0] * fe.x_phys[1]
+    vals = dm.values_at_nodes(coeffs)
+    x, y = dm.mesh.nodes
+    assert np.abs(vals - x * y).max() < 1e-13
+    rng = np.random.default_rng(0)
+    M = rng.standard_normal((2, 2, 40))
+    det, inv = det_inv_2x2(M)
+    ref = np.linalg.inv(np.moveaxis(M, 2, 0))
+    assert np.allclose(np.moveaxis(inv, 2, 0), ref, rtol=1e-12, atol=1e-12)
+    assert np.allclose(det, np.linalg.det(np.moveaxis(M, 2, 0)), rtol=1e-12)
