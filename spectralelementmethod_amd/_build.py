@@ -6,7 +6,7 @@ import subprocess
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_NAME = "libsem_hip.so"
-LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
+LIB_PATH = os.environ.get("SEM_LIB_PATH", os.path.join(PKG_DIR, LIB_NAME))
 SOURCES = ["sem_device.hip", "sem_basis.cpp"]
 DEPS = SOURCES + ["sem_internal.h", "sem_kernels.h", "gll_table.h"]
 ARCH = os.environ.get("SEM_OFFLOAD_ARCH", "gfx950")
@@ -27,17 +27,21 @@ def needs_rebuild():
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force=False, verbose=True):
-    if not force and not needs_rebuild():
+def build(force=False, verbose=True, out=None, defines=()):
+    """Compile the library (``out`` and ``defines`` build diagnostic
+    variants, e.g. for A/B timing in one process)."""
+    out = out or LIB_PATH
+    if not force and out == LIB_PATH and not needs_rebuild():
         return LIB_PATH
     cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-fPIC", "-shared", "-std=c++17",
            "-munsafe-fp-atomics", "-Wall", "-Wno-unused-result",
-           *[os.path.join(CSRC, s) for s in SOURCES], "-o", LIB_PATH + ".tmp"]
+           *["-D" + d for d in defines],
+           *[os.path.join(CSRC, s) for s in SOURCES], "-o", out + ".tmp"]
     if verbose:
         print("[sem build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(LIB_PATH + ".tmp", LIB_PATH)
-    return LIB_PATH
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":

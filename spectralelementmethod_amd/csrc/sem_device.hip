@@ -385,9 +385,10 @@ int ensure_gp(sem_ctx* c, int op_kind) {
 // ---------------------------------------------------------------------------
 // Setup planner (host, once per map).
 //   1. groups = EPW consecutive elements (one wavefront each);
-//   2. greedy colouring of groups so that groups of one colour share no node
-//      (per-node colour bitmask; groups needing > MAX_COLOURS colours, and
-//      every group of a non-conforming mesh, go to a final atomic class);
+//   2. greedy "soft" colouring of groups: groups of one colour share at most
+//      2n nodes pairwise, and those nodes are written atomically (per-node
+//      colour bitmask; groups needing > MAX_COLOURS colours, and every group
+//      of a non-conforming mesh, go to a final all-atomic class);
 //   3. launch order = colour-major; gpos[g] = packed position of group g;
 //   4. write codes in launch order: first writer of a node -> STORE, later
 //      writers -> RMW, the duplicate of a node shared by the elements on two
@@ -424,37 +425,60 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
         }
   P.conforming = conforming;
   auto shared_local = [&](int r, int jj) { return !conforming || is_bnd(r, jj); };
-  // colouring
+  // Soft colouring: a group takes the lowest colour whose earlier groups
+  // share at most `soft` of its boundary nodes; such shared nodes are then
+  // written with atomics by every group (and zeroed first).  On a structured
+  // mesh numbered along columns this gives one colour per column parity, so
+  // every launch writes whole columns (whole cache lines) of y.
+#ifdef SEM_SOFT_COLOUR
+  const int soft = 2 * n;  // measured slower: scattered single-lane atomics
+#else
+  const int soft = 0;
+#endif
   std::vector<uint8_t> cmask(n_node, 0);
+  std::vector<uint8_t> atomic_node(n_node, 0);
   std::vector<int> colour(n_groups);
+  std::vector<int64_t> stamp(n_node, -1);
+  std::vector<uint32_t> gnodes;
   for (int64_t g = 0; g < n_groups; ++g) {
     int c = MAX_COLOURS;
     if (conforming) {
-      uint32_t forb = 0;
+      gnodes.clear();
       for (int k = 0; k < epw; ++k) {
         const int64_t e = g * epw + k;
         if (e >= n_elem) break;
         for (int r = 0; r < n; ++r)
           for (int jj = 0; jj < n; ++jj)
-            if (is_bnd(r, jj)) forb |= cmask[e2n[e * nn + r * n + jj]];
+            if (is_bnd(r, jj)) {
+              const uint32_t gid = e2n[e * nn + r * n + jj];
+              if (stamp[gid] != g) {
+                stamp[gid] = g;
+                gnodes.push_back(gid);
+              }
+            }
       }
+      int shared[MAX_COLOURS] = {0};
+      for (uint32_t gid : gnodes)
+        for (int q = 0; q < MAX_COLOURS; ++q)
+          if (cmask[gid] & (1u << q)) shared[q]++;
       for (int q = 0; q < MAX_COLOURS; ++q)
-        if (!(forb & (1u << q))) {
+        if (shared[q] <= soft) {
           c = q;
           break;
         }
+#ifdef SEM_DIAG_ONE_COLOUR
+      c = 0;  // timing-only diagnostic: racy single launch
+#endif
       if (c < MAX_COLOURS)
-        for (int k = 0; k < epw; ++k) {
-          const int64_t e = g * epw + k;
-          if (e >= n_elem) break;
-          for (int r = 0; r < n; ++r)
-            for (int jj = 0; jj < n; ++jj)
-              if (is_bnd(r, jj)) cmask[e2n[e * nn + r * n + jj]] |= (uint8_t)(1u << c);
+        for (uint32_t gid : gnodes) {
+          if (cmask[gid] & (1u << c)) atomic_node[gid] = 1;
+          cmask[gid] |= (uint8_t)(1u << c);
         }
     }
     colour[g] = c;
   }
   std::vector<uint8_t>().swap(cmask);
+  std::vector<int64_t>().swap(stamp);
   // launch order
   std::vector<int64_t> count(MAX_COLOURS + 2, 0);
   for (int64_t g = 0; g < n_groups; ++g) count[colour[g] + 1]++;
@@ -534,8 +558,18 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
         } else if (dup_of[pos] >= 0) {
           code = W_SKIP;
           out[dup_of[pos]] |= W_MERGE << CODE_SHIFT;
+        } else if (atomic_node[gid]) {
+          code = W_ATOMIC;  // shared by two groups of one colour
+          if (!written[gid]) {
+            P.zero.push_back(gid);
+            written[gid] = 1;
+          }
         } else if (written[gid]) {
+#ifdef SEM_DIAG_RMW_AS_STORE
+          code = W_STORE;  // timing-only diagnostic build: results are wrong
+#else
           code = W_RMW;
+#endif
         } else {
           code = W_STORE;
           written[gid] = 1;

@@ -125,8 +125,15 @@ __device__ __forceinline__ void store_row(double* L, int i, const double (&t)[N]
 // Poisson stiffness action over packed groups [g0, g1)
 //   mapP[g][r][k*N + j] = map[e][r][j] | code,  GP[g][c][r][k*N + j] = G_c(e; r, j)
 // ---------------------------------------------------------------------------
+#ifndef SEM_POISSON_MIN_WAVES
+#define SEM_POISSON_MIN_WAVES 1
+#endif
+#ifndef SEM_PREFETCH_G
+#define SEM_PREFETCH_G 0
+#endif
+
 template <int N>
-__global__ void __launch_bounds__(BLOCK)
+__global__ void __launch_bounds__(BLOCK, SEM_POISSON_MIN_WAVES)
     k_poisson_apply(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
                     const double* __restrict__ u, double* __restrict__ y, int64_t g0, int64_t g1,
                     int accumulate, const DMat<N> D) {
@@ -154,7 +161,20 @@ __global__ void __launch_bounds__(BLOCK)
 #pragma unroll
   for (int r = 0; r < N; ++r) raw[r] = in_wave ? mp[r * LW] : (W_SKIP << CODE_SHIFT);
 #pragma unroll
-  for (int r = 0; r < N; ++r) uc[r] = u[raw[r] & GID_MASK];
+  for (int r = 0; r < N; ++r) {
+#ifdef SEM_DIAG_NO_U
+    uc[r] = (double)(raw[r] & 7u);  // timing-only: no u gather
+#else
+    uc[r] = u[raw[r] & GID_MASK];
+#endif
+  }
+#if SEM_PREFETCH_G
+  double gg[3][N];
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int m = 0; m < N; ++m) gg[c][m] = gp[(c * N + m) * LW];
+#endif
 
   // column j: d0[m][j] = sum_r D[m][r] u[r][j]     (TensorProduct.deriv dim 0)
   double d0[N];
@@ -194,9 +214,15 @@ __global__ void __launch_bounds__(BLOCK)
 #pragma unroll
     for (int m = 0; m < N; ++m) {
       const double d1 = L[m * RS + j];
+#if SEM_PREFETCH_G
+      const double g00 = gg[0][m], g01 = gg[1][m], g11 = gg[2][m];
+#elif defined(SEM_DIAG_NO_G)
+      const double g00 = 1.0 + m, g01 = 0.25 * j, g11 = 2.0;  // timing-only
+#else
       const double g00 = gp[(0 * N + m) * LW];
       const double g01 = gp[(1 * N + m) * LW];
       const double g11 = gp[(2 * N + m) * LW];
+#endif
       w0[m] = fma(g00, d0[m], g01 * d1);
       w1[m] = fma(g01, d0[m], g11 * d1);
     }
@@ -234,7 +260,14 @@ __global__ void __launch_bounds__(BLOCK)
   for (int p = 0; p < N; ++p) {
     const double v = ya[p] + L[p * RS + j];
     const double vn = __shfl_down(v, 1, WAVE);
+#ifdef SEM_DIAG_NO_STORE
+    if (in_wave && v == 1234.5678) y[0] = vn;  // timing-only: keeps v live, never true
+#elif defined(SEM_DIAG_PLAIN_STORE)
+    if (in_wave)  // timing-only: plain store for every lane, codes ignored
+      y[raw[p] & GID_MASK] = ((raw[p] >> CODE_SHIFT) & W_MERGE) ? v + vn : v;
+#else
     if (in_wave) emit1(y, raw[p], v, vn, accumulate);
+#endif
   }
 }
 
