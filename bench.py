@@ -232,7 +232,7 @@ def main():
             "single GPU",
             "kernel_ms_avg": kern_avg_s * 1e3, "kernel_ms_min": float(np.min(kern_ms)),
             "gflops_kernel": F / kern_avg_s / 1e9,
-            "scatter_plan": {k: plan[k] for k in ("colours", "groups_per_colour", "zero_list",
+            "scatter_plan": {k: plan[k] for k in ("colours", "chains_per_colour", "rounds", "zero_list",
                                                   "atomic_groups")},
         },
         "roofline": {

@@ -103,9 +103,11 @@ int sem_set_basis(sem_ctx* ctx, const double* h_D, const double* h_w);
 int sem_set_map(sem_ctx* ctx, const uint32_t* d_e2n, void* stream);
 
 /* Setup plan of the last sem_set_map (diagnostics): info[0] groups (one
- * wavefront of elements each), [1] zero-list length, [2] atomic-fallback
- * groups, [3] mesh conforming (0/1), [4] elements per group, [5] colour
- * classes, [6..] groups per class.  Writes min(n_info, 15) values. */
+ * wavefront of elements each), [1] zero-list length, [2] groups in
+ * atomic-fallback chains, [3] mesh conforming (0/1), [4] elements per group,
+ * [5] colour classes, [6] rounds of 4 groups per chain (one workgroup per
+ * chain), [7] packed group slots, [8..] chains per colour class (one launch
+ * each).  Writes min(n_info, 17) values. */
 int sem_plan_info(sem_ctx* ctx, int64_t* info, int n_info);
 
 /* Geometry from mesh nodes (device, float64 [2][n_node]) for op_kind:

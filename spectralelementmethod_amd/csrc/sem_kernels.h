@@ -11,19 +11,26 @@
 // examples/squirmer-axisymmetric.py:286) to rounding.
 //
 // CDNA4 mapping:
-//  * one wavefront owns a "group" of EPW = floor(64 / n) elements; lane =
-//    (element slot k, line j).  Contractions along the lane's own column/row
-//    run in registers with D as wave-uniform kernel arguments (SGPRs); the two
-//    transposes go through a wave-private LDS tile: no workgroup barrier.
+//  * GROUP = one wavefront's EPW = floor(64 / n) elements; lane = (element
+//    slot k, line j).  Contractions along the lane's own column/row run in
+//    registers with D as wave-uniform kernel arguments (SGPRs); the two
+//    transposes go through a wave-private LDS tile.
+//  * CHAIN = R rounds x 4 consecutive groups, processed by one 256-thread
+//    workgroup (round by round, one group per wavefront).  Consecutive groups
+//    of a chain usually share one column of nodes: the earlier group hands its
+//    partial sums for that column to the later one through LDS ("carry"), so
+//    every node has exactly one writer inside a chain and consecutive y rows
+//    are completed by one workgroup (one XCD's L2), close in time.
+//  * Chains are coloured at setup so that chains of one colour share no node;
+//    one launch per colour.  Every packed map entry carries a 4-bit write code:
+//    plain store for the first writer of a node in launch order,
+//    read-modify-write for later writers, skip + register merge for a node
+//    shared by the elements on two neighbouring lanes, carry-in for the node
+//    handed over by the previous group, atomic only as a fallback.  No
+//    atomics on structured (or any locality-ordered conforming) meshes.
 //  * the map and the geometric factors are repacked at setup into
 //    [group][row][lane] order: every wave-instruction streams one contiguous
 //    run of HBM.
-//  * the scatter needs NO atomics: groups are coloured so that groups of one
-//    colour share no node, one launch per colour; each packed map entry
-//    carries a 3-bit write code computed at setup (plain store for the first
-//    writer of a node in launch order, read-modify-write for later writers,
-//    skip + register merge for the duplicate of the element on the next lane,
-//    atomic only as a fallback for irregular groups).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -33,17 +40,26 @@ namespace semk {
 
 constexpr int WAVE = 64;
 constexpr int BLOCK = 256;
-constexpr int WAVES_PER_BLOCK = BLOCK / WAVE;
+#ifndef SEM_CHAIN_WAVES
+#define SEM_CHAIN_WAVES 4
+#endif
+constexpr int CHAIN_WAVES = SEM_CHAIN_WAVES;  // groups per round = wavefronts per workgroup
+constexpr int CHAIN_BLOCK = CHAIN_WAVES * WAVE;
 constexpr int MAXN = 17;
 
 // packed map entry = gid | code << CODE_SHIFT
-constexpr int CODE_SHIFT = 29;
+constexpr int CODE_SHIFT = 28;
 constexpr uint32_t GID_MASK = (1u << CODE_SHIFT) - 1u;
 constexpr uint32_t W_STORE = 0;   // first writer: y = v   (y += v in accumulate mode)
-constexpr uint32_t W_RMW = 1;     // later writer: y += v (no other writer in this launch)
-constexpr uint32_t W_SKIP = 2;    // value merged into the previous lane / padding
+constexpr uint32_t W_RMW = 1;     // later writer: y += v (no concurrent writer)
+constexpr uint32_t W_SKIP = 2;    // value merged into another lane / padding
 constexpr uint32_t W_ATOMIC = 3;  // fallback
 constexpr uint32_t W_MERGE = 4;   // add the next lane's value before writing
+constexpr uint32_t W_CARRY = 8;   // add the value handed over by the previous group
+
+#ifndef SEM_POISSON_MIN_WAVES
+#define SEM_POISSON_MIN_WAVES 1
+#endif
 
 template <int N>
 struct DMat {
@@ -63,41 +79,36 @@ __device__ __forceinline__ void atomic_add_f64(double* p, double v) {
   unsafeAtomicAdd(p, v);  // global_atomic_add_f64, no return
 }
 
-__device__ __forceinline__ void emit1(double* __restrict__ y, uint32_t raw, double v, double vnext,
+// Read-modify-write targets were written earlier by this workgroup or by an
+// earlier launch: read them past the CU's vector L1 (nt) so a line cached
+// before the workgroup's own store is never reused.
+__device__ __forceinline__ double rmw_load(const double* p) { return __builtin_nontemporal_load(p); }
+
+__device__ __forceinline__ void emit1(double* __restrict__ y, uint32_t raw, double v,
                                       int accumulate) {
-  const uint32_t code = raw >> CODE_SHIFT;
+  const uint32_t a = (raw >> CODE_SHIFT) & 3u;
   double* dst = y + (raw & GID_MASK);
-  if (code & W_MERGE) v += vnext;
-  const uint32_t a = code & 3u;
   if (a == W_STORE) {
-    if (accumulate)
-      *dst += v;
-    else
-      *dst = v;
+    *dst = accumulate ? rmw_load(dst) + v : v;
   } else if (a == W_RMW) {
-    *dst += v;
+    *dst = rmw_load(dst) + v;
   } else if (a == W_ATOMIC) {
     atomic_add_f64(dst, v);
   }
 }
 
 __device__ __forceinline__ void emit2(double* __restrict__ y, uint32_t raw, double v0, double v1,
-                                      double n0, double n1, int accumulate) {
-  const uint32_t code = raw >> CODE_SHIFT;
-  double2* dst = reinterpret_cast<double2*>(y) + (raw & GID_MASK);
-  if (code & W_MERGE) {
-    v0 += n0;
-    v1 += n1;
-  }
-  const uint32_t a = code & 3u;
-  if (a == W_STORE && !accumulate) {
-    *dst = make_double2(v0, v1);
+                                      int accumulate) {
+  const uint32_t a = (raw >> CODE_SHIFT) & 3u;
+  double* dst = y + 2 * (int64_t)(raw & GID_MASK);
+  if ((a == W_STORE && !accumulate)) {
+    *reinterpret_cast<double2*>(dst) = make_double2(v0, v1);
   } else if (a == W_STORE || a == W_RMW) {
-    const double2 o = *dst;
-    *dst = make_double2(o.x + v0, o.y + v1);
+    const double o0 = rmw_load(dst), o1 = rmw_load(dst + 1);
+    *reinterpret_cast<double2*>(dst) = make_double2(o0 + v0, o1 + v1);
   } else if (a == W_ATOMIC) {
-    atomic_add_f64(&dst->x, v0);
-    atomic_add_f64(&dst->y, v1);
+    atomic_add_f64(dst, v0);
+    atomic_add_f64(dst + 1, v1);
   }
 }
 
@@ -121,42 +132,31 @@ __device__ __forceinline__ void store_row(double* L, int i, const double (&t)[N]
   if (N % 2) L[i * RS + N - 1] = t[N - 1];
 }
 
+template <int N>
+struct Tile {
+  static constexpr int EPW = WAVE / N;
+  static constexpr int LW = EPW * N;
+  static constexpr int SLOTS = (WAVE + N - 1) / N;  // every lane owns a tile slot
+  static constexpr int RS = (N % 2) ? N + 1 : N;    // 16-B aligned rows
+  static constexpr int ES = N * RS;
+};
+
 // ---------------------------------------------------------------------------
-// Poisson stiffness action over packed groups [g0, g1)
+// One group of the Poisson action: returns y_e[p][j] (p = 0..N-1) of the
+// lane's column j in v[], and the raw coded map entries in raw[].
 //   mapP[g][r][k*N + j] = map[e][r][j] | code,  GP[g][c][r][k*N + j] = G_c(e; r, j)
 // ---------------------------------------------------------------------------
-#ifndef SEM_POISSON_MIN_WAVES
-#define SEM_POISSON_MIN_WAVES 1
-#endif
-#ifndef SEM_PREFETCH_G
-#define SEM_PREFETCH_G 0
-#endif
-
 template <int N>
-__global__ void __launch_bounds__(BLOCK, SEM_POISSON_MIN_WAVES)
-    k_poisson_apply(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
-                    const double* __restrict__ u, double* __restrict__ y, int64_t g0, int64_t g1,
-                    int accumulate, const DMat<N> D) {
-  constexpr int EPW = WAVE / N;
-  constexpr int LW = EPW * N;
-  constexpr int SLOTS = (WAVE + N - 1) / N;  // every lane owns a tile slot
-  constexpr int RS = (N % 2) ? N + 1 : N;    // 16-B aligned rows
-  constexpr int ES = N * RS;
-  __shared__ __attribute__((aligned(16))) double lds[WAVES_PER_BLOCK * SLOTS * ES];
-
-  const int wave = threadIdx.x / WAVE;
-  const int lane = threadIdx.x % WAVE;
-  const int64_t g = g0 + (int64_t)blockIdx.x * WAVES_PER_BLOCK + wave;
-  if (g >= g1) return;  // whole wavefront leaves; no block barriers below
-  const int k = lane / N;
-  const int j = lane - k * N;
-  const bool in_wave = lane < LW;
-  double* L = lds + (wave * SLOTS + k) * ES;
-
+__device__ __forceinline__ void poisson_group(const uint32_t* __restrict__ mapP,
+                                              const double* __restrict__ GP,
+                                              const double* __restrict__ u, int64_t g, int lane,
+                                              int j, bool in_wave, double* L, const DMat<N>& D,
+                                              uint32_t (&raw)[N], double (&v)[N]) {
+  using T = Tile<N>;
+  constexpr int LW = T::LW;
+  constexpr int RS = T::RS;
   const uint32_t* mp = mapP + g * (int64_t)(N * LW) + lane;
   const double* gp = GP + g * (int64_t)(3 * N * LW) + lane;
-
-  uint32_t raw[N];
   double uc[N];
 #pragma unroll
   for (int r = 0; r < N; ++r) raw[r] = in_wave ? mp[r * LW] : (W_SKIP << CODE_SHIFT);
@@ -168,14 +168,6 @@ __global__ void __launch_bounds__(BLOCK, SEM_POISSON_MIN_WAVES)
     uc[r] = u[raw[r] & GID_MASK];
 #endif
   }
-#if SEM_PREFETCH_G
-  double gg[3][N];
-#pragma unroll
-  for (int c = 0; c < 3; ++c)
-#pragma unroll
-    for (int m = 0; m < N; ++m) gg[c][m] = gp[(c * N + m) * LW];
-#endif
-
   // column j: d0[m][j] = sum_r D[m][r] u[r][j]     (TensorProduct.deriv dim 0)
   double d0[N];
 #pragma unroll
@@ -188,7 +180,6 @@ __global__ void __launch_bounds__(BLOCK, SEM_POISSON_MIN_WAVES)
 #pragma unroll
   for (int r = 0; r < N; ++r) L[r * RS + j] = uc[r];
   wave_sync();
-
   // row i = j: d1[i][q] = sum_s D[q][s] u[i][s]     (TensorProduct.deriv dim 1)
   double t[N];
   {
@@ -205,18 +196,14 @@ __global__ void __launch_bounds__(BLOCK, SEM_POISSON_MIN_WAVES)
   wave_sync();
   store_row<N, RS>(L, j, t);
   wave_sync();
-
-  // column j: geometric factors, w0/w1, and ya = D^T w0 along xi0
-  double ya[N];
+  // column j: geometric factors, w0/w1, and ya = D^T w0 along xi0 (kept in v)
   double w1[N];
   {
     double w0[N];
 #pragma unroll
     for (int m = 0; m < N; ++m) {
       const double d1 = L[m * RS + j];
-#if SEM_PREFETCH_G
-      const double g00 = gg[0][m], g01 = gg[1][m], g11 = gg[2][m];
-#elif defined(SEM_DIAG_NO_G)
+#ifdef SEM_DIAG_NO_G
       const double g00 = 1.0 + m, g01 = 0.25 * j, g11 = 2.0;  // timing-only
 #else
       const double g00 = gp[(0 * N + m) * LW];
@@ -231,14 +218,13 @@ __global__ void __launch_bounds__(BLOCK, SEM_POISSON_MIN_WAVES)
       double a = 0.0;
 #pragma unroll
       for (int m = 0; m < N; ++m) a = fma(D.v[m * N + p], w0[m], a);
-      ya[p] = a;
+      v[p] = a;
     }
   }
   wave_sync();
 #pragma unroll
   for (int m = 0; m < N; ++m) L[m * RS + j] = w1[m];
   wave_sync();
-
   // row i = j: yb[i][q] = sum_n D[n][q] w1[i][n]
   {
     double wr[RS];
@@ -254,19 +240,86 @@ __global__ void __launch_bounds__(BLOCK, SEM_POISSON_MIN_WAVES)
   wave_sync();
   store_row<N, RS>(L, j, t);
   wave_sync();
-
-  // column j: y[p][j] = ya[p] + yb[p][j]; write through the coded map
 #pragma unroll
-  for (int p = 0; p < N; ++p) {
-    const double v = ya[p] + L[p * RS + j];
-    const double vn = __shfl_down(v, 1, WAVE);
+  for (int p = 0; p < N; ++p) v[p] += L[p * RS + j];
+  wave_sync();  // the tile is rewritten by the next group of this wave
+}
+
+// Scatter of one group's column values through the coded map, with the
+// in-group merge (next lane) and the chain carry (previous group) applied.
+// ncomp values per node (1: Poisson, 2: axisymmetric block).
+template <int N, int NC>
+__device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_t (&raw)[N],
+                                           double (&v)[NC][N], int lane, int wave, int rd,
+                                           bool in_wave, double (*carry)[CHAIN_WAVES][NC][N],
+                                           int accumulate) {
+  constexpr int LW = Tile<N>::LW;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int p = 0; p < N; ++p) {
+      const double vn = __shfl_down(v[c][p], 1, WAVE);
+      if ((raw[p] >> CODE_SHIFT) & W_MERGE) v[c][p] += vn;
+    }
+  // hand the last lane's column to the next group of the chain
+  if (lane == LW - 1) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int p = 0; p < N; ++p) carry[rd & 1][wave][c][p] = v[c][p];
+  }
+  __syncthreads();
+  if (lane == 0) {
+    const double* src = (wave > 0) ? &carry[rd & 1][wave - 1][0][0]
+                                   : &carry[(rd + 1) & 1][CHAIN_WAVES - 1][0][0];
+#pragma unroll
+    for (int p = 0; p < N; ++p)
+      if ((raw[p] >> CODE_SHIFT) & W_CARRY) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) v[c][p] += src[c * N + p];
+      }
+  }
+  if (in_wave) {
+#pragma unroll
+    for (int p = 0; p < N; ++p) {
+      if (NC == 1)
+        emit1(y, raw[p], v[0][p], accumulate);
+      else
+        emit2(y, raw[p], v[0][p], v[NC - 1][p], accumulate);
+    }
+  }
+  // this round's stores and carry reads complete before the next round
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// Poisson stiffness action: one workgroup per chain, chains [c0, c1).
+// ---------------------------------------------------------------------------
+template <int N>
+__global__ void __launch_bounds__(CHAIN_BLOCK, SEM_POISSON_MIN_WAVES)
+    k_poisson_apply(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
+                    const double* __restrict__ u, double* __restrict__ y, int64_t c0, int64_t c1,
+                    int rounds, int accumulate, const DMat<N> D) {
+  using T = Tile<N>;
+  __shared__ __attribute__((aligned(16))) double lds[CHAIN_WAVES * T::SLOTS * T::ES];
+  __shared__ double carry[2][CHAIN_WAVES][1][N];
+  const int64_t chain = c0 + blockIdx.x;
+  if (chain >= c1) return;  // uniform over the workgroup
+  const int wave = threadIdx.x / WAVE;
+  const int lane = threadIdx.x % WAVE;
+  const int k = lane / N;
+  const int j = lane - k * N;
+  const bool in_wave = lane < T::LW;
+  double* L = lds + (wave * T::SLOTS + k) * T::ES;
+  for (int rd = 0; rd < rounds; ++rd) {
+    const int64_t g = (chain * rounds + rd) * CHAIN_WAVES + wave;
+    uint32_t raw[N];
+    double v[1][N];
+    poisson_group<N>(mapP, GP, u, g, lane, j, in_wave, L, D, raw, v[0]);
 #ifdef SEM_DIAG_NO_STORE
-    if (in_wave && v == 1234.5678) y[0] = vn;  // timing-only: keeps v live, never true
-#elif defined(SEM_DIAG_PLAIN_STORE)
-    if (in_wave)  // timing-only: plain store for every lane, codes ignored
-      y[raw[p] & GID_MASK] = ((raw[p] >> CODE_SHIFT) & W_MERGE) ? v + vn : v;
+    if (in_wave && v[0][0] == 1234.5678) y[0] = v[0][1];  // timing-only
 #else
-    if (in_wave) emit1(y, raw[p], v, vn, accumulate);
+    chain_emit<N, 1>(y, raw, v, lane, wave, rd, in_wave, carry, accumulate);
 #endif
   }
 }
@@ -279,40 +332,26 @@ __global__ void __launch_bounds__(BLOCK, SEM_POISSON_MIN_WAVES)
 // factors: 0 G00rho 1 G01rho 2 G11rho 3 b0=2W iJ00 4 b1=2W iJ10 5 c=W/rho 6 m=rho^2 W
 // ---------------------------------------------------------------------------
 template <int N>
-__global__ void __launch_bounds__(BLOCK)
-    k_axisym_apply(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
-                   const double* __restrict__ u, double* __restrict__ y, int64_t g0, int64_t g1,
-                   int accumulate, const DMat<N> D) {
-  constexpr int EPW = WAVE / N;
-  constexpr int LW = EPW * N;
-  constexpr int SLOTS = (WAVE + N - 1) / N;
-  constexpr int RS = (N % 2) ? N + 1 : N;
-  constexpr int ES = 2 * N * RS;  // two fields per tile
-  __shared__ __attribute__((aligned(16))) double lds[WAVES_PER_BLOCK * SLOTS * ES];
-
-  const int wave = threadIdx.x / WAVE;
-  const int lane = threadIdx.x % WAVE;
-  const int64_t g = g0 + (int64_t)blockIdx.x * WAVES_PER_BLOCK + wave;
-  if (g >= g1) return;
-  const int k = lane / N;
-  const int j = lane - k * N;
-  const bool in_wave = lane < LW;
-  double* LP = lds + (wave * SLOTS + k) * ES;  // psi tile
-  double* LO = LP + N * RS;                     // omega tile
-
+__device__ __forceinline__ void axisym_group(const uint32_t* __restrict__ mapP,
+                                             const double* __restrict__ GP,
+                                             const double* __restrict__ u, int64_t g, int lane,
+                                             int j, bool in_wave, double* LP, double* LO,
+                                             const DMat<N>& D, uint32_t (&raw)[N],
+                                             double (&vo)[N], double (&vp)[N]) {
+  using T = Tile<N>;
+  constexpr int LW = T::LW;
+  constexpr int RS = T::RS;
   const uint32_t* mp = mapP + g * (int64_t)(N * LW) + lane;
   const double* gp = GP + g * (int64_t)(7 * N * LW) + lane;
   const double2* u2 = reinterpret_cast<const double2*>(u);
-
-  uint32_t raw[N];
   double ps[N], om[N];
 #pragma unroll
   for (int r = 0; r < N; ++r) raw[r] = in_wave ? mp[r * LW] : (W_SKIP << CODE_SHIFT);
 #pragma unroll
   for (int r = 0; r < N; ++r) {
-    const double2 v = u2[raw[r] & GID_MASK];
-    ps[r] = v.x;
-    om[r] = v.y;
+    const double2 val = u2[raw[r] & GID_MASK];
+    ps[r] = val.x;
+    om[r] = val.y;
   }
   double d0p[N], d0o[N];
 #pragma unroll
@@ -353,7 +392,7 @@ __global__ void __launch_bounds__(BLOCK)
     store_row<N, RS>(LO, j, to);
   }
   wave_sync();
-  double yap[N], yao[N], w1p[N], w1o[N];
+  double w1p[N], w1o[N];
   {
     double w0p[N], w0o[N];
 #pragma unroll
@@ -384,8 +423,8 @@ __global__ void __launch_bounds__(BLOCK)
         a = fma(D.v[m * N + p], w0p[m], a);
         b = fma(D.v[m * N + p], w0o[m], b);
       }
-      yap[p] = a + d0p[p];
-      yao[p] = b + d0o[p];
+      vp[p] = a + d0p[p];
+      vo[p] = b + d0o[p];
     }
   }
   wave_sync();
@@ -418,12 +457,35 @@ __global__ void __launch_bounds__(BLOCK)
   wave_sync();
 #pragma unroll
   for (int p = 0; p < N; ++p) {
-    // row 2k <- omega equation (Lve.omega), row 2k+1 <- psi equation
-    const double vo = yao[p] + LO[p * RS + j];
-    const double vp = yap[p] + LP[p * RS + j];
-    const double no = __shfl_down(vo, 1, WAVE);
-    const double np = __shfl_down(vp, 1, WAVE);
-    if (in_wave) emit2(y, raw[p], vo, vp, no, np, accumulate);
+    vo[p] += LO[p * RS + j];
+    vp[p] += LP[p * RS + j];
+  }
+  wave_sync();
+}
+
+template <int N>
+__global__ void __launch_bounds__(CHAIN_BLOCK)
+    k_axisym_apply(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
+                   const double* __restrict__ u, double* __restrict__ y, int64_t c0, int64_t c1,
+                   int rounds, int accumulate, const DMat<N> D) {
+  using T = Tile<N>;
+  __shared__ __attribute__((aligned(16))) double lds[CHAIN_WAVES * T::SLOTS * 2 * T::ES];
+  __shared__ double carry[2][CHAIN_WAVES][2][N];
+  const int64_t chain = c0 + blockIdx.x;
+  if (chain >= c1) return;
+  const int wave = threadIdx.x / WAVE;
+  const int lane = threadIdx.x % WAVE;
+  const int k = lane / N;
+  const int j = lane - k * N;
+  const bool in_wave = lane < T::LW;
+  double* LP = lds + (wave * T::SLOTS + k) * 2 * T::ES;  // psi tile
+  double* LO = LP + T::ES;                               // omega tile
+  for (int rd = 0; rd < rounds; ++rd) {
+    const int64_t g = (chain * rounds + rd) * CHAIN_WAVES + wave;
+    uint32_t raw[N];
+    double v[2][N];  // [0] omega row (y[2k]), [1] psi row (y[2k+1])
+    axisym_group<N>(mapP, GP, u, g, lane, j, in_wave, LP, LO, D, raw, v[0], v[1]);
+    chain_emit<N, 2>(y, raw, v, lane, wave, rd, in_wave, carry, accumulate);
   }
 }
 

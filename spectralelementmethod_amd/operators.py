@@ -141,12 +141,15 @@ class SEMOperator(object):
 
     def plan_info(self):
         """Setup plan of the scatter (see include/sem_hip.h sem_plan_info)."""
-        info = (C.c_int64 * 15)()
-        _lib.check(self._lib.sem_plan_info(self._ctx, info, 15))
+        info = (C.c_int64 * 17)()
+        _lib.check(self._lib.sem_plan_info(self._ctx, info, 17))
         v = list(info)
+        counts = [x for x in v[8:8 + v[5]]]
+        while counts and counts[-1] == 0:
+            counts.pop()
         return dict(groups=v[0], zero_list=v[1], atomic_groups=v[2], conforming=bool(v[3]),
-                    elements_per_group=v[4], colours=v[5],
-                    groups_per_colour=[x for x in v[6:6 + v[5]]])
+                    elements_per_group=v[4], colours=len(counts), rounds=v[6], slots=v[7],
+                    chains_per_colour=counts)
 
     # ------------------------------------------------------------------
     def compute_geometry(self, kind=POISSON, stream=None):
