@@ -35,6 +35,7 @@ from spectralelementmethod_amd.operators import SEMOperator, POISSON, AXISYM_STO
 
 METRIC = "global stiffness-action DOF-updates/s (and % HBM roofline), Poisson p=8"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+DEFAULT_TRAFFIC = "r01/pmc_traffic_p8_1024x1024.json"
 
 
 def log(msg):
@@ -128,6 +129,7 @@ def main():
     dev = torch.device("cuda", local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        dist.barrier()
 
     kind = POISSON if args.op == "poisson" else AXISYM_STOKES
     dpn = 1 if kind == POISSON else 2
@@ -204,8 +206,13 @@ def main():
     F = alg_flops(kind, op.n_elem, p)
     achieved = B / kern_avg_s / 1e9
     traffic = None
-    if args.traffic_json and os.path.exists(args.traffic_json):
-        with open(args.traffic_json) as f:
+    traffic_src = args.traffic_json
+    if traffic_src is None and kind == POISSON and (p, args.nex, args.ney) == (8, 1024, 1024):
+        # PMC measurement of this workload (separate FETCH_SIZE / WRITE_SIZE
+        # passes, tools/gpu_profile.sh + tools/pmc_traffic.py)
+        traffic_src = os.path.join(ROOT, "profiles", DEFAULT_TRAFFIC)
+    if traffic_src and os.path.exists(traffic_src):
+        with open(traffic_src) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
     result = {
         "metric": METRIC if kind == POISSON else METRIC.replace("Poisson p=8",
@@ -241,6 +248,8 @@ def main():
             "kernel": "k_poisson_apply<%d>" % (p + 1) if kind == POISSON else
                       "k_axisym_apply<%d>" % (p + 1),
             "alg_bytes_per_launch": B,
+            "launch": "one sem_apply = %d colour launches" % plan["colours"],
+            "traffic_source": os.path.relpath(traffic_src, ROOT) if traffic is not None else None,
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and kind == POISSON:
