@@ -35,27 +35,38 @@ from spectralelementmethod_amd.operators import SEMOperator, POISSON, AXISYM_STO
 
 METRIC = "global stiffness-action DOF-updates/s (and % HBM roofline), Poisson p=8"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-DEFAULT_TRAFFIC = "r01/pmc_traffic_p8_1024x1024.json"
+FP64_PEAK_TFLOPS = 78.6  # MI355X vector fp64 (256 CUs x 128 FLOP/clk x 2.4 GHz)
+# PMC-measured HBM bytes of the headline workload, per geometry mode
+DEFAULT_TRAFFIC = {"stored": "r01/pmc_traffic_p8_1024x1024.json",
+                   "nodal": "r01/pmc_traffic_nodal_p8_1024x1024.json"}
 
 
 def log(msg):
     print("[bench] " + msg, file=sys.stderr, flush=True)
 
 
-def alg_bytes(kind, ndof_nodes, n_elem, p):
-    """Poisson B = 16*ndof + 28*E*(p+1)^2 (u read, y written,
-    3 fp64 factors + one uint32 map entry per local node); axisymmetric
-    B = 32*n_nodes + 60*E*(p+1)^2."""
+def alg_bytes(kind, ndof_nodes, n_elem, p, geometry="stored"):
+    """Poisson with stored factors B = 16*ndof + 28*E*(p+1)^2
+    (u read, y written, 3 fp64 factors + one uint32 map entry per local
+    node); with nodal geometry the factors are replaced by x_phys per global
+    node: B = 32*ndof + 4*E*(p+1)^2; axisymmetric B = 32*n_nodes +
+    60*E*(p+1)^2."""
     n2 = (p + 1) ** 2
+    if kind == POISSON and geometry == "nodal":
+        return 32 * ndof_nodes + 4 * n_elem * n2
     if kind == POISSON:
         return 16 * ndof_nodes + 28 * n_elem * n2
     return 32 * ndof_nodes + 60 * n_elem * n2
 
 
-def alg_flops(kind, n_elem, p):
+def alg_flops(kind, n_elem, p, geometry="stored"):
+    """fp64 FLOP per action: the four sum-factorised contractions (2 n^3 each)
+    plus pointwise work; nodal geometry adds the four derivatives of x_phys
+    and the per-node det / inverse / detJxW (15 n^2 incl. one division)."""
     n = p + 1
     if kind == POISSON:
-        return n_elem * (8 * n ** 3 + 7 * n ** 2)
+        extra = 8 * n ** 3 + 15 * n ** 2 if geometry == "nodal" else 0
+        return n_elem * (8 * n ** 3 + 7 * n ** 2 + extra)
     return n_elem * (16 * n ** 3 + 22 * n ** 2)
 
 
@@ -114,6 +125,8 @@ def main():
     ap.add_argument("--ney", type=int, default=1024)
     ap.add_argument("--warp", type=float, default=0.05)
     ap.add_argument("--op", choices=["poisson", "axisym_stokes"], default="poisson")
+    ap.add_argument("--geometry", choices=["nodal", "stored"], default="nodal",
+                    help="Poisson geometric factors: re-derived from x_phys per node, or streamed")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--traffic-json", default=None,
@@ -146,7 +159,8 @@ def main():
         nodes, e2n = meshgen.annulus(args.nex, args.ney, p)
     log("rank %d: mesh %d elements, %d nodes (%.1fs)" % (rank, e2n.shape[0], nodes.shape[1],
                                                           time.time() - t0))
-    op = SEMOperator(p, e2n, nodes, dofs_per_node=dpn, device=dev)
+    geometry = args.geometry if kind == POISSON else "stored"
+    op = SEMOperator(p, e2n, nodes, dofs_per_node=dpn, device=dev, geometry=geometry)
     op.compute_geometry(kind)
     plan = op.plan_info()
     log("rank %d: plan %s" % (rank, plan))
@@ -202,15 +216,15 @@ def main():
     n_nodes_local = op.n_node
     ndof_global = part.global_nodes * dpn if kind == POISSON else op.ndof
     value = ndof_global * args.steps / elapsed
-    B = alg_bytes(kind, n_nodes_local, op.n_elem, p)
-    F = alg_flops(kind, op.n_elem, p)
+    B = alg_bytes(kind, n_nodes_local, op.n_elem, p, geometry)
+    F = alg_flops(kind, op.n_elem, p, geometry)
     achieved = B / kern_avg_s / 1e9
     traffic = None
     traffic_src = args.traffic_json
     if traffic_src is None and kind == POISSON and (p, args.nex, args.ney) == (8, 1024, 1024):
         # PMC measurement of this workload (separate FETCH_SIZE / WRITE_SIZE
         # passes, tools/gpu_profile.sh + tools/pmc_traffic.py)
-        traffic_src = os.path.join(ROOT, "profiles", DEFAULT_TRAFFIC)
+        traffic_src = os.path.join(ROOT, "profiles", DEFAULT_TRAFFIC[geometry])
     if traffic_src and os.path.exists(traffic_src):
         with open(traffic_src) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
@@ -233,7 +247,7 @@ def main():
                 args.op, p, args.nex, args.ney,
                 "10^6-element north-star mesh" if (args.nex, args.ney, p) == (1024, 1024, 8)
                 else "custom"),
-            "p": p, "n_elem_per_gpu": op.n_elem, "ndof_global": ndof_global,
+            "p": p, "geometry": geometry, "n_elem_per_gpu": op.n_elem, "ndof_global": ndof_global,
             "ndof_per_gpu": op.ndof, "parallelism": "element column strips x%d, RCCL P2P "
                                                     "interface sum" % world if world > 1 else
             "single GPU",
@@ -248,6 +262,7 @@ def main():
             "kernel": "k_poisson_apply<%d>" % (p + 1) if kind == POISSON else
                       "k_axisym_apply<%d>" % (p + 1),
             "alg_bytes_per_launch": B,
+            "fp64_tflops": F / kern_avg_s / 1e12, "fp64_peak_tflops": FP64_PEAK_TFLOPS,
             "launch": "one sem_apply = %d colour launches" % plan["colours"],
             "traffic_source": os.path.relpath(traffic_src, ROOT) if traffic is not None else None,
         },

@@ -110,6 +110,20 @@ int sem_set_map(sem_ctx* ctx, const uint32_t* d_e2n, void* stream);
  * each).  Writes min(n_info, 17) values. */
 int sem_plan_info(sem_ctx* ctx, int64_t* info, int n_info);
 
+/* How the Poisson action obtains its geometric factors.
+ *  SEM_GEOM_NODAL (default): sem_geom_from_nodes keeps x_phys per global node
+ *    (16 B/node) and the action re-derives J, det, invJ and detJxW at every
+ *    quadrature node from it -- the reference's own order of work, which
+ *    recomputes the geometry inside the element loop (sem/discrete.py:189-209,
+ *    582-597) -- trading ~600 FLOP for ~1.9 KB of HBM per element at p = 8.
+ *  SEM_GEOM_STORED: the 3 factors per quadrature node are precomputed and
+ *    streamed (24 B per element node).
+ * Takes effect at the next sem_geom_from_nodes; sem_set_geom always installs
+ * stored factors.  The axisymmetric block always uses stored factors. */
+#define SEM_GEOM_STORED 0
+#define SEM_GEOM_NODAL 1
+int sem_set_geom_mode(sem_ctx* ctx, int mode);
+
 /* Geometry from mesh nodes (device, float64 [2][n_node]) for op_kind:
  * x_phys = V_eq^-1 X V_eq^-T (Mapping._compute_x_phys, sem/mapping.py:98-103),
  * J = gradient(x_phys) (sem/mapping.py:105-114), det/inverse

@@ -281,6 +281,11 @@ struct sem_ctx {
   int64_t n_atomic_groups = 0;        // groups in atomic-fallback chains
   bool conforming = true;
   double* d_GP[2] = {nullptr, nullptr};
+  // NODAL geometry (Poisson): x_phys per global node + the node's first element
+  int geom_mode = SEM_GEOM_NODAL;
+  double2* d_XG = nullptr;
+  uint32_t* d_owner = nullptr;
+  bool xg_valid = false;
   // CG scratch
   double* d_cg = nullptr;
   int64_t cg_len = 0;
@@ -304,24 +309,47 @@ struct DeviceGuard {
 
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// even-odd halves of D (row-major h[m*N + r]); see DEO in sem_kernels.h
 template <int N>
-DMat<N> make_dmat(const double* h) {
-  DMat<N> d;
-  std::memcpy(d.v, h, sizeof(d.v));
+DEO<N> make_deo(const double* h) {
+  DEO<N> d;
+  constexpr int H = N / 2;
+  for (int m = 0; m < H; ++m)
+    for (int r = 0; r < H; ++r) {
+      d.P[m * H + r] = 0.5 * (h[m * N + r] - h[m * N + N - 1 - r]);
+      d.Q[m * H + r] = 0.5 * (h[m * N + r] + h[m * N + N - 1 - r]);
+    }
+  if (DEO<N>::C)
+    for (int m = 0; m < H; ++m) {
+      d.cc[m] = h[m * N + H];
+      d.rr[m] = h[H * N + m];
+    }
   return d;
+}
+
+// the Poisson action recomputes its factors from x_phys per node (NODAL)
+// unless the stored-factor mode was chosen or the caller supplied factors
+bool use_nodal(const sem_ctx* c, int op_kind) {
+  return op_kind == SEM_OP_POISSON && c->geom_mode == SEM_GEOM_NODAL && c->xg_valid;
 }
 
 template <int N>
 int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc, hipStream_t st) {
-  const DMat<N> D = make_dmat<N>(c->hD);
+  const DEO<N> D = make_deo<N>(c->hD);
+  WVec<N> w;
+  std::memcpy(w.v, c->hw, sizeof(w.v));
+  const bool nodal = use_nodal(c, op_kind);
   const size_t nc = c->colour_start.size() - 1;
   for (size_t k = 0; k < nc; ++k) {
     const int64_t c0 = c->colour_start[k], c1 = c->colour_start[k + 1];
     if (c1 <= c0) continue;
     const int grid = (int)(c1 - c0);
-    if (op_kind == SEM_OP_POISSON)
-      hipLaunchKernelGGL((k_poisson_apply<N>), dim3(grid), dim3(CHAIN_BLOCK), 0, st, c->d_mapP,
-                         c->d_GP[0], u, y, c0, c1, c->rounds, acc, D);
+    if (op_kind == SEM_OP_POISSON && nodal)
+      hipLaunchKernelGGL((k_poisson_apply<N, true>), dim3(grid), dim3(CHAIN_BLOCK), 0, st,
+                         c->d_mapP, nullptr, c->d_XG, u, y, c0, c1, c->rounds, acc, D, w);
+    else if (op_kind == SEM_OP_POISSON)
+      hipLaunchKernelGGL((k_poisson_apply<N, false>), dim3(grid), dim3(CHAIN_BLOCK), 0, st,
+                         c->d_mapP, c->d_GP[0], nullptr, u, y, c0, c1, c->rounds, acc, D, w);
     else
       hipLaunchKernelGGL((k_axisym_apply<N>), dim3(grid), dim3(CHAIN_BLOCK), 0, st, c->d_mapP,
                          c->d_GP[1], u, y, c0, c1, c->rounds, acc, D);
@@ -329,14 +357,16 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
   return SEM_OK;
 }
 
+// nodes -> factors/fields (XGin null), or XGin (x_phys per node) -> factors
 template <int N>
 void launch_geom_n(sem_ctx* c, const double* nodes, int op_kind, double* GP, double* xph,
-                   double* J, double* iJ, double* dJ, double* dJW, hipStream_t st) {
+                   double* J, double* iJ, double* dJ, double* dJW, double2* XG,
+                   const double2* XGin, hipStream_t st) {
   using Sh = GeomShape<N>;
   const int grid = (int)((c->n_elem + Sh::EPB - 1) / Sh::EPB);
   hipLaunchKernelGGL((k_geometry<N>), dim3(grid), dim3(Sh::THREADS), 0, st, nodes, c->n_node,
                      c->d_e2n, c->n_elem, c->d_Vinv, c->d_D, c->d_w, op_kind, c->d_gpos, GP, xph,
-                     J, iJ, dJ, dJW, c->d_bad);
+                     J, iJ, dJ, dJW, XG, XG ? c->d_owner : nullptr, XGin, c->d_bad);
 }
 
 #define SEM_DISPATCH_N(n, FN, ...)       \
@@ -403,6 +433,7 @@ int ensure_gp(sem_ctx* c, int op_kind) {
 //   6. zero list = unreferenced nodes + nodes whose first writer is atomic.
 // ---------------------------------------------------------------------------
 struct Plan {
+  std::vector<uint32_t> owner;  // first element referencing each node
   std::vector<uint32_t> mapP;
   std::vector<int> gpos;
   std::vector<int64_t> colour_start;  // in chains
@@ -421,9 +452,10 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
   auto is_bnd = [n](int r, int jj) { return r == 0 || r == n - 1 || jj == 0 || jj == n - 1; };
   // references and conformity (interior local nodes must be unique)
   std::vector<uint32_t> cnt(n_node, 0);
+  P.owner.assign(n_node, 0xFFFFFFFFu);
   for (int64_t t = 0; t < n_elem * nn; ++t) {
     if (e2n[t] >= n_node) return fail(SEM_E_INVALID, "element map references node >= n_node");
-    cnt[e2n[t]]++;
+    if (!cnt[e2n[t]]++) P.owner[e2n[t]] = (uint32_t)(t / nn);
   }
   bool conforming = true;
   for (int64_t e = 0; e < n_elem && conforming; ++e)
@@ -606,6 +638,7 @@ int sem_ctx_create(sem_ctx** out, int p, int64_t n_elem, int64_t n_node, int dpn
   c->epw = epw_of(c->n);
   c->lw = c->epw * c->n;
   c->n_groups = (n_elem + c->epw - 1) / c->epw;
+  if (const char* s = std::getenv("SEM_GEOM_MODE")) c->geom_mode = std::atoi(s) ? 1 : 0;
   if (c->n_groups > 0x7FFFFFFFll) {
     delete c;
     return fail(SEM_E_INVALID, "too many elements");
@@ -634,6 +667,8 @@ void sem_ctx_destroy(sem_ctx* c) {
   (void)hipFree(c->d_zero);
   (void)hipFree(c->d_GP[0]);
   (void)hipFree(c->d_GP[1]);
+  (void)hipFree(c->d_XG);
+  (void)hipFree(c->d_owner);
   (void)hipFree(c->d_cg);
   (void)hipFree(c->d_red);
   (void)hipFree(c->d_bad);
@@ -691,10 +726,16 @@ int sem_set_map(sem_ctx* c, const uint32_t* d_e2n, void* stream) {
   c->colour_start = P.colour_start;
   c->n_atomic_groups = P.n_atomic_groups;
   c->conforming = P.conforming;
-  // geometry factors were packed for the previous order
+  (void)hipFree(c->d_owner);
+  c->d_owner = nullptr;
+  HIP_TRY(hipMalloc(&c->d_owner, P.owner.size() * sizeof(uint32_t)));
+  HIP_TRY(hipMemcpy(c->d_owner, P.owner.data(), P.owner.size() * sizeof(uint32_t),
+                    hipMemcpyHostToDevice));
+  // geometry was derived for the previous map
   (void)hipFree(c->d_GP[0]);
   (void)hipFree(c->d_GP[1]);
   c->d_GP[0] = c->d_GP[1] = nullptr;
+  c->xg_valid = false;
   return SEM_OK;
 }
 
@@ -718,6 +759,14 @@ static int geom_common(sem_ctx* c, const double* d_nodes, const double* h_Vinv) 
   return SEM_OK;
 }
 
+int sem_set_geom_mode(sem_ctx* c, int mode) {
+  if (!c) return fail(SEM_E_INVALID, "null ctx");
+  if (mode != SEM_GEOM_STORED && mode != SEM_GEOM_NODAL)
+    return fail(SEM_E_INVALID, "unknown geometry mode " + std::to_string(mode));
+  c->geom_mode = mode;
+  return SEM_OK;
+}
+
 int sem_geom_from_nodes(sem_ctx* c, const double* d_nodes, const double* h_Vinv, int op_kind,
                         int64_t* n_bad_nodes, void* stream) {
   if (!c) return fail(SEM_E_INVALID, "null ctx");
@@ -725,18 +774,29 @@ int sem_geom_from_nodes(sem_ctx* c, const double* d_nodes, const double* h_Vinv,
   int rc = geom_common(c, d_nodes, h_Vinv);
   if (rc) return rc;
   if ((rc = check_op(c, op_kind))) return rc;
-  if ((rc = ensure_gp(c, op_kind))) return rc;
+  const bool nodal = op_kind == SEM_OP_POISSON && c->geom_mode == SEM_GEOM_NODAL;
+  double* GP = nullptr;
+  if (nodal) {
+    if (!c->d_XG) HIP_TRY(hipMalloc(&c->d_XG, c->n_node * sizeof(double2)));
+    // stale stored factors would otherwise survive for sem_diag
+    (void)hipFree(c->d_GP[0]);
+    c->d_GP[0] = nullptr;
+  } else {
+    if ((rc = ensure_gp(c, op_kind))) return rc;
+    GP = c->d_GP[op_kind == SEM_OP_POISSON ? 0 : 1];
+  }
   hipStream_t st = S(stream);
   HIP_TRY(hipMemsetAsync(c->d_bad, 0, sizeof(unsigned long long), st));
-  double* GP = c->d_GP[op_kind == SEM_OP_POISSON ? 0 : 1];
+  if (nodal) HIP_TRY(hipMemsetAsync(c->d_XG, 0, c->n_node * sizeof(double2), st));
   SEM_DISPATCH_N(c->n, launch_geom_n, c, d_nodes, op_kind, GP, nullptr, nullptr, nullptr, nullptr,
-                 nullptr, st);
+                 nullptr, nodal ? c->d_XG : nullptr, nullptr, st);
   HIP_TRY(hipGetLastError());
   unsigned long long bad = 0;
   HIP_TRY(hipMemcpyAsync(&bad, c->d_bad, sizeof(bad), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   if (n_bad_nodes) *n_bad_nodes = (int64_t)bad;
   if (bad) return fail(SEM_E_DETJ, "detJ <= 0 at " + std::to_string(bad) + " quadrature nodes");
+  if (op_kind == SEM_OP_POISSON) c->xg_valid = nodal;
   return SEM_OK;
 }
 
@@ -749,7 +809,7 @@ int sem_geom_fields(sem_ctx* c, const double* d_nodes, const double* h_Vinv, dou
   hipStream_t st = S(stream);
   HIP_TRY(hipMemsetAsync(c->d_bad, 0, sizeof(unsigned long long), st));
   SEM_DISPATCH_N(c->n, launch_geom_n, c, d_nodes, SEM_OP_POISSON, nullptr, x_phys, J, invJ, detJ,
-                 detJxW, st);
+                 detJxW, nullptr, nullptr, st);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(st));
   return SEM_OK;
@@ -763,6 +823,7 @@ int sem_set_geom(sem_ctx* c, const double* d_G, int op_kind, void* stream) {
   if ((rc = check_op(c, op_kind))) return rc;
   if ((rc = ensure_gp(c, op_kind))) return rc;
   const int ncomp = sem_op_ncomp(op_kind);
+  if (op_kind == SEM_OP_POISSON) c->xg_valid = false;  // caller's factors take over
   hipLaunchKernelGGL(k_pack_geom, dim3(grid_for(c->n_elem * ncomp * c->n * c->n)), dim3(BLOCK), 0,
                      S(stream), d_G, c->n_elem, c->n, ncomp, c->epw, c->d_gpos,
                      c->d_GP[op_kind == SEM_OP_POISSON ? 0 : 1]);
@@ -788,7 +849,7 @@ int sem_apply(sem_ctx* c, int op_kind, const double* u, double* y, int flags, vo
   int rc;
   if ((rc = check_op(c, op_kind))) return rc;
   if (!c->have_basis || !c->d_mapP) return fail(SEM_E_STATE, "basis and map must be set");
-  if (!c->d_GP[op_kind == SEM_OP_POISSON ? 0 : 1])
+  if (!use_nodal(c, op_kind) && !c->d_GP[op_kind == SEM_OP_POISSON ? 0 : 1])
     return fail(SEM_E_STATE, "geometry for this operator has not been computed");
   DeviceGuard g(c->device);
   hipStream_t st = S(stream);
@@ -814,9 +875,16 @@ int sem_diag(sem_ctx* c, int op_kind, double* d_diag, void* stream) {
   if (op_kind != SEM_OP_POISSON) return fail(SEM_E_NOTIMPL, "sem_diag: Poisson only");
   int rc;
   if ((rc = check_op(c, op_kind))) return rc;
-  if (!c->d_GP[0] || !c->d_mapP) return fail(SEM_E_STATE, "geometry/map not set");
+  if (!c->d_mapP || !(c->d_GP[0] || use_nodal(c, op_kind)))
+    return fail(SEM_E_STATE, "geometry/map not set");
   DeviceGuard g(c->device);
   hipStream_t st = S(stream);
+  if (!c->d_GP[0]) {  // NODAL mode: derive the stored factors once from x_phys per node
+    if ((rc = ensure_gp(c, op_kind))) return rc;
+    SEM_DISPATCH_N(c->n, launch_geom_n, c, nullptr, SEM_OP_POISSON, c->d_GP[0], nullptr, nullptr,
+                   nullptr, nullptr, nullptr, nullptr, c->d_XG, st);
+    HIP_TRY(hipGetLastError());
+  }
   HIP_TRY(hipMemsetAsync(d_diag, 0, c->n_node * sizeof(double), st));
   hipLaunchKernelGGL(k_poisson_diag, dim3(grid_for(c->n_elem * c->n * c->n)), dim3(BLOCK), 0, st,
                      c->d_mapP, c->d_GP[0], c->d_gpos, c->d_D, c->n, c->epw, c->n_elem, d_diag);

@@ -61,10 +61,98 @@ constexpr uint32_t W_CARRY = 8;   // add the value handed over by the previous g
 #define SEM_POISSON_MIN_WAVES 1
 #endif
 
+// D1 in even-odd form.  D is centro-antisymmetric (D[N-1-i][N-1-j] =
+// -D[i][j] on the symmetric GLL nodes), so with e_r = x_r + x_{N-1-r},
+// o_r = x_r - x_{N-1-r} (r < H = N/2) both D x and D^T x need only
+//   P[m][r] = (D[m][r] - D[m][N-1-r]) / 2,  Q[m][r] = (D[m][r] + D[m][N-1-r]) / 2
+// plus, for odd N, the middle column cc[m] = D[m][H] and row rr[r] = D[H][r]:
+// 2H^2 + 2H values instead of N^2 (40 vs 81 doubles at p = 8, so D fits the
+// scalar register file next to the kernel's pointers) and ~40 % fewer FMAs.
 template <int N>
-struct DMat {
-  double v[N * N];
+struct DEO {
+  static constexpr int H = N / 2;
+  static constexpr int C = N % 2;
+  double P[H * H];
+  double Q[H * H];
+  double cc[C ? H : 1];
+  double rr[C ? H : 1];
 };
+
+// v = D x
+template <int N>
+__device__ __forceinline__ void deo_apply(const DEO<N>& E, const double (&x)[N],
+                                          double (&v)[N]) {
+  constexpr int H = N / 2;
+  double e[H], o[H];
+#pragma unroll
+  for (int r = 0; r < H; ++r) {
+    e[r] = x[r] + x[N - 1 - r];
+    o[r] = x[r] - x[N - 1 - r];
+  }
+#pragma unroll
+  for (int m = 0; m < H; ++m) {
+    double sp = 0.0, tp = 0.0;
+    if constexpr (DEO<N>::C) tp = E.cc[m] * x[H];
+#pragma unroll
+    for (int r = 0; r < H; ++r) {
+      sp = fma(E.P[m * H + r], o[r], sp);
+      tp = fma(E.Q[m * H + r], e[r], tp);
+    }
+    v[m] = sp + tp;
+    v[N - 1 - m] = sp - tp;
+  }
+  if constexpr (DEO<N>::C) {
+    double a = 0.0;
+#pragma unroll
+    for (int r = 0; r < H; ++r) a = fma(E.rr[r], o[r], a);
+    v[H] = a;
+  }
+}
+
+// v = D^T x  (the transpose is centro-antisymmetric with P^T <-> Q^T swapped)
+template <int N>
+__device__ __forceinline__ void deo_apply_t(const DEO<N>& E, const double (&x)[N],
+                                            double (&v)[N]) {
+  constexpr int H = N / 2;
+  double e[H], o[H];
+#pragma unroll
+  for (int r = 0; r < H; ++r) {
+    e[r] = x[r] + x[N - 1 - r];
+    o[r] = x[r] - x[N - 1 - r];
+  }
+#pragma unroll
+  for (int q = 0; q < H; ++q) {
+    double sp = 0.0, tp = 0.0;
+    if constexpr (DEO<N>::C) tp = E.rr[q] * x[H];
+#pragma unroll
+    for (int m = 0; m < H; ++m) {
+      sp = fma(E.Q[m * H + q], o[m], sp);
+      tp = fma(E.P[m * H + q], e[m], tp);
+    }
+    v[q] = sp + tp;
+    v[N - 1 - q] = sp - tp;
+  }
+  if constexpr (DEO<N>::C) {
+    double a = 0.0;
+#pragma unroll
+    for (int m = 0; m < H; ++m) a = fma(E.cc[m], o[m], a);
+    v[H] = a;
+  }
+}
+
+template <int N>
+struct WVec {  // 1-D GLL quadrature weights
+  double v[N];
+};
+
+// w[j] for a lane-varying j without dynamic indexing of the kernel arguments
+template <int N>
+__device__ __forceinline__ double pick(const WVec<N>& w, int j) {
+  double r = w.v[0];
+#pragma unroll
+  for (int q = 1; q < N; ++q) r = (j == q) ? w.v[q] : r;
+  return r;
+}
 
 // Ordering point for LDS traffic between lanes of ONE wavefront (a wave's LDS
 // operations complete in issue order; this only stops the compiler moving
@@ -91,7 +179,13 @@ __device__ __forceinline__ void emit1(double* __restrict__ y, uint32_t raw, doub
   if (a == W_STORE) {
     *dst = accumulate ? rmw_load(dst) + v : v;
   } else if (a == W_RMW) {
+#if defined(SEM_DIAG_RMW_AS_STORE)
+    *dst = v;  // timing-only
+#elif SEM_RMW_ATOMIC
+    atomic_add_f64(dst, v);  // no writer runs concurrently: ordered, no return
+#else
     *dst = rmw_load(dst) + v;
+#endif
   } else if (a == W_ATOMIC) {
     atomic_add_f64(dst, v);
   }
@@ -112,47 +206,98 @@ __device__ __forceinline__ void emit2(double* __restrict__ y, uint32_t raw, doub
   }
 }
 
-// row i of the tile (16-B aligned, RS doubles) -> registers
+// row i of the tile (RS doubles, 16-B aligned when RS is even) -> registers
 template <int N, int RS>
 __device__ __forceinline__ void load_row(const double* L, int i, double (&r)[RS]) {
-  const double2* row = reinterpret_cast<const double2*>(L + i * RS);
+  if constexpr (RS % 2 == 0) {
+    const double2* row = reinterpret_cast<const double2*>(L + i * RS);
 #pragma unroll
-  for (int s = 0; s < RS / 2; ++s) {
-    const double2 v = row[s];
-    r[2 * s] = v.x;
-    r[2 * s + 1] = v.y;
+    for (int s = 0; s < RS / 2; ++s) {
+      const double2 v = row[s];
+      r[2 * s] = v.x;
+      r[2 * s + 1] = v.y;
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < RS; ++s) r[s] = L[i * RS + s];
   }
 }
 
 template <int N, int RS>
 __device__ __forceinline__ void store_row(double* L, int i, const double (&t)[N]) {
-  double2* row = reinterpret_cast<double2*>(L + i * RS);
+  if constexpr (RS % 2 == 0) {
+    double2* row = reinterpret_cast<double2*>(L + i * RS);
 #pragma unroll
-  for (int s = 0; s < N / 2; ++s) row[s] = make_double2(t[2 * s], t[2 * s + 1]);
-  if (N % 2) L[i * RS + N - 1] = t[N - 1];
+    for (int s = 0; s < N / 2; ++s) row[s] = make_double2(t[2 * s], t[2 * s + 1]);
+    if (N % 2) L[i * RS + N - 1] = t[N - 1];
+  } else {
+#pragma unroll
+    for (int s = 0; s < N; ++s) L[i * RS + s] = t[s];
+  }
 }
 
-template <int N>
+// LDS tiles: one N x RS slot per element of a group; the padding lanes
+// (lane >= LW when N does not divide 64) of every wave share one scratch
+// slot whose contents are never used.
+// PAD: rows padded to 16 B for ds_read_b128 (odd N).  The nodal Poisson
+// kernel keeps two tiles per element slot and goes unpadded so that four
+// workgroups fit one CU's LDS at p = 8.
+#ifndef SEM_TILE_PAD_STORED
+#define SEM_TILE_PAD_STORED 1
+#endif
+#ifndef SEM_TILE_PAD_NODAL
+#define SEM_TILE_PAD_NODAL 0
+#endif
+#ifndef SEM_NODAL_EARLY_U
+#define SEM_NODAL_EARLY_U 0
+#endif
+#ifndef SEM_RMW_ATOMIC
+#define SEM_RMW_ATOMIC 0
+#endif
+template <int N, bool PAD = true>
 struct Tile {
   static constexpr int EPW = WAVE / N;
   static constexpr int LW = EPW * N;
-  static constexpr int SLOTS = (WAVE + N - 1) / N;  // every lane owns a tile slot
-  static constexpr int RS = (N % 2) ? N + 1 : N;    // 16-B aligned rows
+  static constexpr int RS = (PAD && N % 2) ? N + 1 : N;  // PAD: 16-B aligned rows
   static constexpr int ES = N * RS;
+  static constexpr int TILE_SLOTS = CHAIN_WAVES * EPW + (LW < WAVE ? 1 : 0);
+  __device__ static int slot(int wave, int k, bool in_wave) {
+    return in_wave ? wave * EPW + k : CHAIN_WAVES * EPW;
+  }
 };
 
+// Row pass on a wave-private tile: the lane's row j (written column-wise by
+// the wave and synchronised) is contracted with D (or D^T when TR) and
+// written back, so the tile again holds the result in column layout.  REL
+// differentiates relative to the row's first entry (see poisson_group_nodal).
+template <int N, int RS, bool TR, bool REL>
+__device__ __forceinline__ void row_pass(double* L, int j, const DEO<N>& D) {
+  double r[RS], x[N], t[N];
+  load_row<N, RS>(L, j, r);
+#pragma unroll
+  for (int q = 0; q < N; ++q) x[q] = REL ? r[q] - r[0] : r[q];
+  if constexpr (TR)
+    deo_apply_t<N>(D, x, t);
+  else
+    deo_apply<N>(D, x, t);
+  wave_sync();
+  store_row<N, RS>(L, j, t);
+  wave_sync();
+}
+
 // ---------------------------------------------------------------------------
-// One group of the Poisson action: returns y_e[p][j] (p = 0..N-1) of the
-// lane's column j in v[], and the raw coded map entries in raw[].
+// One group of the Poisson action with STORED factors: returns y_e[p][j]
+// (p = 0..N-1) of the lane's column j in v[], and the raw coded map entries.
 //   mapP[g][r][k*N + j] = map[e][r][j] | code,  GP[g][c][r][k*N + j] = G_c(e; r, j)
 // ---------------------------------------------------------------------------
 template <int N>
-__device__ __forceinline__ void poisson_group(const uint32_t* __restrict__ mapP,
-                                              const double* __restrict__ GP,
-                                              const double* __restrict__ u, int64_t g, int lane,
-                                              int j, bool in_wave, double* L, const DMat<N>& D,
-                                              uint32_t (&raw)[N], double (&v)[N]) {
-  using T = Tile<N>;
+__device__ __forceinline__ void poisson_group_stored(const uint32_t* __restrict__ mapP,
+                                                     const double* __restrict__ GP,
+                                                     const double* __restrict__ u, int64_t g,
+                                                     int lane, int j, bool in_wave, double* L,
+                                                     const DEO<N>& D, uint32_t (&raw)[N],
+                                                     double (&v)[N]) {
+  using T = Tile<N, SEM_TILE_PAD_STORED>;
   constexpr int LW = T::LW;
   constexpr int RS = T::RS;
   const uint32_t* mp = mapP + g * (int64_t)(N * LW) + lane;
@@ -170,40 +315,19 @@ __device__ __forceinline__ void poisson_group(const uint32_t* __restrict__ mapP,
   }
   // column j: d0[m][j] = sum_r D[m][r] u[r][j]     (TensorProduct.deriv dim 0)
   double d0[N];
-#pragma unroll
-  for (int m = 0; m < N; ++m) {
-    double a = 0.0;
-#pragma unroll
-    for (int r = 0; r < N; ++r) a = fma(D.v[m * N + r], uc[r], a);
-    d0[m] = a;
-  }
+  deo_apply<N>(D, uc, d0);
 #pragma unroll
   for (int r = 0; r < N; ++r) L[r * RS + j] = uc[r];
   wave_sync();
   // row i = j: d1[i][q] = sum_s D[q][s] u[i][s]     (TensorProduct.deriv dim 1)
-  double t[N];
-  {
-    double ur[RS];
-    load_row<N, RS>(L, j, ur);
-#pragma unroll
-    for (int q = 0; q < N; ++q) {
-      double a = 0.0;
-#pragma unroll
-      for (int s = 0; s < N; ++s) a = fma(D.v[q * N + s], ur[s], a);
-      t[q] = a;
-    }
-  }
-  wave_sync();
-  store_row<N, RS>(L, j, t);
-  wave_sync();
-  // column j: geometric factors, w0/w1, and ya = D^T w0 along xi0 (kept in v)
-  double w1[N];
+  row_pass<N, RS, false, false>(L, j, D);
+  // column j: w0/w1, and ya = D^T w0 along xi0 (kept in v); w1 -> tile
   {
     double w0[N];
 #pragma unroll
     for (int m = 0; m < N; ++m) {
       const double d1 = L[m * RS + j];
-#ifdef SEM_DIAG_NO_G
+#if defined(SEM_DIAG_NO_G)
       const double g00 = 1.0 + m, g01 = 0.25 * j, g11 = 2.0;  // timing-only
 #else
       const double g00 = gp[(0 * N + m) * LW];
@@ -211,38 +335,155 @@ __device__ __forceinline__ void poisson_group(const uint32_t* __restrict__ mapP,
       const double g11 = gp[(2 * N + m) * LW];
 #endif
       w0[m] = fma(g00, d0[m], g01 * d1);
-      w1[m] = fma(g01, d0[m], g11 * d1);
+      L[m * RS + j] = fma(g01, d0[m], g11 * d1);  // w1, same lane's slot
     }
-#pragma unroll
-    for (int p = 0; p < N; ++p) {
-      double a = 0.0;
-#pragma unroll
-      for (int m = 0; m < N; ++m) a = fma(D.v[m * N + p], w0[m], a);
-      v[p] = a;
-    }
+    deo_apply_t<N>(D, w0, v);
   }
-  wave_sync();
-#pragma unroll
-  for (int m = 0; m < N; ++m) L[m * RS + j] = w1[m];
   wave_sync();
   // row i = j: yb[i][q] = sum_n D[n][q] w1[i][n]
-  {
-    double wr[RS];
-    load_row<N, RS>(L, j, wr);
-#pragma unroll
-    for (int q = 0; q < N; ++q) {
-      double a = 0.0;
-#pragma unroll
-      for (int nn = 0; nn < N; ++nn) a = fma(D.v[nn * N + q], wr[nn], a);
-      t[q] = a;
-    }
-  }
-  wave_sync();
-  store_row<N, RS>(L, j, t);
-  wave_sync();
+  row_pass<N, RS, true, false>(L, j, D);
 #pragma unroll
   for (int p = 0; p < N; ++p) v[p] += L[p * RS + j];
   wave_sync();  // the tile is rewritten by the next group of this wave
+}
+
+// 1/x to full double precision without the IEEE division sequence:
+// hardware reciprocal + two Newton steps (x is a Jacobian determinant, far
+// from 0 and from the denormal range once sem_geom_from_nodes accepted it).
+__device__ __forceinline__ double fast_rcp(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
+
+// ---------------------------------------------------------------------------
+// One group of the Poisson action with NODAL geometry: the factors of the
+// lane's column are re-derived from the GLL node coordinates XG[gid] =
+// x_phys, the reference's own per-element order of work (sem/discrete.py:
+// 189-209 -> sem/mapping.py:105-119 -> sem/linalg.py:105-115, detJxW
+// sem/discrete.py:594-597):
+//   J = [[dx/dr, dx/ds], [dy/dr, dy/ds]] (r = xi0 along the column, s = xi1),
+//   G00 = W (J11^2 + J01^2)/det, G01 = -W (J11 J10 + J01 J00)/det,
+//   G11 = W (J10^2 + J00^2)/det,   W = w_m w_j,
+// i.e. detJxW * invJ invJ^T.  Every line of coordinates is differentiated
+// relative to its first node (D annihilates constants), so O(1) coordinates
+// do not cancel against O(h) differences.  Tiles: A (x, then u, then w1)
+// and B (y).  Measured at p = 8: this order (factors first, x and y
+// transposed together) beats the fully fused order (u/x/y/w1 one tile pass
+// each, no factor arrays): 0.684 vs 0.714 ms.
+// ---------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void poisson_group_nodal(const uint32_t* __restrict__ mapP,
+                                                    const double2* __restrict__ XG,
+                                                    const double* __restrict__ u, int64_t g,
+                                                    int lane, int j, bool in_wave, double* A,
+                                                    double* B, const DEO<N>& D,
+                                                    const WVec<N>& w, double wj,
+                                                    uint32_t (&raw)[N], double (&v)[N]) {
+  using T = Tile<N, SEM_TILE_PAD_NODAL>;
+  constexpr int LW = T::LW;
+  constexpr int RS = T::RS;
+  const uint32_t* mp = mapP + g * (int64_t)(N * LW) + lane;
+  double uc[N];
+  double2 xc[N];
+#pragma unroll
+  for (int r = 0; r < N; ++r) raw[r] = in_wave ? mp[r * LW] : (W_SKIP << CODE_SHIFT);
+#pragma unroll
+  for (int r = 0; r < N; ++r) {
+#ifdef SEM_DIAG_NO_X
+    xc[r] = make_double2(0.01 * (raw[r] & 15u) + j, 0.02 * r + (raw[r] & 3u));  // timing-only
+#else
+    xc[r] = XG[raw[r] & GID_MASK];
+#endif
+  }
+#if SEM_NODAL_EARLY_U
+#pragma unroll
+  for (int r = 0; r < N; ++r) uc[r] = u[raw[r] & GID_MASK];
+#endif
+  // geometry: (dx/dr, dy/dr) along the column, (dx/ds, dy/ds) along the row;
+  // G11 is parked in tile B (free after the geometry) to save registers
+  double g00[N], g01[N];
+  {
+    double jr0[N], jr1[N];
+    {
+      double ta[N], tb[N];
+#pragma unroll
+      for (int r = 0; r < N; ++r) {
+        ta[r] = xc[r].x - xc[0].x;
+        tb[r] = xc[r].y - xc[0].y;
+      }
+      deo_apply<N>(D, ta, jr0);
+      deo_apply<N>(D, tb, jr1);
+    }
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      A[r * RS + j] = xc[r].x;
+      B[r * RS + j] = xc[r].y;
+    }
+    wave_sync();
+#if !SEM_NODAL_EARLY_U
+    // issued here, after an ordering point: its latency hides behind the
+    // geometry without holding registers through the column phase
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+#ifdef SEM_DIAG_NO_U
+      uc[r] = (double)(raw[r] & 7u);  // timing-only: no u gather
+#else
+      uc[r] = u[raw[r] & GID_MASK];
+#endif
+    }
+#endif
+    {
+      double xa[RS], xb[RS], ra[N], rb[N], ta[N], tb[N];
+      load_row<N, RS>(A, j, xa);
+      load_row<N, RS>(B, j, xb);
+#pragma unroll
+      for (int q = 0; q < N; ++q) {
+        ra[q] = xa[q] - xa[0];
+        rb[q] = xb[q] - xb[0];
+      }
+      deo_apply<N>(D, ra, ta);
+      deo_apply<N>(D, rb, tb);
+      wave_sync();
+      store_row<N, RS>(A, j, ta);
+      store_row<N, RS>(B, j, tb);
+    }
+    wave_sync();
+#pragma unroll
+    for (int m = 0; m < N; ++m) {
+      const double js0 = A[m * RS + j], js1 = B[m * RS + j];
+      const double det = jr0[m] * js1 - js0 * jr1[m];
+      const double sc = (w.v[m] * wj) * fast_rcp(det);
+      g00[m] = sc * fma(js1, js1, js0 * js0);
+      g01[m] = -sc * fma(js1, jr1[m], js0 * jr0[m]);
+      B[m * RS + j] = sc * fma(jr1[m], jr1[m], jr0[m] * jr0[m]);  // G11, own slot
+    }
+    wave_sync();  // tile A is rewritten next
+  }
+  // the Laplacian on tile A, as in poisson_group_stored
+  double d0[N];
+  deo_apply<N>(D, uc, d0);
+#pragma unroll
+  for (int r = 0; r < N; ++r) A[r * RS + j] = uc[r];
+  wave_sync();
+  row_pass<N, RS, false, false>(A, j, D);
+  {
+    double w0[N];
+#pragma unroll
+    for (int m = 0; m < N; ++m) {
+      const double d1 = A[m * RS + j];
+      w0[m] = fma(g00[m], d0[m], g01[m] * d1);
+      A[m * RS + j] = fma(g01[m], d0[m], B[m * RS + j] * d1);
+    }
+    deo_apply_t<N>(D, w0, v);
+  }
+  wave_sync();
+  row_pass<N, RS, true, false>(A, j, D);
+#pragma unroll
+  for (int p = 0; p < N; ++p) v[p] += A[p * RS + j];
+  wave_sync();  // the tiles are rewritten by the next group of this wave
 }
 
 // Scatter of one group's column values through the coded map, with the
@@ -261,6 +502,7 @@ __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_
       const double vn = __shfl_down(v[c][p], 1, WAVE);
       if ((raw[p] >> CODE_SHIFT) & W_MERGE) v[c][p] += vn;
     }
+#ifndef SEM_DIAG_NO_SYNC
   // hand the last lane's column to the next group of the chain
   if (lane == LW - 1) {
 #pragma unroll
@@ -279,6 +521,7 @@ __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_
         for (int c = 0; c < NC; ++c) v[c][p] += src[c * N + p];
       }
   }
+#endif
   if (in_wave) {
 #pragma unroll
     for (int p = 0; p < N; ++p) {
@@ -288,20 +531,24 @@ __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_
         emit2(y, raw[p], v[0][p], v[NC - 1][p], accumulate);
     }
   }
+#ifndef SEM_DIAG_NO_SYNC
   // this round's stores and carry reads complete before the next round
   __syncthreads();
+#endif
 }
 
 // ---------------------------------------------------------------------------
 // Poisson stiffness action: one workgroup per chain, chains [c0, c1).
 // ---------------------------------------------------------------------------
-template <int N>
+template <int N, bool NODAL>
 __global__ void __launch_bounds__(CHAIN_BLOCK, SEM_POISSON_MIN_WAVES)
     k_poisson_apply(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
-                    const double* __restrict__ u, double* __restrict__ y, int64_t c0, int64_t c1,
-                    int rounds, int accumulate, const DMat<N> D) {
-  using T = Tile<N>;
-  __shared__ __attribute__((aligned(16))) double lds[CHAIN_WAVES * T::SLOTS * T::ES];
+                    const double2* __restrict__ XG, const double* __restrict__ u,
+                    double* __restrict__ y, int64_t c0, int64_t c1, int rounds, int accumulate,
+                    const DEO<N> D, const WVec<N> w) {
+  using T = Tile<N, NODAL ? SEM_TILE_PAD_NODAL : SEM_TILE_PAD_STORED>;
+  constexpr int NT = NODAL ? 2 : 1;  // tiles per element slot
+  __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * T::ES * NT];
   __shared__ double carry[2][CHAIN_WAVES][1][N];
   const int64_t chain = c0 + blockIdx.x;
   if (chain >= c1) return;  // uniform over the workgroup
@@ -310,12 +557,17 @@ __global__ void __launch_bounds__(CHAIN_BLOCK, SEM_POISSON_MIN_WAVES)
   const int k = lane / N;
   const int j = lane - k * N;
   const bool in_wave = lane < T::LW;
-  double* L = lds + (wave * T::SLOTS + k) * T::ES;
+  double* L = lds + T::slot(wave, k, in_wave) * T::ES * NT;
+  double* LB = L + (NT - 1) * T::ES;
+  const double wj = pick<N>(w, j);
   for (int rd = 0; rd < rounds; ++rd) {
     const int64_t g = (chain * rounds + rd) * CHAIN_WAVES + wave;
     uint32_t raw[N];
     double v[1][N];
-    poisson_group<N>(mapP, GP, u, g, lane, j, in_wave, L, D, raw, v[0]);
+    if constexpr (NODAL)
+      poisson_group_nodal<N>(mapP, XG, u, g, lane, j, in_wave, L, LB, D, w, wj, raw, v[0]);
+    else
+      poisson_group_stored<N>(mapP, GP, u, g, lane, j, in_wave, L, D, raw, v[0]);
 #ifdef SEM_DIAG_NO_STORE
     if (in_wave && v[0][0] == 1234.5678) y[0] = v[0][1];  // timing-only
 #else
@@ -336,7 +588,7 @@ __device__ __forceinline__ void axisym_group(const uint32_t* __restrict__ mapP,
                                              const double* __restrict__ GP,
                                              const double* __restrict__ u, int64_t g, int lane,
                                              int j, bool in_wave, double* LP, double* LO,
-                                             const DMat<N>& D, uint32_t (&raw)[N],
+                                             const DEO<N>& D, uint32_t (&raw)[N],
                                              double (&vo)[N], double (&vp)[N]) {
   using T = Tile<N>;
   constexpr int LW = T::LW;
@@ -354,17 +606,8 @@ __device__ __forceinline__ void axisym_group(const uint32_t* __restrict__ mapP,
     om[r] = val.y;
   }
   double d0p[N], d0o[N];
-#pragma unroll
-  for (int m = 0; m < N; ++m) {
-    double a = 0.0, b = 0.0;
-#pragma unroll
-    for (int r = 0; r < N; ++r) {
-      a = fma(D.v[m * N + r], ps[r], a);
-      b = fma(D.v[m * N + r], om[r], b);
-    }
-    d0p[m] = a;
-    d0o[m] = b;
-  }
+  deo_apply<N>(D, ps, d0p);
+  deo_apply<N>(D, om, d0o);
 #pragma unroll
   for (int r = 0; r < N; ++r) {
     LP[r * RS + j] = ps[r];
@@ -373,20 +616,16 @@ __device__ __forceinline__ void axisym_group(const uint32_t* __restrict__ mapP,
   wave_sync();
   {
     double tp[N], to[N];
-    double rp[RS], ro[RS];
+    double rp[RS], ro[RS], xp[N], xo[N];
     load_row<N, RS>(LP, j, rp);
     load_row<N, RS>(LO, j, ro);
 #pragma unroll
     for (int q = 0; q < N; ++q) {
-      double a = 0.0, b = 0.0;
-#pragma unroll
-      for (int s = 0; s < N; ++s) {
-        a = fma(D.v[q * N + s], rp[s], a);
-        b = fma(D.v[q * N + s], ro[s], b);
-      }
-      tp[q] = a;
-      to[q] = b;
+      xp[q] = rp[q];
+      xo[q] = ro[q];
     }
+    deo_apply<N>(D, xp, tp);
+    deo_apply<N>(D, xo, to);
     wave_sync();
     store_row<N, RS>(LP, j, tp);
     store_row<N, RS>(LO, j, to);
@@ -415,16 +654,12 @@ __device__ __forceinline__ void axisym_group(const uint32_t* __restrict__ mapP,
       d0p[m] = fma(b0, d0p[m], fma(b1, d1p, -mm * om[m]));
       d0o[m] = c * om[m];
     }
+    deo_apply_t<N>(D, w0p, vp);
+    deo_apply_t<N>(D, w0o, vo);
 #pragma unroll
     for (int p = 0; p < N; ++p) {
-      double a = 0.0, b = 0.0;
-#pragma unroll
-      for (int m = 0; m < N; ++m) {
-        a = fma(D.v[m * N + p], w0p[m], a);
-        b = fma(D.v[m * N + p], w0o[m], b);
-      }
-      vp[p] = a + d0p[p];
-      vo[p] = b + d0o[p];
+      vp[p] += d0p[p];
+      vo[p] += d0o[p];
     }
   }
   wave_sync();
@@ -436,20 +671,16 @@ __device__ __forceinline__ void axisym_group(const uint32_t* __restrict__ mapP,
   wave_sync();
   {
     double tp[N], to[N];
-    double rp[RS], ro[RS];
+    double rp[RS], ro[RS], xp[N], xo[N];
     load_row<N, RS>(LP, j, rp);
     load_row<N, RS>(LO, j, ro);
 #pragma unroll
     for (int q = 0; q < N; ++q) {
-      double a = 0.0, b = 0.0;
-#pragma unroll
-      for (int nn = 0; nn < N; ++nn) {
-        a = fma(D.v[nn * N + q], rp[nn], a);
-        b = fma(D.v[nn * N + q], ro[nn], b);
-      }
-      tp[q] = a;
-      to[q] = b;
+      xp[q] = rp[q];
+      xo[q] = ro[q];
     }
+    deo_apply_t<N>(D, xp, tp);
+    deo_apply_t<N>(D, xo, to);
     wave_sync();
     store_row<N, RS>(LP, j, tp);
     store_row<N, RS>(LO, j, to);
@@ -467,9 +698,9 @@ template <int N>
 __global__ void __launch_bounds__(CHAIN_BLOCK)
     k_axisym_apply(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
                    const double* __restrict__ u, double* __restrict__ y, int64_t c0, int64_t c1,
-                   int rounds, int accumulate, const DMat<N> D) {
+                   int rounds, int accumulate, const DEO<N> D) {
   using T = Tile<N>;
-  __shared__ __attribute__((aligned(16))) double lds[CHAIN_WAVES * T::SLOTS * 2 * T::ES];
+  __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * 2 * T::ES];
   __shared__ double carry[2][CHAIN_WAVES][2][N];
   const int64_t chain = c0 + blockIdx.x;
   if (chain >= c1) return;
@@ -478,7 +709,7 @@ __global__ void __launch_bounds__(CHAIN_BLOCK)
   const int k = lane / N;
   const int j = lane - k * N;
   const bool in_wave = lane < T::LW;
-  double* LP = lds + (wave * T::SLOTS + k) * 2 * T::ES;  // psi tile
+  double* LP = lds + T::slot(wave, k, in_wave) * 2 * T::ES;  // psi tile
   double* LO = LP + T::ES;                               // omega tile
   for (int rd = 0; rd < rounds; ++rd) {
     const int64_t g = (chain * rounds + rd) * CHAIN_WAVES + wave;
@@ -507,7 +738,8 @@ __global__ void __launch_bounds__(GeomShape<N>::THREADS)
                const double* __restrict__ gw, int op_kind, const int* __restrict__ gpos,
                double* __restrict__ GP, double* __restrict__ xph, double* __restrict__ Jo,
                double* __restrict__ iJo, double* __restrict__ dJo, double* __restrict__ dJW,
-               unsigned long long* __restrict__ n_bad) {
+               double2* __restrict__ XG, const uint32_t* __restrict__ owner,
+               const double2* __restrict__ XGin, unsigned long long* __restrict__ n_bad) {
   using S = GeomShape<N>;
   constexpr int NN = S::NN;
   constexpr int EPB = S::EPB;
@@ -527,10 +759,17 @@ __global__ void __launch_bounds__(GeomShape<N>::THREADS)
   const int nq = node - m * N;
   const int64_t e = (int64_t)blockIdx.x * EPB + el;
   const bool act = (el < EPB) && (e < n_elem);
+  uint32_t gi = 0;
   if (act) {
-    const uint32_t gi = e2n[e * NN + node];
-    sx[el][0][node] = nodes[gi];
-    sx[el][1][node] = nodes[n_node + gi];
+    gi = e2n[e * NN + node];
+    if (XGin) {  // x_phys already known per global node (NODAL mode re-derivation)
+      const double2 xg = XGin[gi];
+      sx[el][0][node] = xg.x;
+      sx[el][1][node] = xg.y;
+    } else {
+      sx[el][0][node] = nodes[gi];
+      sx[el][1][node] = nodes[n_node + gi];
+    }
   }
   __syncthreads();
   // x_phys = Vinv X Vinv^T   (compute_coeffs_grid_eq: dim 0 then dim 1),
@@ -538,7 +777,7 @@ __global__ void __launch_bounds__(GeomShape<N>::THREADS)
   // is translation invariant (V_eq reproduces constants) and J = D x_phys
   // then no longer cancels the O(1) offset against O(h) variations.
   double x0[2] = {0.0, 0.0};
-  if (act) {
+  if (act && !XGin) {
     x0[0] = sx[el][0][0];
     x0[1] = sx[el][1][0];
     for (int c = 0; c < 2; ++c) {
@@ -549,7 +788,12 @@ __global__ void __launch_bounds__(GeomShape<N>::THREADS)
   }
   __syncthreads();
   double xp[2] = {0.0, 0.0};
-  if (act) {
+  if (act && XGin) {
+    x0[0] = sx[el][0][0];
+    x0[1] = sx[el][1][0];
+    xp[0] = sx[el][0][node] - x0[0];
+    xp[1] = sx[el][1][node] - x0[1];
+  } else if (act) {
     for (int c = 0; c < 2; ++c) {
       double a = 0.0;
       for (int jj = 0; jj < N; ++jj) a = fma(sV[nq * N + jj], st[el][c][m * N + jj], a);
@@ -585,6 +829,10 @@ __global__ void __launch_bounds__(GeomShape<N>::THREADS)
   const int64_t base = e * NN + node;
   const double xabs0 = xp[0] + x0[0];
   const double xabs1 = xp[1] + x0[1];
+  // x_phys per global node, written by the node's first element only (the
+  // copies of a shared node differ in rounding; one writer keeps it
+  // deterministic)
+  if (XG && owner[gi] == (uint32_t)e) XG[gi] = make_double2(xabs0, xabs1);
   if (xph) {
     xph[(e * 2 + 0) * NN + node] = xabs0;
     xph[(e * 2 + 1) * NN + node] = xabs1;

@@ -79,9 +79,20 @@ class SEMOperator(object):
         axisymmetric Stokes block.
     basis : TensorProductQS, optional
     device : torch.device or str, optional
+    geometry : {"nodal", "stored"}
+        How the Poisson action gets its geometric factors: re-derived per
+        quadrature node from x_phys per global node ("nodal", default, least
+        HBM traffic) or streamed from precomputed per-element factors
+        ("stored").  See include/sem_hip.h sem_set_geom_mode.
     """
 
-    def __init__(self, p, e2n, nodes, dofs_per_node=1, basis=None, device=None):
+    GEOMETRY_MODES = {"stored": _lib.GEOM_STORED, "nodal": _lib.GEOM_NODAL}
+
+    def __init__(self, p, e2n, nodes, dofs_per_node=1, basis=None, device=None,
+                 geometry="nodal"):
+        if geometry not in self.GEOMETRY_MODES:
+            raise ValueError("geometry must be one of %s" % sorted(self.GEOMETRY_MODES))
+        self.geometry = geometry
         self._lib = _lib.load()
         self.p = int(p)
         self.n = self.p + 1
@@ -105,6 +116,7 @@ class SEMOperator(object):
             _lib.check(self._lib.sem_ctx_create(C.byref(ctx), self.p, self.n_elem, self.n_node,
                                                 self.dpn, dev))
             self._ctx = ctx
+            _lib.check(self._lib.sem_set_geom_mode(ctx, self.GEOMETRY_MODES[geometry]))
             _lib.check(self._lib.sem_set_basis(ctx, _lib.dptr(self.D), _lib.dptr(self.w)))
             _lib.check(self._lib.sem_set_map(ctx, _lib.tptr(self.e2n), _lib.stream_ptr()))
         self._geom_ready = set()

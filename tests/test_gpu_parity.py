@@ -26,9 +26,13 @@ def sem():
     return operators
 
 
-def make_op(sem, fx, name, dpn=1):
+GEOMETRY = ["nodal", "stored"]
+
+
+def make_op(sem, fx, name, dpn=1, geometry="nodal"):
     p = int(fx[name + "_p"])
-    return sem.SEMOperator(p, fx[name + "_e2n"], fx[name + "_nodes"], dofs_per_node=dpn)
+    return sem.SEMOperator(p, fx[name + "_e2n"], fx[name + "_nodes"], dofs_per_node=dpn,
+                           geometry=geometry)
 
 
 def assert_parity(y, y_ref, y_ext, tol):
@@ -47,10 +51,11 @@ def assert_parity(y, y_ref, y_ext, tol):
     assert e_ref <= 2.0 * e_refx + tol, (e_ref, e_refx)
 
 
+@pytest.mark.parametrize("geometry", GEOMETRY)
 @pytest.mark.parametrize("name", ACTION_CASES)
-def test_poisson_action_golden(sem, poisson_action, gll, name):
+def test_poisson_action_golden(sem, poisson_action, gll, name, geometry):
     import sem_oracle
-    op = make_op(sem, poisson_action, name)
+    op = make_op(sem, poisson_action, name, geometry=geometry)
     u = torch.from_numpy(poisson_action[name + "_u"]).cuda()
     y = op.apply(u).cpu().numpy()
     p = int(poisson_action[name + "_p"])
@@ -116,7 +121,8 @@ def test_axisym_components_golden(sem, axisym_action):
     assert rel_l2(-y[1::2], axisym_action[name + "_Me_omega"]) < TOL_AXISYM
 
 
-def test_poisson_vs_oracle_larger(sem, gll):
+@pytest.mark.parametrize("geometry", GEOMETRY)
+def test_poisson_vs_oracle_larger(sem, gll, geometry):
     """128 x 96 warped mesh at p = 8 vs the batched NumPy oracle (and the
     extended-precision oracle: small elements make J = D x_phys cancel
     O(1) coordinates against O(h) variations in the reference algorithm)."""
@@ -126,7 +132,7 @@ def test_poisson_vs_oracle_larger(sem, gll):
     nodes, e2n = meshgen.structured_square(128, 96, p, warp=0.05)
     prob = sem_oracle.PoissonProblem(nodes, e2n, gll["half_%d" % p], batched_geometry=True)
     u = np.random.default_rng(5).standard_normal(prob.ndof)
-    op = sem.SEMOperator(p, e2n, nodes)
+    op = sem.SEMOperator(p, e2n, nodes, geometry=geometry)
     y = op.apply(torch.from_numpy(u).cuda()).cpu().numpy()
     y_ext = sem_oracle.poisson_apply_extended(nodes, e2n, gll["half_%d" % p], u)
     assert_parity(y, prob.apply(u), y_ext, TOL_ACTION)
@@ -171,6 +177,23 @@ def test_properties_full_size(sem):
     # repeated application agrees (atomics may reorder fp adds: <= 1e-14)
     Ku2 = op.apply(u)
     assert (Ku2 - Ku).norm().item() <= 1e-14 * Ku.norm().item()
+
+
+def test_nodal_vs_stored_full_size(sem):
+    """The two geometry modes agree at 16.8M DOF (they differ only in where
+    x_phys is rounded to absolute coordinates)."""
+    from spectralelementmethod_amd import meshgen
+    p = 8
+    nodes, e2n = meshgen.structured_square(512, 512, p, warp=0.05)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    ys = []
+    for geometry in GEOMETRY:
+        op = sem.SEMOperator(p, e2n, nodes, geometry=geometry)
+        u = torch.randn(op.ndof, dtype=torch.float64, device="cuda",
+                        generator=g.manual_seed(3))
+        ys.append(op.apply(u))
+        del op
+    assert (ys[0] - ys[1]).norm().item() < 1e-11 * ys[1].norm().item()
 
 
 def test_detj_nonpositive_raises(sem, poisson_action):
