@@ -125,8 +125,9 @@ def main():
     ap.add_argument("--ney", type=int, default=1024)
     ap.add_argument("--warp", type=float, default=0.05)
     ap.add_argument("--op", choices=["poisson", "axisym_stokes"], default="poisson")
-    ap.add_argument("--geometry", choices=["nodal", "stored"], default="nodal",
-                    help="Poisson geometric factors: re-derived from x_phys per node, or streamed")
+    ap.add_argument("--geometry", choices=["auto", "nodal", "stored"], default="auto",
+                    help="Poisson geometric factors: re-derived from x_phys per node, or "
+                         "streamed; auto = nodal for p <= 8 (the library's default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--traffic-json", default=None,
@@ -161,6 +162,8 @@ def main():
                                                           time.time() - t0))
     geometry = args.geometry if kind == POISSON else "stored"
     op = SEMOperator(p, e2n, nodes, dofs_per_node=dpn, device=dev, geometry=geometry)
+    if geometry == "auto":  # as resolved by the library (SEM_GEOM_AUTO)
+        geometry = "nodal" if p <= 8 else "stored"
     op.compute_geometry(kind)
     plan = op.plan_info()
     log("rank %d: plan %s" % (rank, plan))

@@ -111,7 +111,10 @@ int sem_set_map(sem_ctx* ctx, const uint32_t* d_e2n, void* stream);
 int sem_plan_info(sem_ctx* ctx, int64_t* info, int n_info);
 
 /* How the Poisson action obtains its geometric factors.
- *  SEM_GEOM_NODAL (default): sem_geom_from_nodes keeps x_phys per global node
+ *  SEM_GEOM_AUTO (default): NODAL for p <= 8, STORED above (measured on
+ *    MI355X at ~10^7 DOF: NODAL wins at p = 2, 4, 8, STORED at p = 12, 16
+ *    where the nodal kernel's register demand halves occupancy).
+ *  SEM_GEOM_NODAL: sem_geom_from_nodes keeps x_phys per global node
  *    (16 B/node) and the action re-derives J, det, invJ and detJxW at every
  *    quadrature node from it -- the reference's own order of work, which
  *    recomputes the geometry inside the element loop (sem/discrete.py:189-209,
@@ -122,6 +125,7 @@ int sem_plan_info(sem_ctx* ctx, int64_t* info, int n_info);
  * stored factors.  The axisymmetric block always uses stored factors. */
 #define SEM_GEOM_STORED 0
 #define SEM_GEOM_NODAL 1
+#define SEM_GEOM_AUTO 2
 int sem_set_geom_mode(sem_ctx* ctx, int mode);
 
 /* Geometry from mesh nodes (device, float64 [2][n_node]) for op_kind:

@@ -27,6 +27,7 @@ APPLY_ACCUMULATE = 1
 APPLY_SKIP_ZERO = 2
 GEOM_STORED = 0
 GEOM_NODAL = 1
+GEOM_AUTO = 2
 
 # every symbol include/sem_hip.h declares, with (restype, argtypes)
 _i64 = C.c_int64

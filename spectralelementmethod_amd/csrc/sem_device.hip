@@ -282,7 +282,7 @@ struct sem_ctx {
   bool conforming = true;
   double* d_GP[2] = {nullptr, nullptr};
   // NODAL geometry (Poisson): x_phys per global node + the node's first element
-  int geom_mode = SEM_GEOM_NODAL;
+  int geom_mode = SEM_GEOM_AUTO;
   double2* d_XG = nullptr;
   uint32_t* d_owner = nullptr;
   bool xg_valid = false;
@@ -329,8 +329,12 @@ DEO<N> make_deo(const double* h) {
 
 // the Poisson action recomputes its factors from x_phys per node (NODAL)
 // unless the stored-factor mode was chosen or the caller supplied factors
+bool nodal_mode(const sem_ctx* c) {
+  return c->geom_mode == SEM_GEOM_NODAL || (c->geom_mode == SEM_GEOM_AUTO && c->n <= 9);
+}
+
 bool use_nodal(const sem_ctx* c, int op_kind) {
-  return op_kind == SEM_OP_POISSON && c->geom_mode == SEM_GEOM_NODAL && c->xg_valid;
+  return op_kind == SEM_OP_POISSON && nodal_mode(c) && c->xg_valid;
 }
 
 template <int N>
@@ -447,7 +451,8 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
                int rounds, Plan& P) {
   const int epw = WAVE / n, lw = epw * n, nn = n * n;
   const int64_t n_groups = (n_elem + epw - 1) / epw;
-  const int CH = CHAIN_WAVES * rounds;
+  const int CW = CHAIN_WAVES;  // groups of a chain that run concurrently
+  const int CH = CW * rounds;
   const int64_t n_chains = (n_groups + CH - 1) / CH;
   auto is_bnd = [n](int r, int jj) { return r == 0 || r == n - 1 || jj == 0 || jj == n - 1; };
   // references and conformity (interior local nodes must be unique)
@@ -552,7 +557,7 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
             const int tag = i * n * lw + pos;
             if (lastc[gid] == ch) {
               const int pi = lastt[gid] / (n * lw), ppos = lastt[gid] % (n * lw);
-              const bool same_round = (pi / CHAIN_WAVES) == (i / CHAIN_WAVES);
+              const bool same_round = (pi / CW) == (i / CW);
               if (pi == i && lane > 0 && ppos == pos - 1 && jj == 0 && (ppos % lw) % n == n - 1) {
                 act[tag] = 1;  // merge into lane L (pos-1)
               } else if (pi == i - 1 && lane == 0 && ppos == r * lw + lw - 1) {
@@ -638,7 +643,7 @@ int sem_ctx_create(sem_ctx** out, int p, int64_t n_elem, int64_t n_node, int dpn
   c->epw = epw_of(c->n);
   c->lw = c->epw * c->n;
   c->n_groups = (n_elem + c->epw - 1) / c->epw;
-  if (const char* s = std::getenv("SEM_GEOM_MODE")) c->geom_mode = std::atoi(s) ? 1 : 0;
+  if (const char* s = std::getenv("SEM_GEOM_MODE")) c->geom_mode = std::atoi(s);
   if (c->n_groups > 0x7FFFFFFFll) {
     delete c;
     return fail(SEM_E_INVALID, "too many elements");
@@ -697,7 +702,10 @@ int sem_set_map(sem_ctx* c, const uint32_t* d_e2n, void* stream) {
   HIP_TRY(hipStreamSynchronize(st));
   Plan P;
   // measured on MI355X at p = 8, 10^6 elements: 1 round 0.79-0.81 ms,
-  // 2: 0.85, 4: 0.88, 8: 0.97 (longer chains: fewer workgroups, lockstep)
+  // 2: 0.85, 4: 0.88, 8: 0.97 (longer chains: fewer workgroups, lockstep).
+  // Single-wave chains (no workgroup barrier, register carry, next-group
+  // prefetch) measured 0.90-0.95 ms (nodal) and 0.89-0.92 (stored): the
+  // prefetch registers halve occupancy.  Not kept.
   int rounds = 1;
   if (const char* s = std::getenv("SEM_CHAIN_ROUNDS")) rounds = std::max(1, std::atoi(s));
   int rc = build_plan(h, c->n_elem, c->n_node, n, rounds, P);
@@ -761,7 +769,7 @@ static int geom_common(sem_ctx* c, const double* d_nodes, const double* h_Vinv) 
 
 int sem_set_geom_mode(sem_ctx* c, int mode) {
   if (!c) return fail(SEM_E_INVALID, "null ctx");
-  if (mode != SEM_GEOM_STORED && mode != SEM_GEOM_NODAL)
+  if (mode != SEM_GEOM_STORED && mode != SEM_GEOM_NODAL && mode != SEM_GEOM_AUTO)
     return fail(SEM_E_INVALID, "unknown geometry mode " + std::to_string(mode));
   c->geom_mode = mode;
   return SEM_OK;
@@ -774,7 +782,7 @@ int sem_geom_from_nodes(sem_ctx* c, const double* d_nodes, const double* h_Vinv,
   int rc = geom_common(c, d_nodes, h_Vinv);
   if (rc) return rc;
   if ((rc = check_op(c, op_kind))) return rc;
-  const bool nodal = op_kind == SEM_OP_POISSON && c->geom_mode == SEM_GEOM_NODAL;
+  const bool nodal = op_kind == SEM_OP_POISSON && nodal_mode(c);
   double* GP = nullptr;
   if (nodal) {
     if (!c->d_XG) HIP_TRY(hipMalloc(&c->d_XG, c->n_node * sizeof(double2)));

@@ -239,14 +239,15 @@ __device__ __forceinline__ void store_row(double* L, int i, const double (&t)[N]
 // LDS tiles: one N x RS slot per element of a group; the padding lanes
 // (lane >= LW when N does not divide 64) of every wave share one scratch
 // slot whose contents are never used.
-// PAD: rows padded to 16 B for ds_read_b128 (odd N).  The nodal Poisson
-// kernel keeps two tiles per element slot and goes unpadded so that four
-// workgroups fit one CU's LDS at p = 8.
+// PAD: rows padded to 16 B for ds_read_b128 (odd N); p = 8 measured padded
+// vs unpadded: 0.704 vs 0.720 ms (nodal).  At N = 9, slot stride 90 doubles
+// and row stride 10 keep column and row accesses within 1.5x of conflict-free
+// (bank model of MI355X_MICROARCH.md §LDS).
 #ifndef SEM_TILE_PAD_STORED
 #define SEM_TILE_PAD_STORED 1
 #endif
 #ifndef SEM_TILE_PAD_NODAL
-#define SEM_TILE_PAD_NODAL 0
+#define SEM_TILE_PAD_NODAL 1
 #endif
 #ifndef SEM_NODAL_EARLY_U
 #define SEM_NODAL_EARLY_U 0
@@ -375,21 +376,17 @@ __device__ __forceinline__ double fast_rcp(double x) {
 // each, no factor arrays): 0.684 vs 0.714 ms.
 // ---------------------------------------------------------------------------
 template <int N>
-__device__ __forceinline__ void poisson_group_nodal(const uint32_t* __restrict__ mapP,
-                                                    const double2* __restrict__ XG,
-                                                    const double* __restrict__ u, int64_t g,
-                                                    int lane, int j, bool in_wave, double* A,
-                                                    double* B, const DEO<N>& D,
-                                                    const WVec<N>& w, double wj,
-                                                    uint32_t (&raw)[N], double (&v)[N]) {
-  using T = Tile<N, SEM_TILE_PAD_NODAL>;
-  constexpr int LW = T::LW;
-  constexpr int RS = T::RS;
+__device__ __forceinline__ void load_map(const uint32_t* __restrict__ mapP, int64_t g, int lane,
+                                         bool in_wave, uint32_t (&raw)[N]) {
+  constexpr int LW = Tile<N>::LW;
   const uint32_t* mp = mapP + g * (int64_t)(N * LW) + lane;
-  double uc[N];
-  double2 xc[N];
 #pragma unroll
   for (int r = 0; r < N; ++r) raw[r] = in_wave ? mp[r * LW] : (W_SKIP << CODE_SHIFT);
+}
+
+template <int N>
+__device__ __forceinline__ void gather_x(const double2* __restrict__ XG, const uint32_t (&raw)[N],
+                                         int j, double2 (&xc)[N]) {
 #pragma unroll
   for (int r = 0; r < N; ++r) {
 #ifdef SEM_DIAG_NO_X
@@ -398,71 +395,81 @@ __device__ __forceinline__ void poisson_group_nodal(const uint32_t* __restrict__
     xc[r] = XG[raw[r] & GID_MASK];
 #endif
   }
-#if SEM_NODAL_EARLY_U
+}
+
+template <int N>
+__device__ __forceinline__ void gather_u(const double* __restrict__ u, const uint32_t (&raw)[N],
+                                         double (&uc)[N]) {
 #pragma unroll
-  for (int r = 0; r < N; ++r) uc[r] = u[raw[r] & GID_MASK];
-#endif
-  // geometry: (dx/dr, dy/dr) along the column, (dx/ds, dy/ds) along the row;
-  // G11 is parked in tile B (free after the geometry) to save registers
-  double g00[N], g01[N];
-  {
-    double jr0[N], jr1[N];
-    {
-      double ta[N], tb[N];
-#pragma unroll
-      for (int r = 0; r < N; ++r) {
-        ta[r] = xc[r].x - xc[0].x;
-        tb[r] = xc[r].y - xc[0].y;
-      }
-      deo_apply<N>(D, ta, jr0);
-      deo_apply<N>(D, tb, jr1);
-    }
-#pragma unroll
-    for (int r = 0; r < N; ++r) {
-      A[r * RS + j] = xc[r].x;
-      B[r * RS + j] = xc[r].y;
-    }
-    wave_sync();
-#if !SEM_NODAL_EARLY_U
-    // issued here, after an ordering point: its latency hides behind the
-    // geometry without holding registers through the column phase
-#pragma unroll
-    for (int r = 0; r < N; ++r) {
+  for (int r = 0; r < N; ++r) {
 #ifdef SEM_DIAG_NO_U
-      uc[r] = (double)(raw[r] & 7u);  // timing-only: no u gather
+    uc[r] = (double)(raw[r] & 7u);  // timing-only: no u gather
 #else
-      uc[r] = u[raw[r] & GID_MASK];
+    uc[r] = u[raw[r] & GID_MASK];
 #endif
-    }
-#endif
-    {
-      double xa[RS], xb[RS], ra[N], rb[N], ta[N], tb[N];
-      load_row<N, RS>(A, j, xa);
-      load_row<N, RS>(B, j, xb);
-#pragma unroll
-      for (int q = 0; q < N; ++q) {
-        ra[q] = xa[q] - xa[0];
-        rb[q] = xb[q] - xb[0];
-      }
-      deo_apply<N>(D, ra, ta);
-      deo_apply<N>(D, rb, tb);
-      wave_sync();
-      store_row<N, RS>(A, j, ta);
-      store_row<N, RS>(B, j, tb);
-    }
-    wave_sync();
-#pragma unroll
-    for (int m = 0; m < N; ++m) {
-      const double js0 = A[m * RS + j], js1 = B[m * RS + j];
-      const double det = jr0[m] * js1 - js0 * jr1[m];
-      const double sc = (w.v[m] * wj) * fast_rcp(det);
-      g00[m] = sc * fma(js1, js1, js0 * js0);
-      g01[m] = -sc * fma(js1, jr1[m], js0 * jr0[m]);
-      B[m * RS + j] = sc * fma(jr1[m], jr1[m], jr0[m] * jr0[m]);  // G11, own slot
-    }
-    wave_sync();  // tile A is rewritten next
   }
-  // the Laplacian on tile A, as in poisson_group_stored
+}
+
+// geometry of the group from its node coordinates: (dx/dr, dy/dr) along the
+// column, (dx/ds, dy/ds) along the row -> G00, G01 in registers, G11 parked
+// in tile B (free until the next group) to save registers
+template <int N>
+__device__ __forceinline__ void nodal_geometry(const double2 (&xc)[N], int j, double* A, double* B,
+                                               const DEO<N>& D, const WVec<N>& w, double wj,
+                                               double (&g00)[N], double (&g01)[N]) {
+  constexpr int RS = Tile<N, SEM_TILE_PAD_NODAL>::RS;
+  double jr0[N], jr1[N];
+  {
+    double ta[N], tb[N];
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      ta[r] = xc[r].x - xc[0].x;
+      tb[r] = xc[r].y - xc[0].y;
+    }
+    deo_apply<N>(D, ta, jr0);
+    deo_apply<N>(D, tb, jr1);
+  }
+#pragma unroll
+  for (int r = 0; r < N; ++r) {
+    A[r * RS + j] = xc[r].x;
+    B[r * RS + j] = xc[r].y;
+  }
+  wave_sync();
+  {
+    double xa[RS], xb[RS], ra[N], rb[N], ta[N], tb[N];
+    load_row<N, RS>(A, j, xa);
+    load_row<N, RS>(B, j, xb);
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+      ra[q] = xa[q] - xa[0];
+      rb[q] = xb[q] - xb[0];
+    }
+    deo_apply<N>(D, ra, ta);
+    deo_apply<N>(D, rb, tb);
+    wave_sync();
+    store_row<N, RS>(A, j, ta);
+    store_row<N, RS>(B, j, tb);
+  }
+  wave_sync();
+#pragma unroll
+  for (int m = 0; m < N; ++m) {
+    const double js0 = A[m * RS + j], js1 = B[m * RS + j];
+    const double det = jr0[m] * js1 - js0 * jr1[m];
+    const double sc = (w.v[m] * wj) * fast_rcp(det);
+    g00[m] = sc * fma(js1, js1, js0 * js0);
+    g01[m] = -sc * fma(js1, jr1[m], js0 * jr0[m]);
+    B[m * RS + j] = sc * fma(jr1[m], jr1[m], jr0[m] * jr0[m]);  // G11, own slot
+  }
+  wave_sync();  // tile A is rewritten next
+}
+
+// the Laplacian of the group on tile A with G00/G01 in registers, G11 in B
+template <int N>
+__device__ __forceinline__ void nodal_laplacian(const double (&uc)[N], int j, double* A,
+                                                const double* B, const DEO<N>& D,
+                                                const double (&g00)[N], const double (&g01)[N],
+                                                double (&v)[N]) {
+  constexpr int RS = Tile<N, SEM_TILE_PAD_NODAL>::RS;
   double d0[N];
   deo_apply<N>(D, uc, d0);
 #pragma unroll
@@ -484,6 +491,30 @@ __device__ __forceinline__ void poisson_group_nodal(const uint32_t* __restrict__
 #pragma unroll
   for (int p = 0; p < N; ++p) v[p] += A[p * RS + j];
   wave_sync();  // the tiles are rewritten by the next group of this wave
+}
+
+// One group of the Poisson action with NODAL geometry (no prefetch).
+template <int N>
+__device__ __forceinline__ void poisson_group_nodal(const uint32_t* __restrict__ mapP,
+                                                    const double2* __restrict__ XG,
+                                                    const double* __restrict__ u, int64_t g,
+                                                    int lane, int j, bool in_wave, double* A,
+                                                    double* B, const DEO<N>& D,
+                                                    const WVec<N>& w, double wj,
+                                                    uint32_t (&raw)[N], double (&v)[N]) {
+  double uc[N];
+  double2 xc[N];
+  load_map<N>(mapP, g, lane, in_wave, raw);
+  gather_x<N>(XG, raw, j, xc);
+#if SEM_NODAL_EARLY_U
+  gather_u<N>(u, raw, uc);
+#endif
+  double g00[N], g01[N];
+  nodal_geometry<N>(xc, j, A, B, D, w, wj, g00, g01);
+#if !SEM_NODAL_EARLY_U
+  gather_u<N>(u, raw, uc);
+#endif
+  nodal_laplacian<N>(uc, j, A, B, D, g00, g01, v);
 }
 
 // Scatter of one group's column values through the coded map, with the
@@ -557,8 +588,11 @@ __global__ void __launch_bounds__(CHAIN_BLOCK, SEM_POISSON_MIN_WAVES)
   const int k = lane / N;
   const int j = lane - k * N;
   const bool in_wave = lane < T::LW;
-  double* L = lds + T::slot(wave, k, in_wave) * T::ES * NT;
-  double* LB = L + (NT - 1) * T::ES;
+  // tile planes: all slots of tile A, then all slots of tile B (slot stride
+  // ES in each plane; interleaving A/B per slot doubles the stride and makes
+  // the column accesses 2-way bank conflicts)
+  double* L = lds + T::slot(wave, k, in_wave) * T::ES;
+  double* LB = L + (NT - 1) * T::TILE_SLOTS * T::ES;
   const double wj = pick<N>(w, j);
   for (int rd = 0; rd < rounds; ++rd) {
     const int64_t g = (chain * rounds + rd) * CHAIN_WAVES + wave;
@@ -709,8 +743,8 @@ __global__ void __launch_bounds__(CHAIN_BLOCK)
   const int k = lane / N;
   const int j = lane - k * N;
   const bool in_wave = lane < T::LW;
-  double* LP = lds + T::slot(wave, k, in_wave) * 2 * T::ES;  // psi tile
-  double* LO = LP + T::ES;                               // omega tile
+  double* LP = lds + T::slot(wave, k, in_wave) * T::ES;  // psi tile plane
+  double* LO = LP + T::TILE_SLOTS * T::ES;                // omega tile plane
   for (int rd = 0; rd < rounds; ++rd) {
     const int64_t g = (chain * rounds + rd) * CHAIN_WAVES + wave;
     uint32_t raw[N];

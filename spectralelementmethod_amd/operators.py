@@ -79,17 +79,19 @@ class SEMOperator(object):
         axisymmetric Stokes block.
     basis : TensorProductQS, optional
     device : torch.device or str, optional
-    geometry : {"nodal", "stored"}
+    geometry : {"auto", "nodal", "stored"}
         How the Poisson action gets its geometric factors: re-derived per
-        quadrature node from x_phys per global node ("nodal", default, least
-        HBM traffic) or streamed from precomputed per-element factors
-        ("stored").  See include/sem_hip.h sem_set_geom_mode.
+        quadrature node from x_phys per global node ("nodal", least HBM
+        traffic) or streamed from precomputed per-element factors ("stored");
+        "auto" (default) picks nodal for p <= 8.  See include/sem_hip.h
+        sem_set_geom_mode.
     """
 
-    GEOMETRY_MODES = {"stored": _lib.GEOM_STORED, "nodal": _lib.GEOM_NODAL}
+    GEOMETRY_MODES = {"stored": _lib.GEOM_STORED, "nodal": _lib.GEOM_NODAL,
+                      "auto": _lib.GEOM_AUTO}
 
     def __init__(self, p, e2n, nodes, dofs_per_node=1, basis=None, device=None,
-                 geometry="nodal"):
+                 geometry="auto"):
         if geometry not in self.GEOMETRY_MODES:
             raise ValueError("geometry must be one of %s" % sorted(self.GEOMETRY_MODES))
         self.geometry = geometry
