@@ -102,6 +102,20 @@ int sem_set_basis(sem_ctx* ctx, const double* h_D, const double* h_w);
  * plus the list of element-boundary nodes; synchronises `stream`. */
 int sem_set_map(sem_ctx* ctx, const uint32_t* d_e2n, void* stream);
 
+/* sem_set_map for an operator that shares y with other operators applied in
+ * stream order (e.g. partition-interface elements first, interior elements
+ * second, so the interface sum can start early -- SURVEY.md §8(e)).
+ * d_node_state (device uint8 [n_node], may be NULL):
+ *   SEM_NODE_PRIOR  y[node] already holds the earlier operators' sum when this
+ *                   one runs: its first touch adds (read-modify-write) and the
+ *                   node is never zeroed;
+ *   SEM_NODE_OTHER  a later operator writes y[node]: not zeroed here when this
+ *                   operator does not reference it. */
+#define SEM_NODE_PRIOR 1
+#define SEM_NODE_OTHER 2
+int sem_set_map_shared(sem_ctx* ctx, const uint32_t* d_e2n, const uint8_t* d_node_state,
+                       void* stream);
+
 /* Setup plan of the last sem_set_map (diagnostics): info[0] groups (one
  * wavefront of elements each), [1] zero-list length, [2] groups in
  * atomic-fallback chains, [3] mesh conforming (0/1), [4] elements per group,

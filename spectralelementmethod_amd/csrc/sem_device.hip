@@ -447,8 +447,11 @@ struct Plan {
   bool conforming = true;
 };
 
+// node_state (may be empty): SEM_NODE_PRIOR = y already holds a value when
+// this operator runs (first touches become read-modify-write, never zeroed);
+// SEM_NODE_OTHER = another operator writes it (not zeroed when unreferenced).
 int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node, int n,
-               int rounds, Plan& P) {
+               int rounds, const std::vector<uint8_t>& node_state, Plan& P) {
   const int epw = WAVE / n, lw = epw * n, nn = n * n;
   const int64_t n_groups = (n_elem + epw - 1) / epw;
   const int CW = CHAIN_WAVES;  // groups of a chain that run concurrently
@@ -535,6 +538,8 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
   // 4./5. validation and write codes, chain by chain in launch order
   P.mapP.assign((size_t)P.n_slots * n * lw, W_SKIP << CODE_SHIFT);
   std::vector<uint8_t> written(n_node, 0);
+  if (!node_state.empty())
+    for (int64_t i = 0; i < n_node; ++i) written[i] = (node_state[i] & SEM_NODE_PRIOR) ? 1 : 0;
   std::vector<int64_t> lastc(n_node, -1);  // chain of the last touch
   std::vector<int> lastt(n_node, -1);      // (group in chain) * n * lw + pos of the last touch
   std::vector<uint8_t> act((size_t)CH * n * lw);  // per entry: 0 normal, 1 merge-skip, 2 carry-skip, 3 carry-in
@@ -590,7 +595,7 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
           const uint8_t a = act[i * n * lw + pos];
           uint32_t code;
           if (!shared_local(r, jj)) {
-            code = W_STORE;  // conforming interior node: sole writer
+            code = written[gid] ? W_RMW : W_STORE;  // conforming interior node: sole writer
           } else if (atomic_chain) {
             code = W_ATOMIC;
             if (!written[gid]) {
@@ -612,7 +617,7 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
     }
   }
   for (int64_t i = 0; i < n_node; ++i)
-    if (cnt[i] == 0) P.zero.push_back((uint32_t)i);
+    if (cnt[i] == 0 && (node_state.empty() || !node_state[i])) P.zero.push_back((uint32_t)i);
   std::sort(P.zero.begin(), P.zero.end());
   return SEM_OK;
 }
@@ -693,12 +698,22 @@ int sem_set_basis(sem_ctx* c, const double* hD, const double* hw) {
 }
 
 int sem_set_map(sem_ctx* c, const uint32_t* d_e2n, void* stream) {
+  return sem_set_map_shared(c, d_e2n, nullptr, stream);
+}
+
+int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_state,
+                       void* stream) {
   if (!c || !d_e2n) return fail(SEM_E_INVALID, "null argument");
   DeviceGuard g(c->device);
   hipStream_t st = S(stream);
   const int n = c->n;
   std::vector<uint32_t> h((size_t)c->n_elem * n * n);
+  std::vector<uint8_t> state;
   HIP_TRY(hipMemcpyAsync(h.data(), d_e2n, h.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  if (d_node_state) {
+    state.resize(c->n_node);
+    HIP_TRY(hipMemcpyAsync(state.data(), d_node_state, state.size(), hipMemcpyDeviceToHost, st));
+  }
   HIP_TRY(hipStreamSynchronize(st));
   Plan P;
   // measured on MI355X at p = 8, 10^6 elements: 1 round 0.79-0.81 ms,
@@ -708,7 +723,7 @@ int sem_set_map(sem_ctx* c, const uint32_t* d_e2n, void* stream) {
   // prefetch registers halve occupancy.  Not kept.
   int rounds = 1;
   if (const char* s = std::getenv("SEM_CHAIN_ROUNDS")) rounds = std::max(1, std::atoi(s));
-  int rc = build_plan(h, c->n_elem, c->n_node, n, rounds, P);
+  int rc = build_plan(h, c->n_elem, c->n_node, n, rounds, state, P);
   if (rc) return rc;
   c->rounds = rounds;
   c->n_slots = P.n_slots;

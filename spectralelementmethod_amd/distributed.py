@@ -184,3 +184,102 @@ class DistributedOperator(object):
         s = torch.sum(a[own] * b[own]).reshape(1)
         dist.all_reduce(s, group=group)
         return s.item()
+
+
+# ---------------------------------------------------------------- overlap
+def split_interface_elements(e2n, neighbors):
+    """Split a rank's elements into the ones touching a partition interface
+    (computed first, so the interface sum can start) and the interior ones,
+    with the node states of include/sem_hip.h sem_set_map_shared:
+    returns (iface_elems, interior_elems, state_iface, state_interior)."""
+    e2n = np.asarray(e2n)
+    n_elem = e2n.shape[0]
+    flat = e2n.reshape(n_elem, -1)
+    n_node = int(flat.max()) + 1 if flat.size else 0
+    iface = np.zeros(n_node, dtype=bool)
+    for nodes in neighbors.values():
+        iface[np.asarray(nodes, dtype=np.int64)] = True
+    touch = iface[flat].any(axis=1)
+    ie = np.nonzero(touch)[0]
+    be = np.nonzero(~touch)[0]
+    in_i = np.zeros(n_node, dtype=bool)
+    in_b = np.zeros(n_node, dtype=bool)
+    in_i[flat[ie].ravel()] = True
+    in_b[flat[be].ravel()] = True
+    state_i = np.where(in_b & ~in_i, _lib.NODE_OTHER, 0).astype(np.uint8)
+    # interior operator: everything the interface operator wrote is PRIOR;
+    # nodes neither references were zeroed by the interface operator
+    state_b = np.where(in_i, _lib.NODE_PRIOR, np.where(in_b, 0, _lib.NODE_OTHER)).astype(np.uint8)
+    return ie, be, state_i, state_b
+
+
+class OverlappedOperator(object):
+    """Rank-local operator whose interface sum overlaps the interior
+    elements: interface elements are applied first, an
+    event releases the RCCL exchange on a side stream, and the interior
+    elements run meanwhile on the caller's stream.  Interface nodes are
+    touched only by interface elements, so the exchange's scatter-add never
+    races the interior kernel."""
+
+    def __init__(self, p, nodes, e2n, neighbors, dofs_per_node=1, device=None, group=None,
+                 geometry="auto", kind=0):
+        from .operators import SEMOperator
+        self.dpn = dofs_per_node
+        self.kind = kind
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        e2n = np.asarray(e2n)
+        n_node = np.asarray(nodes).shape[1]
+        ie, be, st_i, st_b = split_interface_elements(e2n, neighbors)
+        if st_i.size < n_node:  # nodes beyond the last referenced one
+            pad = n_node - st_i.size
+            st_i = np.concatenate([st_i, np.zeros(pad, np.uint8)])
+            st_b = np.concatenate([st_b, np.full(pad, _lib.NODE_OTHER, np.uint8)])
+        self.n_iface_elem, self.n_interior_elem = ie.size, be.size
+        if ie.size == 0 or be.size == 0:  # nothing to overlap
+            self.ops = [SEMOperator(p, e2n, nodes, dofs_per_node, device=self.device,
+                                    geometry=geometry)]
+        else:
+            self.ops = [SEMOperator(p, e2n[ie], nodes, dofs_per_node, device=self.device,
+                                    geometry=geometry, node_state=st_i),
+                        SEMOperator(p, e2n[be], nodes, dofs_per_node, device=self.device,
+                                    geometry=geometry, node_state=st_b)]
+        for op in self.ops:
+            op.compute_geometry(kind)
+        self.ndof = self.ops[0].ndof
+        self.n_elem = e2n.shape[0]
+        self.xchg = InterfaceExchange(neighbors, dofs_per_node, self.device, group) \
+            if neighbors else None
+        self.side = torch.cuda.Stream(device=self.device)
+        self.ready = torch.cuda.Event()
+        self._lib = _lib.load()
+
+    def plan_info(self):
+        return self.ops[-1].plan_info()
+
+    def step(self, u, y, events=None):
+        """y = K u on this rank's nodes, interface sum included.  ``events``
+        (start, end) bracket the element kernels on the caller's stream."""
+        main = torch.cuda.current_stream(self.device)
+        sp = _lib.stream_ptr(main)
+        up, yp = _lib.tptr(u), _lib.tptr(y)
+        last = len(self.ops) - 1
+        for i, op in enumerate(self.ops):
+            _lib.check(self._lib.sem_zero_shared(op._ctx, yp, sp))
+            if events is not None and i == 0:
+                events[0].record(main)
+            _lib.check(self._lib.sem_apply(op._ctx, self.kind, up, yp, _lib.APPLY_SKIP_ZERO, sp))
+            if i == 0 and self.xchg is not None:
+                self.ready.record(main)
+            if events is not None and i == last:
+                events[1].record(main)
+        if self.xchg is not None:
+            with torch.cuda.stream(self.side):
+                self.side.wait_event(self.ready)
+                self.xchg.exchange(y)
+            main.wait_stream(self.side)
+        return y
+
+    def apply(self, u, out=None):
+        if out is None:
+            out = torch.empty_like(u)
+        return self.step(u, out)

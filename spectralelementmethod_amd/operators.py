@@ -85,13 +85,19 @@ class SEMOperator(object):
         traffic) or streamed from precomputed per-element factors ("stored");
         "auto" (default) picks nodal for p <= 8.  See include/sem_hip.h
         sem_set_geom_mode.
+    node_state : array-like uint8 [n_node], optional
+        For operators that share the output vector with others applied
+        before / after it in stream order: NODE_PRIOR marks nodes whose y
+        entry already holds a value (added to, never zeroed), NODE_OTHER
+        nodes another operator writes (left alone).  See
+        include/sem_hip.h sem_set_map_shared.
     """
 
     GEOMETRY_MODES = {"stored": _lib.GEOM_STORED, "nodal": _lib.GEOM_NODAL,
                       "auto": _lib.GEOM_AUTO}
 
     def __init__(self, p, e2n, nodes, dofs_per_node=1, basis=None, device=None,
-                 geometry="auto"):
+                 geometry="auto", node_state=None):
         if geometry not in self.GEOMETRY_MODES:
             raise ValueError("geometry must be one of %s" % sorted(self.GEOMETRY_MODES))
         self.geometry = geometry
@@ -120,7 +126,15 @@ class SEMOperator(object):
             self._ctx = ctx
             _lib.check(self._lib.sem_set_geom_mode(ctx, self.GEOMETRY_MODES[geometry]))
             _lib.check(self._lib.sem_set_basis(ctx, _lib.dptr(self.D), _lib.dptr(self.w)))
-            _lib.check(self._lib.sem_set_map(ctx, _lib.tptr(self.e2n), _lib.stream_ptr()))
+            if node_state is None:
+                _lib.check(self._lib.sem_set_map(ctx, _lib.tptr(self.e2n), _lib.stream_ptr()))
+            else:
+                st = torch.as_tensor(np.asarray(node_state, dtype=np.uint8))
+                if st.shape != (self.n_node,):
+                    raise ValueError("node_state must have shape [n_node]")
+                st = st.to(self.device)
+                _lib.check(self._lib.sem_set_map_shared(ctx, _lib.tptr(self.e2n), _lib.tptr(st),
+                                                        _lib.stream_ptr()))
         self._geom_ready = set()
 
     @staticmethod

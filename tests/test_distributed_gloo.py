@@ -112,3 +112,28 @@ def test_strip_partition_bookkeeping():
         assert np.array_equal(ga, gb)
     with pytest.raises(ValueError):
         StripPartition(3, 4, 2, 4, 0)
+
+
+def test_split_interface_elements():
+    """Interface / interior element split and node states of the overlapped
+    multi-GPU operator (host logic)."""
+    from spectralelementmethod_amd import _lib
+    from spectralelementmethod_amd.distributed import StripPartition, split_interface_elements
+    for rank in range(3):
+        part = StripPartition(12, 4, 3, 3, rank)
+        nodes, e2n = part.local_mesh(0.05)
+        ie, be, st_i, st_b = split_interface_elements(e2n, part.neighbors)
+        assert np.union1d(ie, be).size == e2n.shape[0] and np.intersect1d(ie, be).size == 0
+        n_nb = len(part.neighbors)
+        assert ie.size == n_nb * part.ney  # one element column per interface
+        iface = np.concatenate(list(part.neighbors.values()))
+        # interface nodes belong to interface elements only
+        assert not np.isin(iface, e2n[be]).any()
+        in_i = np.zeros(part.n_nodes, bool)
+        in_i[e2n[ie].ravel()] = True
+        assert (st_b[in_i] == _lib.NODE_PRIOR).all()
+        only_b = np.zeros(part.n_nodes, bool)
+        only_b[e2n[be].ravel()] = True
+        only_b &= ~in_i
+        assert (st_i[only_b] == _lib.NODE_OTHER).all() and (st_b[only_b] == 0).all()
+        assert (st_i[in_i] == 0).all()

@@ -275,3 +275,34 @@ def test_poisson_solution_golden(sem, poisson_solution):
         x[torch.from_numpy(ebc).cuda()] = torch.from_numpy(ref[ebc]).cuda()
         x, its, rel = op.pcg_solve(torch.from_numpy(fx[name + "_rhs"]).cuda(), x, ebc, rtol=1e-13)
         assert rel_l2(x.cpu().numpy(), ref) < TOL_SOLVE, (name, its, rel)
+
+
+@pytest.mark.parametrize("geometry", GEOMETRY)
+def test_shared_output_split(sem, gll, geometry):
+    """Interface elements first, interior elements second into the same y
+    (sem_set_map_shared node states) == the single operator, in overwrite
+    and in accumulate mode."""
+    from spectralelementmethod_amd import meshgen
+    from spectralelementmethod_amd.distributed import split_interface_elements
+    p, nex, ney = 6, 9, 5
+    nodes, e2n = meshgen.structured_square(nex, ney, p, warp=0.05)
+    Ny = ney * p + 1
+    nn = nodes.shape[1]
+    neighbors = {1: np.arange(nn - Ny, nn)}  # right edge line as the "interface"
+    ie, be, st_i, st_b = split_interface_elements(e2n, neighbors)
+    assert ie.size == ney and be.size == (nex - 1) * ney
+    full = sem.SEMOperator(p, e2n, nodes, geometry=geometry)
+    op_i = sem.SEMOperator(p, e2n[ie], nodes, geometry=geometry, node_state=st_i)
+    op_b = sem.SEMOperator(p, e2n[be], nodes, geometry=geometry, node_state=st_b)
+    u = torch.randn(full.ndof, dtype=torch.float64, device="cuda",
+                    generator=torch.Generator(device="cuda").manual_seed(7))
+    ref = full.apply(u)
+    y = torch.full_like(u, 3.0)
+    op_i.apply(u, out=y)
+    op_b.apply(u, out=y)
+    assert (y - ref).norm().item() <= 1e-13 * ref.norm().item()
+    y0 = torch.linspace(-1, 1, u.numel(), dtype=torch.float64, device="cuda")
+    y = y0.clone()
+    op_i.apply(u, out=y, accumulate=True)
+    op_b.apply(u, out=y, accumulate=True)
+    assert (y - y0 - ref).norm().item() <= 1e-13 * ref.norm().item()
