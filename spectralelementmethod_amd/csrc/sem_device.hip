@@ -270,6 +270,7 @@ struct sem_ctx {
   double* d_D = nullptr;
   double* d_w = nullptr;
   double* d_Vinv = nullptr;
+  double* d_deo = nullptr;  // even-odd D for n >= SEM_D_SCALAR_LOAD_N (scalar loads)
   uint32_t* d_mapP = nullptr;   // packed coded map, launch (colour) order
   int* d_gpos = nullptr;         // natural group -> packed slot
   const uint32_t* d_e2n = nullptr;
@@ -311,20 +312,36 @@ inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // even-odd halves of D (row-major h[m*N + r]); see DEO in sem_kernels.h
 template <int N>
-DEO<N> make_deo(const double* h) {
-  DEO<N> d;
+DEOData<N> make_deo_data(const double* h) {
+  DEOData<N> d;
   constexpr int H = N / 2;
   for (int m = 0; m < H; ++m)
     for (int r = 0; r < H; ++r) {
       d.P[m * H + r] = 0.5 * (h[m * N + r] - h[m * N + N - 1 - r]);
       d.Q[m * H + r] = 0.5 * (h[m * N + r] + h[m * N + N - 1 - r]);
     }
-  if (DEO<N>::C)
+  if (DEOData<N>::C)
     for (int m = 0; m < H; ++m) {
       d.cc[m] = h[m * N + H];
       d.rr[m] = h[H * N + m];
     }
   return d;
+}
+
+template <int N>
+DEO<N> make_deo(const sem_ctx* c) {
+  DEO<N> a;
+  if constexpr (N >= SEM_D_SCALAR_LOAD_N)
+    a.p = reinterpret_cast<const DEOData<N>*>(c->d_deo);
+  else
+    a.d = make_deo_data<N>(c->hD);
+  return a;
+}
+
+template <int N>
+void upload_deo(sem_ctx* c, hipError_t* err) {
+  const DEOData<N> d = make_deo_data<N>(c->hD);
+  *err = hipMemcpy(c->d_deo, &d, sizeof(d), hipMemcpyHostToDevice);
 }
 
 // the Poisson action recomputes its factors from x_phys per node (NODAL)
@@ -339,7 +356,7 @@ bool use_nodal(const sem_ctx* c, int op_kind) {
 
 template <int N>
 int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc, hipStream_t st) {
-  const DEO<N> D = make_deo<N>(c->hD);
+  const DEO<N> D = make_deo<N>(c);
   WVec<N> w;
   std::memcpy(w.v, c->hw, sizeof(w.v));
   const bool nodal = use_nodal(c, op_kind);
@@ -657,6 +674,7 @@ int sem_ctx_create(sem_ctx** out, int p, int64_t n_elem, int64_t n_node, int dpn
   hipError_t e2 = hipMalloc(&c->d_w, SEM_MAXN * sizeof(double));
   hipError_t e3 = hipMalloc(&c->d_Vinv, SEM_MAXN * SEM_MAXN * sizeof(double));
   hipError_t e4 = hipMalloc(&c->d_bad, sizeof(unsigned long long));
+  if (!e4) e4 = hipMalloc(&c->d_deo, sizeof(DEOData<SEM_MAXN>));
   hipError_t e5 = hipMalloc(&c->d_red, (2 * RED_BLOCKS + 8) * sizeof(double));
   if (e1 || e2 || e3 || e4 || e5) {
     sem_ctx_destroy(c);
@@ -672,6 +690,7 @@ void sem_ctx_destroy(sem_ctx* c) {
   (void)hipFree(c->d_D);
   (void)hipFree(c->d_w);
   (void)hipFree(c->d_Vinv);
+  (void)hipFree(c->d_deo);
   (void)hipFree(c->d_mapP);
   (void)hipFree(c->d_gpos);
   (void)hipFree(c->d_zero);
@@ -693,6 +712,9 @@ int sem_set_basis(sem_ctx* c, const double* hD, const double* hw) {
   std::memcpy(c->hw, hw, sizeof(double) * n);
   HIP_TRY(hipMemcpy(c->d_D, hD, sizeof(double) * n * n, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(c->d_w, hw, sizeof(double) * n, hipMemcpyHostToDevice));
+  hipError_t err = hipSuccess;
+  SEM_DISPATCH_N(n, upload_deo, c, &err);
+  HIP_TRY(err);
   c->have_basis = true;
   return SEM_OK;
 }

@@ -69,7 +69,7 @@ constexpr uint32_t W_CARRY = 8;   // add the value handed over by the previous g
 // 2H^2 + 2H values instead of N^2 (40 vs 81 doubles at p = 8, so D fits the
 // scalar register file next to the kernel's pointers) and ~40 % fewer FMAs.
 template <int N>
-struct DEO {
+struct DEOData {
   static constexpr int H = N / 2;
   static constexpr int C = N % 2;
   double P[H * H];
@@ -78,9 +78,40 @@ struct DEO {
   double rr[C ? H : 1];
 };
 
+// How the kernels see D.  Up to n = 9 the even-odd halves are kernel
+// arguments (SGPRs for the whole kernel).  Above, they no longer fit the
+// 102-SGPR file and the compiler would spill them to VGPR lanes (two
+// v_readlane per FMA operand); instead each contraction row re-reads its
+// 2H values with scalar loads from a device copy: the pointer is laundered
+// through an empty asm per row so the loads are neither hoisted nor CSE'd.
+#ifndef SEM_D_SCALAR_LOAD_N
+#define SEM_D_SCALAR_LOAD_N 10
+#endif
+template <int N>
+using CDEOData = const __attribute__((address_space(4))) DEOData<N>;
+
+template <int N, bool PTR = (N >= SEM_D_SCALAR_LOAD_N)>
+struct DEO;
+
+template <int N>
+struct DEO<N, false> {
+  DEOData<N> d;
+  __device__ __forceinline__ const DEOData<N>* row() const { return &d; }
+};
+
+template <int N>
+struct DEO<N, true> {
+  const DEOData<N>* p;  // device copy (constant during the launch)
+  __device__ __forceinline__ CDEOData<N>* row() const {
+    CDEOData<N>* q = (CDEOData<N>*)(p);
+    asm volatile("" : "+s"(q));
+    return q;
+  }
+};
+
 // v = D x
 template <int N>
-__device__ __forceinline__ void deo_apply(const DEO<N>& E, const double (&x)[N],
+__device__ __forceinline__ void deo_apply(const DEO<N>& D, const double (&x)[N],
                                           double (&v)[N]) {
   constexpr int H = N / 2;
   double e[H], o[H];
@@ -91,27 +122,29 @@ __device__ __forceinline__ void deo_apply(const DEO<N>& E, const double (&x)[N],
   }
 #pragma unroll
   for (int m = 0; m < H; ++m) {
+    const auto E = D.row();
     double sp = 0.0, tp = 0.0;
-    if constexpr (DEO<N>::C) tp = E.cc[m] * x[H];
+    if constexpr (DEOData<N>::C) tp = E->cc[m] * x[H];
 #pragma unroll
     for (int r = 0; r < H; ++r) {
-      sp = fma(E.P[m * H + r], o[r], sp);
-      tp = fma(E.Q[m * H + r], e[r], tp);
+      sp = fma(E->P[m * H + r], o[r], sp);
+      tp = fma(E->Q[m * H + r], e[r], tp);
     }
     v[m] = sp + tp;
     v[N - 1 - m] = sp - tp;
   }
-  if constexpr (DEO<N>::C) {
+  if constexpr (DEOData<N>::C) {
+    const auto E = D.row();
     double a = 0.0;
 #pragma unroll
-    for (int r = 0; r < H; ++r) a = fma(E.rr[r], o[r], a);
+    for (int r = 0; r < H; ++r) a = fma(E->rr[r], o[r], a);
     v[H] = a;
   }
 }
 
 // v = D^T x  (the transpose is centro-antisymmetric with P^T <-> Q^T swapped)
 template <int N>
-__device__ __forceinline__ void deo_apply_t(const DEO<N>& E, const double (&x)[N],
+__device__ __forceinline__ void deo_apply_t(const DEO<N>& D, const double (&x)[N],
                                             double (&v)[N]) {
   constexpr int H = N / 2;
   double e[H], o[H];
@@ -122,20 +155,22 @@ __device__ __forceinline__ void deo_apply_t(const DEO<N>& E, const double (&x)[N
   }
 #pragma unroll
   for (int q = 0; q < H; ++q) {
+    const auto E = D.row();
     double sp = 0.0, tp = 0.0;
-    if constexpr (DEO<N>::C) tp = E.rr[q] * x[H];
+    if constexpr (DEOData<N>::C) tp = E->rr[q] * x[H];
 #pragma unroll
     for (int m = 0; m < H; ++m) {
-      sp = fma(E.Q[m * H + q], o[m], sp);
-      tp = fma(E.P[m * H + q], e[m], tp);
+      sp = fma(E->Q[m * H + q], o[m], sp);
+      tp = fma(E->P[m * H + q], e[m], tp);
     }
     v[q] = sp + tp;
     v[N - 1 - q] = sp - tp;
   }
-  if constexpr (DEO<N>::C) {
+  if constexpr (DEOData<N>::C) {
+    const auto E = D.row();
     double a = 0.0;
 #pragma unroll
-    for (int m = 0; m < H; ++m) a = fma(E.cc[m], o[m], a);
+    for (int m = 0; m < H; ++m) a = fma(E->cc[m], o[m], a);
     v[H] = a;
   }
 }
