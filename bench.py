@@ -128,6 +128,9 @@ def main():
     ap.add_argument("--geometry", choices=["auto", "nodal", "stored"], default="auto",
                     help="Poisson geometric factors: re-derived from x_phys per node, or "
                          "streamed; auto = nodal for p <= 8 (the library's default)")
+    ap.add_argument("--kernel", choices=["auto", "column", "mfma"], default="auto",
+                    help="Poisson kernel family: LDS column kernel or fp64-MFMA element kernel; "
+                         "auto = the library's measured choice")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--traffic-json", default=None,
@@ -164,10 +167,12 @@ def main():
     # interface elements first, RCCL interface sum on a side stream while the
     # interior elements run (one plain operator when there is no neighbour)
     op = OverlappedOperator(p, nodes, e2n, part.neighbors if world > 1 else {}, dpn, dev,
-                            geometry=geometry, kind=kind)
-    if geometry == "auto":  # as resolved by the library (SEM_GEOM_AUTO)
-        geometry = "nodal" if p <= 8 else "stored"
+                            geometry=geometry, kind=kind, kernel=args.kernel)
     plan = op.plan_info()
+    if plan["kernel"] == "mfma":  # the MFMA kernel streams stored factors
+        geometry = "stored"
+    elif geometry == "auto":  # as resolved by the library (SEM_GEOM_AUTO)
+        geometry = "nodal" if p <= 8 else "stored"
     log("rank %d: plan %s; %d interface + %d interior elements" % (
         rank, plan, op.n_iface_elem, op.n_interior_elem))
     n_elem_local = op.n_elem
@@ -215,7 +220,8 @@ def main():
     achieved = B / kern_avg_s / 1e9
     traffic = None
     traffic_src = args.traffic_json
-    if traffic_src is None and kind == POISSON and (p, args.nex, args.ney) == (8, 1024, 1024):
+    if (traffic_src is None and kind == POISSON and plan["kernel"] == "column"
+            and (p, args.nex, args.ney) == (8, 1024, 1024)):
         # PMC measurement of this workload (separate FETCH_SIZE / WRITE_SIZE
         # passes, tools/gpu_profile.sh + tools/pmc_traffic.py)
         traffic_src = os.path.join(ROOT, "profiles", DEFAULT_TRAFFIC[geometry])
@@ -248,14 +254,15 @@ def main():
             "single GPU",
             "kernel_ms_avg": kern_avg_s * 1e3, "kernel_ms_min": float(np.min(kern_ms)),
             "gflops_kernel": F / kern_avg_s / 1e9,
+            "kernel_family": plan["kernel"],
             "scatter_plan": {k: plan[k] for k in ("colours", "chains_per_colour", "rounds", "zero_list",
                                                   "atomic_groups")},
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "kernel": "k_poisson_apply<%d>" % (p + 1) if kind == POISSON else
-                      "k_axisym_apply<%d>" % (p + 1),
+            "kernel": ("k_poisson_mfma<%d>" if plan["kernel"] == "mfma" else "k_poisson_apply<%d>")
+                      % (p + 1) if kind == POISSON else "k_axisym_apply<%d>" % (p + 1),
             "alg_bytes_per_launch": B,
             "fp64_tflops": F / kern_avg_s / 1e12, "fp64_peak_tflops": FP64_PEAK_TFLOPS,
             "launch": "one sem_apply = %d colour launches" % plan["colours"],

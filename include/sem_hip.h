@@ -120,8 +120,9 @@ int sem_set_map_shared(sem_ctx* ctx, const uint32_t* d_e2n, const uint8_t* d_nod
  * wavefront of elements each), [1] zero-list length, [2] groups in
  * atomic-fallback chains, [3] mesh conforming (0/1), [4] elements per group,
  * [5] colour classes, [6] rounds of 4 groups per chain (one workgroup per
- * chain), [7] packed group slots, [8..] chains per colour class (one launch
- * each).  Writes min(n_info, 17) values. */
+ * chain), [7] packed group slots, [8..16] chains per colour class (one launch
+ * each; elements for the MFMA kernel), [17] kernel family (SEM_KERNEL_COLUMN
+ * or SEM_KERNEL_MFMA).  Writes min(n_info, 18) values. */
 int sem_plan_info(sem_ctx* ctx, int64_t* info, int n_info);
 
 /* How the Poisson action obtains its geometric factors.
@@ -141,6 +142,25 @@ int sem_plan_info(sem_ctx* ctx, int64_t* info, int n_info);
 #define SEM_GEOM_NODAL 1
 #define SEM_GEOM_AUTO 2
 int sem_set_geom_mode(sem_ctx* ctx, int mode);
+
+/* Kernel family of the Poisson action; takes effect at the next sem_set_map,
+ * which plans the scatter for it.
+ *  SEM_KERNEL_COLUMN: k_poisson_apply -- a wavefront holds floor(64/n)
+ *    elements, each lane one element column; contractions along the lane in
+ *    registers (D in even-odd form), transposes through LDS; chains of 4
+ *    groups hand shared columns over through LDS; NODAL or STORED geometry.
+ *  SEM_KERNEL_MFMA: k_poisson_mfma -- one element per wavefront as 16 x 16
+ *    tiles on the fp64 matrix cores (v_mfma_f64_16x16x4_f64, six products
+ *    per element, no LDS); element-level colouring; stored factors only
+ *    (a NODAL request is ignored); n = p + 1 <= 16 and dpn = 1, else
+ *    SEM_E_NOTIMPL.
+ *  SEM_KERNEL_AUTO (default): COLUMN (measured faster at every order on
+ *    MI355X; the threshold SEM_MFMA_MIN_N is a build knob).
+ * The environment variable SEM_KERNEL (0/1/2) sets the initial value. */
+#define SEM_KERNEL_COLUMN 0
+#define SEM_KERNEL_MFMA 1
+#define SEM_KERNEL_AUTO 2
+int sem_set_kernel(sem_ctx* ctx, int kernel);
 
 /* Geometry from mesh nodes (device, float64 [2][n_node]) for op_kind:
  * x_phys = V_eq^-1 X V_eq^-T (Mapping._compute_x_phys, sem/mapping.py:98-103),

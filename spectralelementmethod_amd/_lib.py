@@ -28,6 +28,9 @@ APPLY_SKIP_ZERO = 2
 GEOM_STORED = 0
 GEOM_NODAL = 1
 GEOM_AUTO = 2
+KERNEL_COLUMN = 0
+KERNEL_MFMA = 1
+KERNEL_AUTO = 2
 NODE_PRIOR = 1
 NODE_OTHER = 2
 
@@ -54,6 +57,7 @@ SIGNATURES = {
     "sem_geom_fields": (C.c_int, [_vp, _vp, _dp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "sem_set_geom": (C.c_int, [_vp, _vp, C.c_int, _vp]),
     "sem_set_geom_mode": (C.c_int, [_vp, C.c_int]),
+    "sem_set_kernel": (C.c_int, [_vp, C.c_int]),
     "sem_set_map_shared": (C.c_int, [_vp, _vp, _vp, _vp]),
     "sem_apply": (C.c_int, [_vp, C.c_int, _vp, _vp, C.c_int, _vp]),
     "sem_zero_shared": (C.c_int, [_vp, _vp, _vp]),

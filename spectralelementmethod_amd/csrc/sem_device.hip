@@ -284,6 +284,11 @@ struct sem_ctx {
   double* d_GP[2] = {nullptr, nullptr};
   // NODAL geometry (Poisson): x_phys per global node + the node's first element
   int geom_mode = SEM_GEOM_AUTO;
+  // kernel family of the Poisson action (sem_set_kernel), fixed by
+  // sem_set_map: the LDS column kernel or the fp64-MFMA element kernel (they
+  // need different plans and packed layouts)
+  int kernel = SEM_KERNEL_AUTO;
+  bool mfma = false;
   double2* d_XG = nullptr;
   uint32_t* d_owner = nullptr;
   bool xg_valid = false;
@@ -347,7 +352,23 @@ void upload_deo(sem_ctx* c, hipError_t* err) {
 // the Poisson action recomputes its factors from x_phys per node (NODAL)
 // unless the stored-factor mode was chosen or the caller supplied factors
 bool nodal_mode(const sem_ctx* c) {
+  if (c->mfma) return false;  // the MFMA kernel streams stored factors
   return c->geom_mode == SEM_GEOM_NODAL || (c->geom_mode == SEM_GEOM_AUTO && c->n <= 9);
+}
+
+// AUTO: the MFMA element kernel from SEM_MFMA_MIN_N nodes per line up,
+// Poisson only (dpn = 1), one 16 x 16 tile (n <= 16), and not when nodal
+// geometry was requested explicitly.  Measured on MI355X
+// the column kernel is faster at every order, so AUTO never picks MFMA
+// (17 > the largest tile) unless built with a smaller threshold.
+#ifndef SEM_MFMA_MIN_N
+#define SEM_MFMA_MIN_N 17
+#endif
+bool want_mfma(const sem_ctx* c) {
+  if (c->dpn != 1 || c->n > 16) return false;
+  if (c->kernel == SEM_KERNEL_MFMA) return true;
+  if (c->kernel == SEM_KERNEL_COLUMN) return false;
+  return c->n >= SEM_MFMA_MIN_N && c->geom_mode != SEM_GEOM_NODAL;
 }
 
 bool use_nodal(const sem_ctx* c, int op_kind) {
@@ -365,7 +386,11 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
     const int64_t c0 = c->colour_start[k], c1 = c->colour_start[k + 1];
     if (c1 <= c0) continue;
     const int grid = (int)(c1 - c0);
-    if (op_kind == SEM_OP_POISSON && nodal)
+    if (op_kind == SEM_OP_POISSON && c->mfma) {
+      if constexpr (N <= 16)
+        hipLaunchKernelGGL((k_poisson_mfma<N>), dim3((grid + MFMA_EPB - 1) / MFMA_EPB),
+                           dim3(BLOCK), 0, st, c->d_mapP, c->d_GP[0], u, y, c->d_D, c0, c1, acc);
+    } else if (op_kind == SEM_OP_POISSON && nodal)
       hipLaunchKernelGGL((k_poisson_apply<N, true>), dim3(grid), dim3(CHAIN_BLOCK), 0, st,
                          c->d_mapP, nullptr, c->d_XG, u, y, c0, c1, c->rounds, acc, D, w);
     else if (op_kind == SEM_OP_POISSON)
@@ -386,7 +411,8 @@ void launch_geom_n(sem_ctx* c, const double* nodes, int op_kind, double* GP, dou
   using Sh = GeomShape<N>;
   const int grid = (int)((c->n_elem + Sh::EPB - 1) / Sh::EPB);
   hipLaunchKernelGGL((k_geometry<N>), dim3(grid), dim3(Sh::THREADS), 0, st, nodes, c->n_node,
-                     c->d_e2n, c->n_elem, c->d_Vinv, c->d_D, c->d_w, op_kind, c->d_gpos, GP, xph,
+                     c->d_e2n, c->n_elem, c->d_Vinv, c->d_D, c->d_w, op_kind, c->epw, c->d_gpos, GP,
+                     xph,
                      J, iJ, dJ, dJW, XG, XG ? c->d_owner : nullptr, XGin, c->d_bad);
 }
 
@@ -639,6 +665,115 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
   return SEM_OK;
 }
 
+
+// ---------------------------------------------------------------------------
+// Element-level plan for the MFMA kernel (one element per wavefront, no
+// chains): elements are greedily coloured so that elements of one colour
+// share no node (a per-node colour bitmask over their element-boundary nodes,
+// all nodes on a non-conforming map); one launch per colour, natural element
+// order inside a colour; STORE for the first writer of a node in launch
+// order, RMW after it.  Elements that would need more than MAX_COLOURS
+// colours, or that reference one node twice, go to a final class whose
+// shareable nodes are written with atomics.  Group = slot = one element, so
+// the packed map and factors are compact per element ([slot][r][j]).
+// ---------------------------------------------------------------------------
+int build_plan_elem(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node, int n,
+                    const std::vector<uint8_t>& node_state, Plan& P) {
+  const int nn = n * n;
+  auto is_bnd = [n](int r, int jj) { return r == 0 || r == n - 1 || jj == 0 || jj == n - 1; };
+  std::vector<uint32_t> cnt(n_node, 0);
+  P.owner.assign(n_node, 0xFFFFFFFFu);
+  for (int64_t t = 0; t < n_elem * nn; ++t) {
+    if (e2n[t] >= n_node) return fail(SEM_E_INVALID, "element map references node >= n_node");
+    if (!cnt[e2n[t]]++) P.owner[e2n[t]] = (uint32_t)(t / nn);
+  }
+  bool conforming = true;
+  for (int64_t e = 0; e < n_elem && conforming; ++e)
+    for (int r = 1; r < n - 1 && conforming; ++r)
+      for (int jj = 1; jj < n - 1; ++jj)
+        if (cnt[e2n[e * nn + r * n + jj]] != 1) {
+          conforming = false;
+          break;
+        }
+  P.conforming = conforming;
+  auto shared_local = [&](int r, int jj) { return !conforming || is_bnd(r, jj); };
+  std::vector<uint8_t> cmask(n_node, 0);
+  std::vector<int64_t> stamp(n_node, -1);
+  std::vector<int> colour(n_elem);
+  std::vector<uint32_t> cn;
+  for (int64_t e = 0; e < n_elem; ++e) {
+    cn.clear();
+    uint32_t forb = 0;
+    bool dup = false;
+    for (int r = 0; r < n; ++r)
+      for (int jj = 0; jj < n; ++jj)
+        if (shared_local(r, jj)) {
+          const uint32_t gid = e2n[e * nn + r * n + jj];
+          if (stamp[gid] == e) {
+            dup = true;
+            continue;
+          }
+          stamp[gid] = e;
+          cn.push_back(gid);
+          forb |= cmask[gid];
+        }
+    int c = MAX_COLOURS;
+    if (!dup)
+      for (int q = 0; q < MAX_COLOURS; ++q)
+        if (!(forb & (1u << q))) {
+          c = q;
+          break;
+        }
+#ifdef SEM_DIAG_ONE_COLOUR
+    if (!dup) c = 0;  // timing-only diagnostic: racy single launch
+#endif
+    if (c < MAX_COLOURS)
+      for (uint32_t gid : cn) cmask[gid] |= (uint8_t)(1u << c);
+    colour[e] = c;
+  }
+  std::vector<uint8_t>().swap(cmask);
+  std::vector<int64_t> count(MAX_COLOURS + 2, 0);
+  for (int64_t e = 0; e < n_elem; ++e) count[colour[e] + 1]++;
+  P.colour_start.assign(MAX_COLOURS + 2, 0);
+  for (int q = 0; q <= MAX_COLOURS; ++q) P.colour_start[q + 1] = P.colour_start[q] + count[q + 1];
+  std::vector<int64_t> order(n_elem);
+  {
+    std::vector<int64_t> fill(P.colour_start.begin(), P.colour_start.end() - 1);
+    for (int64_t e = 0; e < n_elem; ++e) order[fill[colour[e]]++] = e;
+  }
+  P.n_slots = n_elem;
+  P.gpos.assign(n_elem, 0);
+  for (int64_t q = 0; q < n_elem; ++q) P.gpos[order[q]] = (int)q;
+  P.mapP.assign((size_t)n_elem * nn, W_SKIP << CODE_SHIFT);
+  std::vector<uint8_t> written(n_node, 0);
+  if (!node_state.empty())
+    for (int64_t i = 0; i < n_node; ++i) written[i] = (node_state[i] & SEM_NODE_PRIOR) ? 1 : 0;
+  P.n_atomic_groups = 0;
+  for (int64_t q = 0; q < n_elem; ++q) {
+    const int64_t e = order[q];
+    const bool atomic = colour[e] >= MAX_COLOURS;
+    if (atomic) P.n_atomic_groups++;
+    uint32_t* out = P.mapP.data() + q * nn;
+    for (int r = 0; r < n; ++r)
+      for (int jj = 0; jj < n; ++jj) {
+        const uint32_t gid = e2n[e * nn + r * n + jj];
+        uint32_t code;
+        if (atomic && shared_local(r, jj)) {
+          code = W_ATOMIC;
+          if (!written[gid]) P.zero.push_back(gid);
+        } else {
+          code = written[gid] ? W_RMW : W_STORE;
+        }
+        written[gid] = 1;
+        out[r * n + jj] = gid | (code << CODE_SHIFT);
+      }
+  }
+  for (int64_t i = 0; i < n_node; ++i)
+    if (cnt[i] == 0 && (node_state.empty() || !node_state[i])) P.zero.push_back((uint32_t)i);
+  std::sort(P.zero.begin(), P.zero.end());
+  return SEM_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -666,6 +801,7 @@ int sem_ctx_create(sem_ctx** out, int p, int64_t n_elem, int64_t n_node, int dpn
   c->lw = c->epw * c->n;
   c->n_groups = (n_elem + c->epw - 1) / c->epw;
   if (const char* s = std::getenv("SEM_GEOM_MODE")) c->geom_mode = std::atoi(s);
+  if (const char* s = std::getenv("SEM_KERNEL")) c->kernel = std::atoi(s);
   if (c->n_groups > 0x7FFFFFFFll) {
     delete c;
     return fail(SEM_E_INVALID, "too many elements");
@@ -745,9 +881,15 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
   // prefetch registers halve occupancy.  Not kept.
   int rounds = 1;
   if (const char* s = std::getenv("SEM_CHAIN_ROUNDS")) rounds = std::max(1, std::atoi(s));
-  int rc = build_plan(h, c->n_elem, c->n_node, n, rounds, state, P);
+  const bool mfma = want_mfma(c);
+  int rc = mfma ? build_plan_elem(h, c->n_elem, c->n_node, n, state, P)
+                : build_plan(h, c->n_elem, c->n_node, n, rounds, state, P);
   if (rc) return rc;
-  c->rounds = rounds;
+  c->mfma = mfma;
+  c->epw = mfma ? 1 : epw_of(n);
+  c->lw = c->epw * n;
+  c->n_groups = (c->n_elem + c->epw - 1) / c->epw;
+  c->rounds = mfma ? 1 : rounds;
   c->n_slots = P.n_slots;
   std::vector<uint32_t>().swap(h);
   c->d_e2n = d_e2n;
@@ -787,12 +929,13 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
 int sem_plan_info(sem_ctx* c, int64_t* info, int n_info) {
   if (!c || !info || n_info < 1) return fail(SEM_E_INVALID, "bad arguments");
   const int64_t nc = c->colour_start.empty() ? 0 : (int64_t)c->colour_start.size() - 1;
-  int64_t vals[8 + MAX_COLOURS + 1] = {c->n_groups, c->n_zero, c->n_atomic_groups,
-                                       c->conforming ? 1 : 0, c->epw, nc, c->rounds,
-                                       c->n_slots};
+  constexpr int NV = 8 + MAX_COLOURS + 1 + 1;
+  int64_t vals[NV] = {c->n_groups, c->n_zero, c->n_atomic_groups, c->conforming ? 1 : 0,
+                      c->epw,      nc,        c->rounds,          c->n_slots};
   for (int64_t q = 0; q < nc && q <= MAX_COLOURS; ++q)
     vals[8 + q] = c->colour_start[q + 1] - c->colour_start[q];
-  for (int i = 0; i < n_info && i < 8 + MAX_COLOURS + 1; ++i) info[i] = vals[i];
+  vals[NV - 1] = c->mfma ? SEM_KERNEL_MFMA : SEM_KERNEL_COLUMN;
+  for (int i = 0; i < n_info && i < NV; ++i) info[i] = vals[i];
   return SEM_OK;
 }
 
@@ -809,6 +952,16 @@ int sem_set_geom_mode(sem_ctx* c, int mode) {
   if (mode != SEM_GEOM_STORED && mode != SEM_GEOM_NODAL && mode != SEM_GEOM_AUTO)
     return fail(SEM_E_INVALID, "unknown geometry mode " + std::to_string(mode));
   c->geom_mode = mode;
+  return SEM_OK;
+}
+
+int sem_set_kernel(sem_ctx* c, int kernel) {
+  if (!c) return fail(SEM_E_INVALID, "null ctx");
+  if (kernel != SEM_KERNEL_COLUMN && kernel != SEM_KERNEL_MFMA && kernel != SEM_KERNEL_AUTO)
+    return fail(SEM_E_INVALID, "unknown kernel " + std::to_string(kernel));
+  if (kernel == SEM_KERNEL_MFMA && (c->dpn != 1 || c->n > 16))
+    return fail(SEM_E_NOTIMPL, "the MFMA kernel needs dofs_per_node == 1 and p <= 15");
+  c->kernel = kernel;
   return SEM_OK;
 }
 

@@ -790,6 +790,124 @@ __global__ void __launch_bounds__(CHAIN_BLOCK)
 }
 
 // ---------------------------------------------------------------------------
+// Poisson stiffness action on the fp64 matrix cores (n = p + 1 <= 16).
+//
+// One element per wavefront, its nodal arrays held as 16 x 16 tiles (zero
+// padded) in the v_mfma_f64_16x16x4_f64 accumulator layout: lane l, register
+// i holds entry (row h + 4i, column c) with c = l & 15, h = l >> 4.  That
+// register i is also the B operand of k-step i of a product contracting over
+// the row index, and used as the A operand it supplies the TRANSPOSED tile.
+// With the element slab gathered twice (L1: lane <-> xi1 column j, registers
+// <-> xi0 row m; L2: lane <-> m, registers <-> j) and A = D held as
+// Da[s] = D[c][4s + h], the four derivatives come out of four products
+// without any LDS transpose:
+//   d0 (L1) = D U          mfma(Da, U_L1)      d1 (L1) = U D^T   mfma(U_L2, Da)
+//   d0 (L2) = (D U)^T      mfma(U_L1, Da)      d1 (L2) = (U D^T)^T mfma(Da, U_L2)
+// then w0 = G00 d0 + G01 d1 in L1 and w1 = G01 d0 + G11 d1 in L2 (the
+// factors are read in both layouts from one compact per-element array), and
+//   y (L1) = D^T w0 + w1 D = mfma(Dt, w0_L1) + mfma(w1_L2, Dt),  Dt[s] = D[4s+h][c]
+// accumulate into one tile.  6 products x ceil(n/4) MFMAs per element; the
+// contraction count is 6 instead of 4, but there is no wave_sync, no LDS and
+// few VGPRs, so many elements are in flight per SIMD.  Same arithmetic as
+// the column kernel, summed in a different order.
+//
+// Padding lanes / rows (index >= n) load a valid entry (clamped index) and
+// zero it with a select: no load sits under a branch.
+//
+// Elements of one launch (colour) share no node (element-level colouring,
+// build_plan_elem), so the scatter is plain stores / read-modify-writes.
+// Maps and factors are compact per element: mapP[slot][r][j], GP[slot][c][r][j].
+// ---------------------------------------------------------------------------
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ dbl4 mfma_f64(double a, double b, dbl4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+constexpr int MFMA_EPB = BLOCK / WAVE;  // elements (waves) per workgroup
+
+template <int N>
+__global__ void __launch_bounds__(BLOCK)
+    k_poisson_mfma(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
+                   const double* __restrict__ u, double* __restrict__ y,
+                   const double* __restrict__ gD, int64_t s0, int64_t s1, int accumulate) {
+  static_assert(N <= 16, "one 16x16 tile per element");
+  constexpr int KS = (N + 3) / 4;  // k-steps covering the n nodes of a line
+  constexpr int NN = N * N;
+  const int lane = threadIdx.x % WAVE;
+  const int64_t slot = s0 + (int64_t)blockIdx.x * MFMA_EPB + threadIdx.x / WAVE;
+  if (slot >= s1) return;  // uniform per wavefront; no workgroup barrier below
+  const int c = lane & 15;
+  const int h = lane >> 4;
+  const bool cok = c < N;
+  const int cc = cok ? c : N - 1;
+  bool ok[KS];
+  int rr[KS];
+#pragma unroll
+  for (int i = 0; i < KS; ++i) {
+    const int r = 4 * i + h;
+    ok[i] = cok && r < N;
+    rr[i] = r < N ? r : N - 1;
+  }
+  double Da[KS], Dt[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const double a = gD[cc * N + rr[s]], t = gD[rr[s] * N + cc];
+    Da[s] = ok[s] ? a : 0.0;
+    Dt[s] = ok[s] ? t : 0.0;
+  }
+  const uint32_t* mp = mapP + slot * NN;
+  const double* gp = GP + slot * (3 * NN);
+  uint32_t raw[KS];
+  double x1[KS], x2[KS];
+#pragma unroll
+  for (int i = 0; i < KS; ++i) {
+    const uint32_t e1 = mp[rr[i] * N + cc];  // L1: (m = r, j = c)
+    const uint32_t e2 = mp[cc * N + rr[i]];  // L2: (m = c, j = r)
+    const double v1 = u[e1 & GID_MASK], v2 = u[e2 & GID_MASK];
+    raw[i] = ok[i] ? e1 : (W_SKIP << CODE_SHIFT);
+    x1[i] = ok[i] ? v1 : 0.0;
+    x2[i] = ok[i] ? v2 : 0.0;
+  }
+  const dbl4 z = {0.0, 0.0, 0.0, 0.0};
+  dbl4 w0 = z, w1 = z;
+  {
+    dbl4 d0 = z, d1 = z;  // L1
+#pragma unroll
+    for (int s = 0; s < KS; ++s) d0 = mfma_f64(Da[s], x1[s], d0);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) d1 = mfma_f64(x2[s], Da[s], d1);
+#pragma unroll
+    for (int i = 0; i < KS; ++i) {
+      const double g00 = gp[0 * NN + rr[i] * N + cc];
+      const double g01 = gp[1 * NN + rr[i] * N + cc];
+      w0[i] = ok[i] ? fma(g00, d0[i], g01 * d1[i]) : 0.0;
+    }
+  }
+  {
+    dbl4 d0 = z, d1 = z;  // L2
+#pragma unroll
+    for (int s = 0; s < KS; ++s) d0 = mfma_f64(x1[s], Da[s], d0);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) d1 = mfma_f64(Da[s], x2[s], d1);
+#pragma unroll
+    for (int i = 0; i < KS; ++i) {
+      const double g01 = gp[1 * NN + cc * N + rr[i]];
+      const double g11 = gp[2 * NN + cc * N + rr[i]];
+      w1[i] = ok[i] ? fma(g01, d0[i], g11 * d1[i]) : 0.0;
+    }
+  }
+  dbl4 acc = z;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) acc = mfma_f64(Dt[s], w0[s], acc);
+#pragma unroll
+  for (int s = 0; s < KS; ++s) acc = mfma_f64(w1[s], Dt[s], acc);
+  // row 4i + h < N implies i < KS; padding entries carry SKIP
+#pragma unroll
+  for (int i = 0; i < KS; ++i) emit1(y, raw[i], acc[i], accumulate);
+}
+
+// ---------------------------------------------------------------------------
 // Geometry: nodes -> x_phys -> J -> det/inv -> W -> operator factors.
 // Thread per local node, EPB elements per block, LDS staging (setup path).
 // ---------------------------------------------------------------------------
@@ -804,7 +922,7 @@ template <int N>
 __global__ void __launch_bounds__(GeomShape<N>::THREADS)
     k_geometry(const double* __restrict__ nodes, int64_t n_node, const uint32_t* __restrict__ e2n,
                int64_t n_elem, const double* __restrict__ gVinv, const double* __restrict__ gD,
-               const double* __restrict__ gw, int op_kind, const int* __restrict__ gpos,
+               const double* __restrict__ gw, int op_kind, int epw, const int* __restrict__ gpos,
                double* __restrict__ GP, double* __restrict__ xph, double* __restrict__ Jo,
                double* __restrict__ iJo, double* __restrict__ dJo, double* __restrict__ dJW,
                double2* __restrict__ XG, const uint32_t* __restrict__ owner,
@@ -812,8 +930,7 @@ __global__ void __launch_bounds__(GeomShape<N>::THREADS)
   using S = GeomShape<N>;
   constexpr int NN = S::NN;
   constexpr int EPB = S::EPB;
-  constexpr int EPW = WAVE / N;
-  constexpr int LW = EPW * N;
+  const int LW = epw * N;  // packed row: the epw elements of a group (1 for the MFMA kernel)
   __shared__ double sV[NN], sD[NN], sw[N];
   __shared__ double sx[EPB][2][NN], st[EPB][2][NN];
   const int tid = threadIdx.x;
@@ -921,8 +1038,8 @@ __global__ void __launch_bounds__(GeomShape<N>::THREADS)
   if (dJo) dJo[base] = det;
   if (dJW) dJW[base] = W;
   if (GP) {
-    const int64_t grp = e / EPW;
-    const int kk = (int)(e - grp * EPW);
+    const int64_t grp = e / epw;
+    const int kk = (int)(e - grp * epw);
     const int64_t gg = gpos[grp];
     const int ncomp = (op_kind == 0) ? 3 : 7;
     double* o = GP + gg * (int64_t)(ncomp * N * LW) + m * LW + kk * N + nq;

@@ -222,7 +222,7 @@ class OverlappedOperator(object):
     races the interior kernel."""
 
     def __init__(self, p, nodes, e2n, neighbors, dofs_per_node=1, device=None, group=None,
-                 geometry="auto", kind=0):
+                 geometry="auto", kind=0, kernel="auto"):
         from .operators import SEMOperator
         self.dpn = dofs_per_node
         self.kind = kind
@@ -237,12 +237,12 @@ class OverlappedOperator(object):
         self.n_iface_elem, self.n_interior_elem = ie.size, be.size
         if ie.size == 0 or be.size == 0:  # nothing to overlap
             self.ops = [SEMOperator(p, e2n, nodes, dofs_per_node, device=self.device,
-                                    geometry=geometry)]
+                                    geometry=geometry, kernel=kernel)]
         else:
             self.ops = [SEMOperator(p, e2n[ie], nodes, dofs_per_node, device=self.device,
-                                    geometry=geometry, node_state=st_i),
+                                    geometry=geometry, node_state=st_i, kernel=kernel),
                         SEMOperator(p, e2n[be], nodes, dofs_per_node, device=self.device,
-                                    geometry=geometry, node_state=st_b)]
+                                    geometry=geometry, node_state=st_b, kernel=kernel)]
         for op in self.ops:
             op.compute_geometry(kind)
         self.ndof = self.ops[0].ndof

@@ -85,6 +85,11 @@ class SEMOperator(object):
         traffic) or streamed from precomputed per-element factors ("stored");
         "auto" (default) picks nodal for p <= 8.  See include/sem_hip.h
         sem_set_geom_mode.
+    kernel : {"auto", "column", "mfma"}
+        Kernel family of the Poisson action: the LDS column kernel or the
+        fp64 matrix-core element kernel (p <= 15, stored factors); "auto"
+        (default) resolves to the library's measured choice (column).  See
+        include/sem_hip.h sem_set_kernel.
     node_state : array-like uint8 [n_node], optional
         For operators that share the output vector with others applied
         before / after it in stream order: NODE_PRIOR marks nodes whose y
@@ -95,11 +100,14 @@ class SEMOperator(object):
 
     GEOMETRY_MODES = {"stored": _lib.GEOM_STORED, "nodal": _lib.GEOM_NODAL,
                       "auto": _lib.GEOM_AUTO}
+    KERNELS = {"column": _lib.KERNEL_COLUMN, "mfma": _lib.KERNEL_MFMA, "auto": _lib.KERNEL_AUTO}
 
     def __init__(self, p, e2n, nodes, dofs_per_node=1, basis=None, device=None,
-                 geometry="auto", node_state=None):
+                 geometry="auto", node_state=None, kernel="auto"):
         if geometry not in self.GEOMETRY_MODES:
             raise ValueError("geometry must be one of %s" % sorted(self.GEOMETRY_MODES))
+        if kernel not in self.KERNELS:
+            raise ValueError("kernel must be one of %s" % sorted(self.KERNELS))
         self.geometry = geometry
         self._lib = _lib.load()
         self.p = int(p)
@@ -125,6 +133,8 @@ class SEMOperator(object):
                                                 self.dpn, dev))
             self._ctx = ctx
             _lib.check(self._lib.sem_set_geom_mode(ctx, self.GEOMETRY_MODES[geometry]))
+            if kernel != "auto":
+                _lib.check(self._lib.sem_set_kernel(ctx, self.KERNELS[kernel]))
             _lib.check(self._lib.sem_set_basis(ctx, _lib.dptr(self.D), _lib.dptr(self.w)))
             if node_state is None:
                 _lib.check(self._lib.sem_set_map(ctx, _lib.tptr(self.e2n), _lib.stream_ptr()))
@@ -169,15 +179,16 @@ class SEMOperator(object):
 
     def plan_info(self):
         """Setup plan of the scatter (see include/sem_hip.h sem_plan_info)."""
-        info = (C.c_int64 * 17)()
-        _lib.check(self._lib.sem_plan_info(self._ctx, info, 17))
+        info = (C.c_int64 * 18)()
+        _lib.check(self._lib.sem_plan_info(self._ctx, info, 18))
         v = list(info)
         counts = [x for x in v[8:8 + v[5]]]
         while counts and counts[-1] == 0:
             counts.pop()
         return dict(groups=v[0], zero_list=v[1], atomic_groups=v[2], conforming=bool(v[3]),
                     elements_per_group=v[4], colours=len(counts), rounds=v[6], slots=v[7],
-                    chains_per_colour=counts)
+                    chains_per_colour=counts,
+                    kernel="mfma" if v[17] == _lib.KERNEL_MFMA else "column")
 
     # ------------------------------------------------------------------
     def compute_geometry(self, kind=POISSON, stream=None):

@@ -306,3 +306,123 @@ def test_shared_output_split(sem, gll, geometry):
     op_i.apply(u, out=y, accumulate=True)
     op_b.apply(u, out=y, accumulate=True)
     assert (y - y0 - ref).norm().item() <= 1e-13 * ref.norm().item()
+
+
+# ---------------------------------------------------------------------------
+# fp64 matrix-core kernel (k_poisson_mfma, sem_set_kernel SEM_KERNEL_MFMA)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("name", [c for c in ACTION_CASES if not c.startswith("p16")])
+def test_poisson_action_golden_mfma(sem, poisson_action, gll, name):
+    import sem_oracle
+    fx = poisson_action
+    p = int(fx[name + "_p"])
+    op = sem.SEMOperator(p, fx[name + "_e2n"], fx[name + "_nodes"], kernel="mfma")
+    assert op.plan_info()["kernel"] == "mfma"
+    y = op.apply(torch.from_numpy(fx[name + "_u"]).cuda()).cpu().numpy()
+    y_ext = None
+    if p > 10:
+        y_ext = sem_oracle.poisson_apply_extended(fx[name + "_nodes"], fx[name + "_e2n"],
+                                                  gll["half_%d" % p], fx[name + "_u"])
+    assert_parity(y, fx[name + "_y"], y_ext, TOL_ACTION)
+
+
+@pytest.mark.parametrize("p", list(range(1, 16)))
+def test_poisson_all_orders_mfma(sem, gll, p):
+    import sem_oracle
+    from spectralelementmethod_amd import meshgen
+    nodes, e2n = meshgen.structured_square(5, 4, p, warp=0.05)
+    prob = sem_oracle.PoissonProblem(nodes, e2n, gll["half_%d" % p])
+    u = np.random.default_rng(p).standard_normal(prob.ndof)
+    op = sem.SEMOperator(p, e2n, nodes, kernel="mfma")
+    y = op.apply(torch.from_numpy(u).cuda()).cpu().numpy()
+    y_ext = sem_oracle.poisson_apply_extended(nodes, e2n, gll["half_%d" % p], u)
+    assert_parity(y, prob.apply(u), y_ext, TOL_ACTION)
+
+
+def test_mfma_auto_selection_and_limits(sem, poisson_action):
+    from spectralelementmethod_amd import meshgen
+    for p, expect in ((8, "column"), (9, "column"), (12, "column"), (16, "column")):
+        nodes, e2n = meshgen.structured_square(3, 2, p)
+        assert sem.SEMOperator(p, e2n, nodes).plan_info()["kernel"] == expect, p
+    # nodal geometry requested explicitly keeps the column kernel under auto
+    nodes, e2n = meshgen.structured_square(3, 2, 12)
+    assert sem.SEMOperator(12, e2n, nodes, geometry="nodal").plan_info()["kernel"] == "column"
+    nodes, e2n = meshgen.structured_square(2, 2, 16)
+    with pytest.raises(NotImplementedError):
+        sem.SEMOperator(16, e2n, nodes, kernel="mfma")
+    fx = poisson_action
+    with pytest.raises(NotImplementedError):
+        sem.SEMOperator(4, fx["p4_4x4_e2n"], fx["p4_4x4_nodes"], dofs_per_node=2, kernel="mfma")
+    with pytest.raises(ValueError):
+        sem.SEMOperator(4, fx["p4_4x4_e2n"], fx["p4_4x4_nodes"], kernel="bogus")
+
+
+def test_mfma_accumulate_unreferenced_nonconforming(sem, poisson_action, gll):
+    import sem_oracle
+    fx = poisson_action
+    name = "p4_4x4"
+    nodes, e2n, u = fx[name + "_nodes"], fx[name + "_e2n"], fx[name + "_u"]
+    op = sem.SEMOperator(4, e2n, nodes, kernel="mfma")
+    ut = torch.from_numpy(u).cuda()
+    y0 = torch.linspace(-1, 1, u.size, dtype=torch.float64, device="cuda")
+    y = y0.clone()
+    op.apply(ut, out=y, accumulate=True)
+    assert rel_l2(y.cpu().numpy(), y0.cpu().numpy() + fx[name + "_y"]) < TOL_ACTION
+    y.fill_(123.0)
+    op.apply(ut, out=y)
+    assert rel_l2(y.cpu().numpy(), fx[name + "_y"]) < TOL_ACTION
+    # unreferenced trailing nodes are zeroed in overwrite mode
+    extra = np.concatenate([nodes, np.array([[5.0, 6.0], [5.0, 6.0]])], axis=1)
+    op = sem.SEMOperator(4, e2n, extra, kernel="mfma")
+    y = torch.full((op.ndof,), 7.0, dtype=torch.float64, device="cuda")
+    op.apply(torch.from_numpy(np.concatenate([u, [1.0, 2.0]])).cuda(), out=y)
+    y = y.cpu().numpy()
+    assert y[-2] == 0.0 and y[-1] == 0.0
+    assert rel_l2(y[:-2], fx[name + "_y"]) < TOL_ACTION
+    # duplicated elements (shared interior nodes): non-conforming map, the
+    # colouring then separates elements sharing any node
+    e2d = np.concatenate([e2n, e2n[:2]])
+    op = sem.SEMOperator(4, e2d, nodes, kernel="mfma")
+    assert not op.plan_info()["conforming"]
+    y = op.apply(ut).cpu().numpy()
+    assert rel_l2(y, sem_oracle.PoissonProblem(nodes, e2d, gll["half_4"]).apply(u)) < TOL_ACTION
+
+
+def test_mfma_shared_output_split(sem):
+    from spectralelementmethod_amd import meshgen
+    from spectralelementmethod_amd.distributed import split_interface_elements
+    p, nex, ney = 10, 7, 4
+    nodes, e2n = meshgen.structured_square(nex, ney, p, warp=0.05)
+    Ny = ney * p + 1
+    nn = nodes.shape[1]
+    ie, be, st_i, st_b = split_interface_elements(e2n, {1: np.arange(nn - Ny, nn)})
+    full = sem.SEMOperator(p, e2n, nodes, kernel="column", geometry="stored")
+    op_i = sem.SEMOperator(p, e2n[ie], nodes, node_state=st_i, kernel="mfma")
+    op_b = sem.SEMOperator(p, e2n[be], nodes, node_state=st_b, kernel="mfma")
+    u = torch.randn(full.ndof, dtype=torch.float64, device="cuda",
+                    generator=torch.Generator(device="cuda").manual_seed(9))
+    ref = full.apply(u)
+    y = torch.full_like(u, 3.0)
+    op_i.apply(u, out=y)
+    op_b.apply(u, out=y)
+    assert (y - ref).norm().item() <= 1e-13 * ref.norm().item()
+
+
+def test_mfma_vs_column_larger(sem):
+    """The two kernel families agree at 2.4M DOF (p = 12, 128 x 96 warped),
+    and the MFMA action is symmetric and annihilates constants."""
+    from spectralelementmethod_amd import meshgen
+    p = 12
+    nodes, e2n = meshgen.structured_square(128, 96, p, warp=0.05)
+    g = torch.Generator(device="cuda").manual_seed(4)
+    col = sem.SEMOperator(p, e2n, nodes, kernel="column", geometry="stored")
+    mf = sem.SEMOperator(p, e2n, nodes, kernel="mfma")
+    u = torch.randn(col.ndof, dtype=torch.float64, device="cuda", generator=g)
+    v = torch.randn(col.ndof, dtype=torch.float64, device="cuda", generator=g)
+    ya, yb = col.apply(u), mf.apply(u)
+    assert (ya - yb).norm().item() < 1e-13 * ya.norm().item()
+    Kv = mf.apply(v)
+    a, b = torch.dot(v, yb).item(), torch.dot(u, Kv).item()
+    assert abs(a - b) <= 1e-11 * max(abs(a), abs(b))
+    K1 = mf.apply(torch.ones_like(u))
+    assert K1.abs().max().item() < 1e-10 * yb.abs().max().item()
