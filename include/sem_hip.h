@@ -154,8 +154,9 @@ int sem_set_geom_mode(sem_ctx* ctx, int mode);
  *    per element, no LDS); element-level colouring; stored factors only
  *    (a NODAL request is ignored); n = p + 1 <= 16 and dpn = 1, else
  *    SEM_E_NOTIMPL.
- *  SEM_KERNEL_AUTO (default): COLUMN (measured faster at every order on
- *    MI355X; the threshold SEM_MFMA_MIN_N is a build knob).
+ *  SEM_KERNEL_AUTO (default): MFMA for 12 <= p <= 15 unless NODAL geometry
+ *    was requested, COLUMN otherwise (measured on MI355X, DESIGN.md §4.6;
+ *    the threshold SEM_MFMA_MIN_N is a build knob).
  * The environment variable SEM_KERNEL (0/1/2) sets the initial value. */
 #define SEM_KERNEL_COLUMN 0
 #define SEM_KERNEL_MFMA 1

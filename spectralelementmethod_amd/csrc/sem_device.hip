@@ -358,11 +358,11 @@ bool nodal_mode(const sem_ctx* c) {
 
 // AUTO: the MFMA element kernel from SEM_MFMA_MIN_N nodes per line up,
 // Poisson only (dpn = 1), one 16 x 16 tile (n <= 16), and not when nodal
-// geometry was requested explicitly.  Measured on MI355X
-// the column kernel is faster at every order, so AUTO never picks MFMA
-// (17 > the largest tile) unless built with a smaller threshold.
+// geometry was requested explicitly.  Measured on MI355X at ~1e7 DOF
+// (profiles/r01/mfma_v2): the MFMA kernel wins from p = 12
+// (n = 13) to p = 15, the column kernel up to p = 11.
 #ifndef SEM_MFMA_MIN_N
-#define SEM_MFMA_MIN_N 17
+#define SEM_MFMA_MIN_N 13
 #endif
 bool want_mfma(const sem_ctx* c) {
   if (c->dpn != 1 || c->n > 16) return false;
@@ -387,9 +387,10 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
     if (c1 <= c0) continue;
     const int grid = (int)(c1 - c0);
     if (op_kind == SEM_OP_POISSON && c->mfma) {
-      if constexpr (N <= 16)
+      if constexpr (N <= 16) {
         hipLaunchKernelGGL((k_poisson_mfma<N>), dim3((grid + MFMA_EPB - 1) / MFMA_EPB),
                            dim3(BLOCK), 0, st, c->d_mapP, c->d_GP[0], u, y, c->d_D, c0, c1, acc);
+      }
     } else if (op_kind == SEM_OP_POISSON && nodal)
       hipLaunchKernelGGL((k_poisson_apply<N, true>), dim3(grid), dim3(CHAIN_BLOCK), 0, st,
                          c->d_mapP, nullptr, c->d_XG, u, y, c0, c1, c->rounds, acc, D, w);

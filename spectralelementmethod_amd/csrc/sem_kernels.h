@@ -603,6 +603,24 @@ __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_
 #endif
 }
 
+// Workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8 share
+// one L2).  With SEM_XCD_SWIZZLE the chain index is remapped so that each XCD
+// works on one contiguous run of chains (neighbouring chains share node
+// columns of u / x_phys); a bijection of [0, nwg) for any nwg.
+#ifndef SEM_XCD_SWIZZLE
+#define SEM_XCD_SWIZZLE 0
+#endif
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nwg) {
+#if SEM_XCD_SWIZZLE
+  constexpr int64_t NX = 8;
+  const int64_t q = nwg / NX, r = nwg % NX, x = b % NX, k = b / NX;
+  return x * q + (x < r ? x : r) + k;
+#else
+  (void)nwg;
+  return b;
+#endif
+}
+
 // ---------------------------------------------------------------------------
 // Poisson stiffness action: one workgroup per chain, chains [c0, c1).
 // ---------------------------------------------------------------------------
@@ -616,7 +634,7 @@ __global__ void __launch_bounds__(CHAIN_BLOCK, SEM_POISSON_MIN_WAVES)
   constexpr int NT = NODAL ? 2 : 1;  // tiles per element slot
   __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * T::ES * NT];
   __shared__ double carry[2][CHAIN_WAVES][1][N];
-  const int64_t chain = c0 + blockIdx.x;
+  const int64_t chain = c0 + xcd_block(blockIdx.x, gridDim.x);
   if (chain >= c1) return;  // uniform over the workgroup
   const int wave = threadIdx.x / WAVE;
   const int lane = threadIdx.x % WAVE;
@@ -794,29 +812,32 @@ __global__ void __launch_bounds__(CHAIN_BLOCK)
 //
 // One element per wavefront, its nodal arrays held as 16 x 16 tiles (zero
 // padded) in the v_mfma_f64_16x16x4_f64 accumulator layout: lane l, register
-// i holds entry (row h + 4i, column c) with c = l & 15, h = l >> 4.  That
-// register i is also the B operand of k-step i of a product contracting over
-// the row index, and used as the A operand it supplies the TRANSPOSED tile.
-// With the element slab gathered twice (L1: lane <-> xi1 column j, registers
-// <-> xi0 row m; L2: lane <-> m, registers <-> j) and A = D held as
-// Da[s] = D[c][4s + h], the four derivatives come out of four products
-// without any LDS transpose:
-//   d0 (L1) = D U          mfma(Da, U_L1)      d1 (L1) = U D^T   mfma(U_L2, Da)
-//   d0 (L2) = (D U)^T      mfma(U_L1, Da)      d1 (L2) = (U D^T)^T mfma(Da, U_L2)
-// then w0 = G00 d0 + G01 d1 in L1 and w1 = G01 d0 + G11 d1 in L2 (the
-// factors are read in both layouts from one compact per-element array), and
-//   y (L1) = D^T w0 + w1 D = mfma(Dt, w0_L1) + mfma(w1_L2, Dt),  Dt[s] = D[4s+h][c]
-// accumulate into one tile.  6 products x ceil(n/4) MFMAs per element; the
-// contraction count is 6 instead of 4, but there is no wave_sync, no LDS and
-// few VGPRs, so many elements are in flight per SIMD.  Same arithmetic as
-// the column kernel, summed in a different order.
+// i holds entry (row h + 4i, column c) with c = l & 15, h = l >> 4 ("L1":
+// lane <-> xi1 index j, registers <-> xi0 index m).  Register i is also the
+// B operand of k-step i of a product contracting over the row index, and
+// used as the A operand it supplies the TRANSPOSED tile.  With A = D held as
+// Da[s] = D[c][4s + h] and Dt[s] = D[4s + h][c]:
+//   d0 = D U     = mfma(Da, U_L1)        d1 = U D^T = mfma(U_L2, Da)
+//   w0 = G00 d0 + G01 d1,  w1 = G01 d0 + G11 d1      (pointwise, L1)
+//   y  = D^T w0 + w1 D = mfma(Dt, w0) + mfma(w1_L2, Dt)
+// where X_L2 (lane <-> m, registers <-> j) is X transposed through a
+// wave-private 16 x 17 LDS tile (rows padded to 17 doubles: the row write
+// and the column read are both bank-conflict free).  4 products x ceil(n/4)
+// MFMAs per element; map, u and the factors are read in the L1 layout only.
+// One element per wavefront: walking 2 / 4 / 8 slots per wavefront with D
+// kept in registers and the next map prefetched measured 10 / 24 / 36 %
+// slower at p = 12 than more, shorter waves.  Same arithmetic as the column kernel (SURVEY.md §8(a)
+// a11), summed in a different order.
 //
 // Padding lanes / rows (index >= n) load a valid entry (clamped index) and
-// zero it with a select: no load sits under a branch.
+// zero it with a select: no load sits under a branch.  Elements of one launch
+// (colour) share no node (element-level colouring, build_plan_elem), so the
+// scatter is plain stores / read-modify-writes.  Maps and factors are compact
+// per element: mapP[slot][r][j], GP[slot][c][r][j].
 //
-// Elements of one launch (colour) share no node (element-level colouring,
-// build_plan_elem), so the scatter is plain stores / read-modify-writes.
-// Maps and factors are compact per element: mapP[slot][r][j], GP[slot][c][r][j].
+// A first form (six products, U and the factors gathered in both layouts,
+// no LDS) measured 0.215 / 0.179 ms at p = 12 / 15 against 0.191 / 0.139 for
+// this one (profiles/r01/mfma_v1).
 // ---------------------------------------------------------------------------
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
@@ -826,82 +847,86 @@ __device__ __forceinline__ dbl4 mfma_f64(double a, double b, dbl4 c) {
 
 constexpr int MFMA_EPB = BLOCK / WAVE;  // elements (waves) per workgroup
 
+constexpr int MFMA_TS = 17;  // LDS tile row stride (doubles)
+
 template <int N>
-__global__ void __launch_bounds__(BLOCK)
+__device__ __forceinline__ void mfma_transpose(double* T, int h, int c, const double (&in)[(N + 3) / 4],
+                                               double (&out)[(N + 3) / 4]) {
+  constexpr int KS = (N + 3) / 4;
+#pragma unroll
+  for (int i = 0; i < KS; ++i) T[(4 * i + h) * MFMA_TS + c] = in[i];
+  wave_sync();
+#pragma unroll
+  for (int i = 0; i < KS; ++i) out[i] = T[c * MFMA_TS + 4 * i + h];
+  wave_sync();
+}
+
+#ifndef SEM_MFMA_MIN_WAVES
+#define SEM_MFMA_MIN_WAVES 1
+#endif
+template <int N>
+__global__ void __launch_bounds__(BLOCK, SEM_MFMA_MIN_WAVES)
     k_poisson_mfma(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
                    const double* __restrict__ u, double* __restrict__ y,
                    const double* __restrict__ gD, int64_t s0, int64_t s1, int accumulate) {
   static_assert(N <= 16, "one 16x16 tile per element");
   constexpr int KS = (N + 3) / 4;  // k-steps covering the n nodes of a line
   constexpr int NN = N * N;
+  __shared__ double lds[MFMA_EPB][16 * MFMA_TS];
   const int lane = threadIdx.x % WAVE;
-  const int64_t slot = s0 + (int64_t)blockIdx.x * MFMA_EPB + threadIdx.x / WAVE;
+  const int wave = threadIdx.x / WAVE;
+  const int64_t slot = s0 + (int64_t)blockIdx.x * MFMA_EPB + wave;
   if (slot >= s1) return;  // uniform per wavefront; no workgroup barrier below
+  double* T = lds[wave];
   const int c = lane & 15;
   const int h = lane >> 4;
   const bool cok = c < N;
   const int cc = cok ? c : N - 1;
   bool ok[KS];
-  int rr[KS];
+  int off[KS];  // (r, c) offset in an element's [n][n] arrays, clamped into range
 #pragma unroll
   for (int i = 0; i < KS; ++i) {
     const int r = 4 * i + h;
     ok[i] = cok && r < N;
-    rr[i] = r < N ? r : N - 1;
-  }
-  double Da[KS], Dt[KS];
-#pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    const double a = gD[cc * N + rr[s]], t = gD[rr[s] * N + cc];
-    Da[s] = ok[s] ? a : 0.0;
-    Dt[s] = ok[s] ? t : 0.0;
+    off[i] = (r < N ? r : N - 1) * N + cc;
   }
   const uint32_t* mp = mapP + slot * NN;
   const double* gp = GP + slot * (3 * NN);
+  double x1[KS], x2[KS], g0[KS], g1[KS], g2[KS], Da[KS], Dt[KS];
   uint32_t raw[KS];
-  double x1[KS], x2[KS];
 #pragma unroll
   for (int i = 0; i < KS; ++i) {
-    const uint32_t e1 = mp[rr[i] * N + cc];  // L1: (m = r, j = c)
-    const uint32_t e2 = mp[cc * N + rr[i]];  // L2: (m = c, j = r)
-    const double v1 = u[e1 & GID_MASK], v2 = u[e2 & GID_MASK];
-    raw[i] = ok[i] ? e1 : (W_SKIP << CODE_SHIFT);
-    x1[i] = ok[i] ? v1 : 0.0;
-    x2[i] = ok[i] ? v2 : 0.0;
+    const uint32_t e = mp[off[i]];
+    const double v = u[e & GID_MASK];
+    x1[i] = ok[i] ? v : 0.0;
+    raw[i] = ok[i] ? e : (W_SKIP << CODE_SHIFT);
+    g0[i] = gp[0 * NN + off[i]];
+    g1[i] = gp[1 * NN + off[i]];
+    g2[i] = gp[2 * NN + off[i]];
+    const int k = 4 * i + h < N ? 4 * i + h : N - 1;
+    const double a = gD[cc * N + k], t = gD[k * N + cc];
+    Da[i] = ok[i] ? a : 0.0;
+    Dt[i] = ok[i] ? t : 0.0;
   }
   const dbl4 z = {0.0, 0.0, 0.0, 0.0};
-  dbl4 w0 = z, w1 = z;
-  {
-    dbl4 d0 = z, d1 = z;  // L1
+  mfma_transpose<N>(T, h, c, x1, x2);
+  dbl4 d0 = z, d1 = z;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) d0 = mfma_f64(Da[s], x1[s], d0);
+  for (int s = 0; s < KS; ++s) d0 = mfma_f64(Da[s], x1[s], d0);
 #pragma unroll
-    for (int s = 0; s < KS; ++s) d1 = mfma_f64(x2[s], Da[s], d1);
+  for (int s = 0; s < KS; ++s) d1 = mfma_f64(x2[s], Da[s], d1);
+  double w0[KS], w1[KS], w1t[KS];
 #pragma unroll
-    for (int i = 0; i < KS; ++i) {
-      const double g00 = gp[0 * NN + rr[i] * N + cc];
-      const double g01 = gp[1 * NN + rr[i] * N + cc];
-      w0[i] = ok[i] ? fma(g00, d0[i], g01 * d1[i]) : 0.0;
-    }
+  for (int i = 0; i < KS; ++i) {
+    w0[i] = ok[i] ? fma(g0[i], d0[i], g1[i] * d1[i]) : 0.0;
+    w1[i] = ok[i] ? fma(g1[i], d0[i], g2[i] * d1[i]) : 0.0;
   }
-  {
-    dbl4 d0 = z, d1 = z;  // L2
-#pragma unroll
-    for (int s = 0; s < KS; ++s) d0 = mfma_f64(x1[s], Da[s], d0);
-#pragma unroll
-    for (int s = 0; s < KS; ++s) d1 = mfma_f64(Da[s], x2[s], d1);
-#pragma unroll
-    for (int i = 0; i < KS; ++i) {
-      const double g01 = gp[1 * NN + cc * N + rr[i]];
-      const double g11 = gp[2 * NN + cc * N + rr[i]];
-      w1[i] = ok[i] ? fma(g01, d0[i], g11 * d1[i]) : 0.0;
-    }
-  }
+  mfma_transpose<N>(T, h, c, w1, w1t);
   dbl4 acc = z;
 #pragma unroll
   for (int s = 0; s < KS; ++s) acc = mfma_f64(Dt[s], w0[s], acc);
 #pragma unroll
-  for (int s = 0; s < KS; ++s) acc = mfma_f64(w1[s], Dt[s], acc);
+  for (int s = 0; s < KS; ++s) acc = mfma_f64(w1t[s], Dt[s], acc);
   // row 4i + h < N implies i < KS; padding entries carry SKIP
 #pragma unroll
   for (int i = 0; i < KS; ++i) emit1(y, raw[i], acc[i], accumulate);

@@ -88,8 +88,9 @@ class SEMOperator(object):
     kernel : {"auto", "column", "mfma"}
         Kernel family of the Poisson action: the LDS column kernel or the
         fp64 matrix-core element kernel (p <= 15, stored factors); "auto"
-        (default) resolves to the library's measured choice (column).  See
-        include/sem_hip.h sem_set_kernel.
+        (default) resolves to the library's measured choice (mfma for
+        12 <= p <= 15 with stored geometry).  See include/sem_hip.h
+        sem_set_kernel.
     node_state : array-like uint8 [n_node], optional
         For operators that share the output vector with others applied
         before / after it in stream order: NODE_PRIOR marks nodes whose y

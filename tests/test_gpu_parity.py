@@ -341,7 +341,7 @@ def test_poisson_all_orders_mfma(sem, gll, p):
 
 def test_mfma_auto_selection_and_limits(sem, poisson_action):
     from spectralelementmethod_amd import meshgen
-    for p, expect in ((8, "column"), (9, "column"), (12, "column"), (16, "column")):
+    for p, expect in ((8, "column"), (11, "column"), (12, "mfma"), (15, "mfma"), (16, "column")):
         nodes, e2n = meshgen.structured_square(3, 2, p)
         assert sem.SEMOperator(p, e2n, nodes).plan_info()["kernel"] == expect, p
     # nodal geometry requested explicitly keeps the column kernel under auto
