@@ -153,6 +153,7 @@ class Mesh(object):
         self._boundary_id_lookup = {}
         self._boundary_map = {}
         self._boundary_cells = []
+        self._adj = None           # [E, n_sides] neighbour cell per side, -1 on a boundary
         self._e2n = None
         self.condensed = False
         self.version = 0           # bumped whenever nodes are permuted
@@ -224,7 +225,7 @@ class Mesh(object):
         self._e2n = None
 
     def add_cells(self, e2n, geometry_id, region_id):
-        """Batched add_cell: e2n [k, *shape]."""
+        """Batched add_cell: e2n [k, *shape]; region_id one id or k ids."""
         e2n = np.ascontiguousarray(e2n, dtype=np.uint32)
         geo = self._geometries[geometry_id]
         if tuple(e2n.shape[1:]) != tuple(geo.shape):
@@ -232,8 +233,30 @@ class Mesh(object):
         self._flush()
         self._blocks.append(e2n)
         self._geom_ids.extend([geometry_id] * e2n.shape[0])
-        self._region_ids.extend([region_id] * e2n.shape[0])
+        if np.ndim(region_id) == 0:
+            self._region_ids.extend([region_id] * e2n.shape[0])
+        else:
+            region_id = [int(r) for r in region_id]
+            if len(region_id) != e2n.shape[0]:
+                raise ValueError("one region id per cell expected")
+            self._region_ids.extend(region_id)
         self._e2n = None
+
+    def set_adjacency(self, adj):
+        """Neighbour cell across each side ([E, n_sides], -1 where the side is
+        on the mesh boundary): the reference's per-cell _adj_map
+        (sem/discrete.py:1048; filled by sem/grid_importers.py:268)."""
+        adj = np.asarray(adj, dtype=np.int64)
+        if adj.shape[0] != self.n_cells:
+            raise ValueError("one adjacency row per cell expected")
+        self._adj = adj
+
+    def adjacency(self, i):
+        """[neighbour or None per side] of cell i (reference _adj_map[i])."""
+        if self._adj is None:
+            geo = self._geometries[self._geom_ids[i]]
+            return [None] * geo.n_sub_geometries()
+        return [int(a) if a >= 0 else None for a in self._adj[i]]
 
     def add_boundary_cell(self, cell_number, bnd_id, ndim, index):
         cell = self._boundary_map.setdefault(cell_number, {})
@@ -266,7 +289,7 @@ class Mesh(object):
     def get_cell(self, i):
         e2n = self.element_map()
         geo = self._geometries[self._geom_ids[i]]
-        return Cell(self, geo, e2n[i], self._region_ids[i], None,
+        return Cell(self, geo, e2n[i], self._region_ids[i], self.adjacency(i),
                     self._boundary_map.get(i, {}))
 
     @property

@@ -89,3 +89,33 @@ def square_dirichlet_left_bottom(nodes, tol=1e-12):
     vals = np.zeros(x.shape)
     vals[on] = 0.2 * ((x[on] + 1) + (y[on] + 1))
     return on, vals
+
+
+def square_boundary_lines(e2n, nex, ney):
+    """Lexicographic node maps of the boundary sides of a structured_square
+    mesh, keyed by side: 'left' (x = x0), 'right', 'bottom' (y = y0), 'top'.
+    Element (ex, ey) has id ex*ney + ey; its row r runs along x, column j
+    along y."""
+    e2n = np.asarray(e2n)
+    out = {"left": [], "right": [], "bottom": [], "top": []}
+    for ey in range(ney):
+        out["left"].append(e2n[ey][0, :])
+        out["right"].append(e2n[(nex - 1) * ney + ey][-1, :])
+    for ex in range(nex):
+        out["bottom"].append(e2n[ex * ney][:, 0])
+        out["top"].append(e2n[ex * ney + ney - 1][:, -1])
+    return out
+
+
+def write_square_msh(path, nex, ney, p, warp=0.0):
+    """The square.geo stand-in as a Gmsh 2.2 binary file: region 'interior',
+    boundaries 'ebc' (left + bottom) and 'nbc' (top + right), the tags of
+    examples/meshes/square.geo:1-15.  Returns (nodes, e2n)."""
+    from .grid_importers import write_msh
+    nodes, e2n = structured_square(nex, ney, p, warp)
+    sides = square_boundary_lines(e2n, nex, ney)
+    lines = [(1, m) for m in sides["left"] + sides["bottom"]] + \
+            [(2, m) for m in sides["top"] + sides["right"]]
+    names = [(1, 1, "ebc"), (1, 2, "nbc"), (2, 3, "interior")]
+    write_msh(path, nodes, e2n, np.full(e2n.shape[0], 3), names, lines)
+    return nodes, e2n

@@ -442,16 +442,48 @@ def gen_geometry():
     print("geometry.npz")
 
 
+def gen_msh():
+    """Gmsh 2.2 binary meshes written by the package's writer
+    (spectralelementmethod_amd.meshgen.write_square_msh: the square.geo
+    stand-in) and read by the REFERENCE reader load_msh
+    (sem/grid_importers.py:45-68).  The .msh files are committed as input
+    fixtures; msh_reference.npz holds what the reference reader built."""
+    sys.path.insert(1, os.path.dirname(os.path.dirname(OUT)))
+    from spectralelementmethod_amd import meshgen
+    import sem.grid_importers as gi
+    out = {}
+    cases = {"sq_p4": (3, 2, 4, 0.05), "sq_p2": (4, 3, 2, 0.0), "sq_p8": (2, 3, 8, 0.05)}
+    for name, (nex, ney, p, warp) in cases.items():
+        path = os.path.join(OUT, "mesh_%s.msh" % name)
+        meshgen.write_square_msh(path, nex, ney, p, warp)
+        mesh = gi.load_msh(path, 2)
+        out[name + "_nodes"] = np.asarray(mesh.nodes, dtype=np.float64)
+        out[name + "_e2n"] = mesh_map(mesh)
+        out[name + "_region"] = np.array([cd.region_id for cd in mesh._cell_data])
+        out[name + "_adj"] = np.array([[-1 if a is None else a for a in row]
+                                       for row in mesh._adj_map], dtype=np.int64)
+        rows = []
+        for cell in sorted(mesh._boundary_map):
+            for bid in sorted(mesh._boundary_map[cell]):
+                for k, bd in enumerate(mesh._boundary_map[cell][bid]):
+                    rows.append((cell, bid, k, bd.ndim, bd.index))
+        out[name + "_bnd"] = np.array(rows, dtype=np.int64)
+        out[name + "_region_names"] = np.array(mesh._region_names)
+        out[name + "_boundary_names"] = np.array(mesh._boundary_names)
+    np.savez_compressed(os.path.join(OUT, "msh_reference.npz"), **out)
+    print("msh_reference.npz")
+
+
 GENERATORS = {"gll": gen_gll, "tensor_ops": gen_tensor_ops, "poisson_action": gen_poisson_action,
               "poisson_solution": gen_poisson_solution, "axisym": gen_axisym,
-              "geometry": gen_geometry}
+              "geometry": gen_geometry, "msh": gen_msh}
 
 
 def main(names=None):
     _TABLES.update(decode_basis_hdf5())
     install_runtime_shims()
     for name in (names or list(GENERATORS)):
-        if name != "gll" and len(_TABLES) < 16:
+        if name not in ("gll", "msh") and len(_TABLES) < 16:
             # extended-order tables are needed by every generator
             import sem.basis_data as bd
             for p in range(11, MAX_ORDER_EXT + 1):
