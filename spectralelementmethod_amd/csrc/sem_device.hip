@@ -352,7 +352,7 @@ void upload_deo(sem_ctx* c, hipError_t* err) {
 // the Poisson action recomputes its factors from x_phys per node (NODAL)
 // unless the stored-factor mode was chosen or the caller supplied factors
 bool nodal_mode(const sem_ctx* c) {
-  if (c->mfma) return false;  // the MFMA kernel streams stored factors
+  if (c->mfma) return c->geom_mode == SEM_GEOM_NODAL;  // AUTO: stored factors
   return c->geom_mode == SEM_GEOM_NODAL || (c->geom_mode == SEM_GEOM_AUTO && c->n <= 9);
 }
 
@@ -388,8 +388,14 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
     const int grid = (int)(c1 - c0);
     if (op_kind == SEM_OP_POISSON && c->mfma) {
       if constexpr (N <= 16) {
-        hipLaunchKernelGGL((k_poisson_mfma<N>), dim3((grid + MFMA_EPB - 1) / MFMA_EPB),
-                           dim3(BLOCK), 0, st, c->d_mapP, c->d_GP[0], u, y, c->d_D, c0, c1, acc);
+        constexpr int per_block = MFMA_EPB * (16 / N) * (16 / N);
+        const dim3 g((grid + per_block - 1) / per_block);
+        if (nodal)
+          hipLaunchKernelGGL((k_poisson_mfma<N, true>), g, dim3(BLOCK), 0, st, c->d_mapP, nullptr,
+                             c->d_XG, u, y, c->d_D, w, c0, c1, acc);
+        else
+          hipLaunchKernelGGL((k_poisson_mfma<N, false>), g, dim3(BLOCK), 0, st, c->d_mapP,
+                             c->d_GP[0], nullptr, u, y, c->d_D, w, c0, c1, acc);
       }
     } else if (op_kind == SEM_OP_POISSON && nodal)
       hipLaunchKernelGGL((k_poisson_apply<N, true>), dim3(grid), dim3(CHAIN_BLOCK), 0, st,

@@ -849,85 +849,147 @@ constexpr int MFMA_EPB = BLOCK / WAVE;  // elements (waves) per workgroup
 
 constexpr int MFMA_TS = 17;  // LDS tile row stride (doubles)
 
-template <int N>
-__device__ __forceinline__ void mfma_transpose(double* T, int h, int c, const double (&in)[(N + 3) / 4],
-                                               double (&out)[(N + 3) / 4]) {
-  constexpr int KS = (N + 3) / 4;
+// transpose KS registers of a 16 x 16 C-layout tile through a wave-private
+// LDS tile: out[i] (lane (h, c)) = in-tile entry (c, 4i + h)
+template <int KS, int NT>
+__device__ __forceinline__ void mfma_transpose(double* T, int h, int c, const double (*in)[KS],
+                                               double (*out)[KS]) {
 #pragma unroll
-  for (int i = 0; i < KS; ++i) T[(4 * i + h) * MFMA_TS + c] = in[i];
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < KS; ++i) T[t * 16 * MFMA_TS + (4 * i + h) * MFMA_TS + c] = in[t][i];
   wave_sync();
 #pragma unroll
-  for (int i = 0; i < KS; ++i) out[i] = T[c * MFMA_TS + 4 * i + h];
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < KS; ++i) out[t][i] = T[t * 16 * MFMA_TS + c * MFMA_TS + 4 * i + h];
   wave_sync();
 }
 
 #ifndef SEM_MFMA_MIN_WAVES
 #define SEM_MFMA_MIN_WAVES 1
 #endif
-template <int N>
+// B = 16 / n elements per tile side: for n <= 8 a wavefront packs B x B
+// elements block-diagonally into one tile (D_blk = diag(D, ..., D) keeps the
+// contractions inside each element), so (B n / 16)^2 of the tile is used
+// instead of (n / 16)^2.  NODAL: the factors are re-derived per node from
+// x_phys per global node, as in the column kernel, with the
+// four Jacobian entries from four more products on coordinates taken
+// relative to the element's node (0, 0).
+template <int N, bool NODAL>
 __global__ void __launch_bounds__(BLOCK, SEM_MFMA_MIN_WAVES)
     k_poisson_mfma(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
-                   const double* __restrict__ u, double* __restrict__ y,
-                   const double* __restrict__ gD, int64_t s0, int64_t s1, int accumulate) {
+                   const double2* __restrict__ XG, const double* __restrict__ u,
+                   double* __restrict__ y, const double* __restrict__ gD, const WVec<N> w,
+                   int64_t s0, int64_t s1, int accumulate) {
   static_assert(N <= 16, "one 16x16 tile per element");
-  constexpr int KS = (N + 3) / 4;  // k-steps covering the n nodes of a line
+  constexpr int B = 16 / N;     // elements per tile side
+  constexpr int TN = B * N;     // used rows / columns
+  constexpr int EPT = B * B;    // elements per tile = per wavefront
+  constexpr int KS = (TN + 3) / 4;  // k-steps covering the used rows
   constexpr int NN = N * N;
-  __shared__ double lds[MFMA_EPB][16 * MFMA_TS];
+  __shared__ double lds[MFMA_EPB][(NODAL ? 2 : 1) * 16 * MFMA_TS];
   const int lane = threadIdx.x % WAVE;
   const int wave = threadIdx.x / WAVE;
-  const int64_t slot = s0 + (int64_t)blockIdx.x * MFMA_EPB + wave;
-  if (slot >= s1) return;  // uniform per wavefront; no workgroup barrier below
+  const int64_t slot0 = s0 + ((int64_t)blockIdx.x * MFMA_EPB + wave) * EPT;
+  if (slot0 >= s1) return;  // uniform per wavefront; no workgroup barrier below
   double* T = lds[wave];
   const int c = lane & 15;
   const int h = lane >> 4;
-  const bool cok = c < N;
-  const int cc = cok ? c : N - 1;
+  const bool cok = c < TN;
+  const int cl = cok ? c % N : N - 1;  // local column of the lane's element
+  const int ce = cok ? c / N : 0;      // element column inside the tile
   bool ok[KS];
-  int off[KS];  // (r, c) offset in an element's [n][n] arrays, clamped into range
+  int off[KS];     // local (row, column) offset in an element's [n][n] arrays
+  int64_t es[KS];  // slot of the element holding register i
+  int rl[KS];
 #pragma unroll
   for (int i = 0; i < KS; ++i) {
     const int r = 4 * i + h;
-    ok[i] = cok && r < N;
-    off[i] = (r < N ? r : N - 1) * N + cc;
+    const bool rok = r < TN;
+    rl[i] = rok ? r % N : N - 1;
+    const int64_t sl = slot0 + (rok ? r / N : 0) * B + ce;
+    ok[i] = cok && rok && sl < s1;
+    es[i] = ok[i] ? sl : slot0;
+    off[i] = rl[i] * N + cl;
   }
-  const uint32_t* mp = mapP + slot * NN;
-  const double* gp = GP + slot * (3 * NN);
-  double x1[KS], x2[KS], g0[KS], g1[KS], g2[KS], Da[KS], Dt[KS];
+  double Da[KS], Dt[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = 4 * s + h;
+    const bool same = cok && k < TN && k / N == ce;  // block-diagonal D
+    const double a = gD[cl * N + k % N], t = gD[(k % N) * N + cl];
+    Da[s] = same ? a : 0.0;
+    Dt[s] = same ? t : 0.0;
+  }
+  uint32_t e[KS];
+#pragma unroll
+  for (int i = 0; i < KS; ++i) e[i] = mapP[es[i] * NN + off[i]];
+  const dbl4 z = {0.0, 0.0, 0.0, 0.0};
+  double g0[KS], g1[KS], g2[KS];
+  if constexpr (NODAL) {
+    const double wc = pick<N>(w, cl);
+    double X[2][KS], XT[2][KS];
+#pragma unroll
+    for (int i = 0; i < KS; ++i) {
+      const double2 xg = XG[e[i] & GID_MASK];
+      const double2 x0 = XG[mapP[es[i] * NN] & GID_MASK];  // element's node (0, 0)
+      X[0][i] = ok[i] ? xg.x - x0.x : 0.0;
+      X[1][i] = ok[i] ? xg.y - x0.y : 0.0;
+    }
+    mfma_transpose<KS, 2>(T, h, c, X, XT);
+    dbl4 jr0 = z, jr1 = z, js0 = z, js1 = z;  // dx/dr, dy/dr, dx/ds, dy/ds
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      jr0 = mfma_f64(Da[s], X[0][s], jr0);
+      jr1 = mfma_f64(Da[s], X[1][s], jr1);
+      js0 = mfma_f64(XT[0][s], Da[s], js0);
+      js1 = mfma_f64(XT[1][s], Da[s], js1);
+    }
+#pragma unroll
+    for (int i = 0; i < KS; ++i) {
+      const double det = jr0[i] * js1[i] - js0[i] * jr1[i];
+      const double sc = ok[i] ? (pick<N>(w, rl[i]) * wc) * fast_rcp(det) : 0.0;
+      g0[i] = sc * fma(js1[i], js1[i], js0[i] * js0[i]);
+      g1[i] = -sc * fma(js1[i], jr1[i], js0[i] * jr0[i]);
+      g2[i] = sc * fma(jr1[i], jr1[i], jr0[i] * jr0[i]);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < KS; ++i) {
+      const double* gp = GP + es[i] * (3 * NN) + off[i];
+      g0[i] = gp[0 * NN];
+      g1[i] = gp[1 * NN];
+      g2[i] = gp[2 * NN];
+    }
+  }
+  double U[1][KS], UT[1][KS];
   uint32_t raw[KS];
 #pragma unroll
   for (int i = 0; i < KS; ++i) {
-    const uint32_t e = mp[off[i]];
-    const double v = u[e & GID_MASK];
-    x1[i] = ok[i] ? v : 0.0;
-    raw[i] = ok[i] ? e : (W_SKIP << CODE_SHIFT);
-    g0[i] = gp[0 * NN + off[i]];
-    g1[i] = gp[1 * NN + off[i]];
-    g2[i] = gp[2 * NN + off[i]];
-    const int k = 4 * i + h < N ? 4 * i + h : N - 1;
-    const double a = gD[cc * N + k], t = gD[k * N + cc];
-    Da[i] = ok[i] ? a : 0.0;
-    Dt[i] = ok[i] ? t : 0.0;
+    const double v = u[e[i] & GID_MASK];
+    U[0][i] = ok[i] ? v : 0.0;
+    raw[i] = ok[i] ? e[i] : (W_SKIP << CODE_SHIFT);
   }
-  const dbl4 z = {0.0, 0.0, 0.0, 0.0};
-  mfma_transpose<N>(T, h, c, x1, x2);
+  mfma_transpose<KS, 1>(T, h, c, U, UT);
   dbl4 d0 = z, d1 = z;
 #pragma unroll
-  for (int s = 0; s < KS; ++s) d0 = mfma_f64(Da[s], x1[s], d0);
+  for (int s = 0; s < KS; ++s) d0 = mfma_f64(Da[s], U[0][s], d0);
 #pragma unroll
-  for (int s = 0; s < KS; ++s) d1 = mfma_f64(x2[s], Da[s], d1);
-  double w0[KS], w1[KS], w1t[KS];
+  for (int s = 0; s < KS; ++s) d1 = mfma_f64(UT[0][s], Da[s], d1);
+  double w0[KS], W1[1][KS], W1T[1][KS];
 #pragma unroll
   for (int i = 0; i < KS; ++i) {
     w0[i] = ok[i] ? fma(g0[i], d0[i], g1[i] * d1[i]) : 0.0;
-    w1[i] = ok[i] ? fma(g1[i], d0[i], g2[i] * d1[i]) : 0.0;
+    W1[0][i] = ok[i] ? fma(g1[i], d0[i], g2[i] * d1[i]) : 0.0;
   }
-  mfma_transpose<N>(T, h, c, w1, w1t);
+  mfma_transpose<KS, 1>(T, h, c, W1, W1T);
   dbl4 acc = z;
 #pragma unroll
   for (int s = 0; s < KS; ++s) acc = mfma_f64(Dt[s], w0[s], acc);
 #pragma unroll
-  for (int s = 0; s < KS; ++s) acc = mfma_f64(w1t[s], Dt[s], acc);
-  // row 4i + h < N implies i < KS; padding entries carry SKIP
+  for (int s = 0; s < KS; ++s) acc = mfma_f64(W1T[0][s], Dt[s], acc);
+  // row 4i + h < TN implies i < KS; padding entries carry SKIP
 #pragma unroll
   for (int i = 0; i < KS; ++i) emit1(y, raw[i], acc[i], accumulate);
 }

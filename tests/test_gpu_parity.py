@@ -311,12 +311,14 @@ def test_shared_output_split(sem, gll, geometry):
 # ---------------------------------------------------------------------------
 # fp64 matrix-core kernel (k_poisson_mfma, sem_set_kernel SEM_KERNEL_MFMA)
 # ---------------------------------------------------------------------------
+@pytest.mark.parametrize("geometry", GEOMETRY)
 @pytest.mark.parametrize("name", [c for c in ACTION_CASES if not c.startswith("p16")])
-def test_poisson_action_golden_mfma(sem, poisson_action, gll, name):
+def test_poisson_action_golden_mfma(sem, poisson_action, gll, name, geometry):
     import sem_oracle
     fx = poisson_action
     p = int(fx[name + "_p"])
-    op = sem.SEMOperator(p, fx[name + "_e2n"], fx[name + "_nodes"], kernel="mfma")
+    op = sem.SEMOperator(p, fx[name + "_e2n"], fx[name + "_nodes"], kernel="mfma",
+                         geometry=geometry)
     assert op.plan_info()["kernel"] == "mfma"
     y = op.apply(torch.from_numpy(fx[name + "_u"]).cuda()).cpu().numpy()
     y_ext = None
@@ -326,14 +328,18 @@ def test_poisson_action_golden_mfma(sem, poisson_action, gll, name):
     assert_parity(y, fx[name + "_y"], y_ext, TOL_ACTION)
 
 
+@pytest.mark.parametrize("geometry", GEOMETRY)
 @pytest.mark.parametrize("p", list(range(1, 16)))
-def test_poisson_all_orders_mfma(sem, gll, p):
+def test_poisson_all_orders_mfma(sem, gll, p, geometry):
+    """Every tile packing: 16 // (p + 1) elements per tile side for p <= 7
+    (block-diagonal D), one element per tile above; the 7 x 5 mesh leaves
+    partly filled tiles at the end of every colour."""
     import sem_oracle
     from spectralelementmethod_amd import meshgen
-    nodes, e2n = meshgen.structured_square(5, 4, p, warp=0.05)
+    nodes, e2n = meshgen.structured_square(7, 5, p, warp=0.05)
     prob = sem_oracle.PoissonProblem(nodes, e2n, gll["half_%d" % p])
     u = np.random.default_rng(p).standard_normal(prob.ndof)
-    op = sem.SEMOperator(p, e2n, nodes, kernel="mfma")
+    op = sem.SEMOperator(p, e2n, nodes, kernel="mfma", geometry=geometry)
     y = op.apply(torch.from_numpy(u).cuda()).cpu().numpy()
     y_ext = sem_oracle.poisson_apply_extended(nodes, e2n, gll["half_%d" % p], u)
     assert_parity(y, prob.apply(u), y_ext, TOL_ACTION)
@@ -388,17 +394,18 @@ def test_mfma_accumulate_unreferenced_nonconforming(sem, poisson_action, gll):
     assert rel_l2(y, sem_oracle.PoissonProblem(nodes, e2d, gll["half_4"]).apply(u)) < TOL_ACTION
 
 
-def test_mfma_shared_output_split(sem):
+@pytest.mark.parametrize("p,geometry", [(10, "stored"), (4, "nodal"), (3, "stored")])
+def test_mfma_shared_output_split(sem, p, geometry):
     from spectralelementmethod_amd import meshgen
     from spectralelementmethod_amd.distributed import split_interface_elements
-    p, nex, ney = 10, 7, 4
+    nex, ney = 7, 4
     nodes, e2n = meshgen.structured_square(nex, ney, p, warp=0.05)
     Ny = ney * p + 1
     nn = nodes.shape[1]
     ie, be, st_i, st_b = split_interface_elements(e2n, {1: np.arange(nn - Ny, nn)})
     full = sem.SEMOperator(p, e2n, nodes, kernel="column", geometry="stored")
-    op_i = sem.SEMOperator(p, e2n[ie], nodes, node_state=st_i, kernel="mfma")
-    op_b = sem.SEMOperator(p, e2n[be], nodes, node_state=st_b, kernel="mfma")
+    op_i = sem.SEMOperator(p, e2n[ie], nodes, node_state=st_i, kernel="mfma", geometry=geometry)
+    op_b = sem.SEMOperator(p, e2n[be], nodes, node_state=st_b, kernel="mfma", geometry=geometry)
     u = torch.randn(full.ndof, dtype=torch.float64, device="cuda",
                     generator=torch.Generator(device="cuda").manual_seed(9))
     ref = full.apply(u)
