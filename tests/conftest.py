@@ -50,3 +50,8 @@ def rel_l2(a, b):
     b = np.asarray(b, dtype=np.float64)
     nb = np.linalg.norm(b)
     return np.linalg.norm(a - b) / (nb if nb else 1.0)
+
+
+@pytest.fixture(scope="session")
+def axisym_ns():
+    return load_golden("axisym_ns.npz")

@@ -408,6 +408,87 @@ def gen_axisym():
     print("axisym_action.npz")
 
 
+def axisym_Ae(fe, n_rey):
+    """Advection operator of examples/squirmer-axisymmetric.py:229-250 (built
+    with the reference's own KroneckerArray, sem/sp_array.py:11-113)."""
+    from sem.sp_array import KroneckerArray
+    JxW = fe.detJxW
+    invJ = fe.invJ
+    x = fe.x_phys
+    dmats = fe.basis.get_D1_matrices()
+    gradh_xi0 = np.einsum("imn,mp->imnp", invJ[0, :], dmats[0])
+    gradh_xi1 = np.einsum("imn,nq->imnq", invJ[1, :], dmats[1])
+    Ae = KroneckerArray(shape=fe.basis.coeff_shape * 3)
+    Ae.add_diag(n_rey * (np.einsum("mn,mnr,mnu->mnru", JxW, gradh_xi0[0], gradh_xi1[1]) -
+                         np.einsum("mn,mnr,mnu->mnru", JxW, gradh_xi0[1], gradh_xi1[0])),
+                [0, 1, 2, 1, 0, 3])
+    Ae.add_diag(n_rey * (np.einsum("mn,mns,mnt->mnst", JxW, gradh_xi1[0], gradh_xi0[1]) -
+                         np.einsum("mn,mns,mnt->mnst", JxW, gradh_xi1[1], gradh_xi0[0])),
+                [0, 1, 0, 2, 3, 1])
+    Ae.add_diag(n_rey * np.einsum("mn,mnr->mnr", JxW / x[0], gradh_xi0[1]), [0, 1, 2, 1, 0, 1])
+    Ae.add_diag(n_rey * np.einsum("mn,mns->mns", JxW / x[0], gradh_xi1[1]), [0, 1, 0, 2, 0, 1])
+    return Ae
+
+
+def gen_axisym_ns():
+    """Navier-Stokes (Re > 0) squirmer residual and its Newton Jacobian:
+    compute_local_system (examples/squirmer-axisymmetric.py:259-297) with
+    the operators of pre_assembly (:193-254), Ae as the reference's
+    KroneckerArray.  res[0::2] = Ae.w.psi + Lve.w, res[1::2] = E2e.psi -
+    Me.w; the dense local Jacobian jac_l is assembled and applied to a
+    random direction (the JVP golden)."""
+    from sem.discrete import DOFManager
+    from sem.sp_array import KroneckerArray
+    np.float = float  # sem/sp_array.py:39 (NumPy >= 1.24 removed np.float)
+    out = {}
+    rng = np.random.default_rng(7)
+    for name, p, nth, nr, n_rey in [("p6_4x8", 6, 4, 8, 3.7), ("p4_3x2", 4, 3, 2, 12.5)]:
+        nodes, e2n = annulus(nth, nr, p)
+        mesh = ref_mesh(nodes, e2n)
+        _, tb = ref_basis(p)
+        dm = DOFManager(mesh, 2, tb, rcm_order=False)
+        nn = mesh.n_nodes
+        sfn = rng.standard_normal(nn)
+        vort = rng.standard_normal(nn)
+        delta = rng.standard_normal(2 * nn)
+        res = np.zeros(2 * nn)
+        jvp = np.zeros(2 * nn)
+        for fe in dm.finite_elements(x_phys=True, Jacobian=True):
+            E2e, Lve, Me_d = axisym_ops(fe)
+            Ae = axisym_Ae(fe, n_rey)
+            Me = KroneckerArray(shape=fe.basis.coeff_shape * 2)
+            Me.add_diag(Me_d, [0, 1, 0, 1])
+            loc = fe.node_ind
+            s_l, w_l = sfn[loc], vort[loc]
+            n_nodes = loc.size
+            Ae_w = Ae.dot_dense(w_l, [4, 5])
+            r0 = Ae_w.dot_dense(s_l, [2, 3]).to_array() + np.einsum("pqrs,rs", Lve, w_l)
+            r1 = np.einsum("pqrs,rs", E2e, s_l) - Me.dot_dense(w_l, [2, 3]).to_array()
+            jac = np.zeros((2 * n_nodes, 2 * n_nodes))
+            jac[0::2, 0::2] = Ae_w.to_array().reshape(n_nodes, n_nodes)
+            jac[0::2, 1::2] = (Ae.dot_dense(s_l, [2, 3]).to_array() + Lve).reshape(n_nodes, n_nodes)
+            jac[1::2, 0::2] = E2e.reshape(n_nodes, n_nodes)
+            jac[1::2, 1::2] = -Me.to_array().reshape(n_nodes, n_nodes)
+            dofs = (2 * loc.ravel()[:, None] + np.arange(2)[None, :]).ravel()
+            np.add.at(res, 2 * loc.ravel(), r0.ravel())
+            np.add.at(res, 2 * loc.ravel() + 1, r1.ravel())
+            np.add.at(jvp, dofs, jac @ delta[dofs])
+        sol = np.empty(2 * nn)
+        sol[0::2], sol[1::2] = sfn, vort
+        out[name + "_nodes"] = mesh.nodes.copy()
+        out[name + "_e2n"] = mesh_map(mesh)
+        out[name + "_p"] = np.array(p)
+        out[name + "_re"] = np.array(n_rey)
+        out[name + "_soln"] = sol
+        out[name + "_res"] = res
+        out[name + "_delta"] = delta
+        out[name + "_jvp"] = jvp
+        print("  axisym NS %s Re=%g |res|=%.6e |jvp|=%.6e" % (name, n_rey, np.linalg.norm(res),
+                                                           np.linalg.norm(jvp)))
+    np.savez_compressed(os.path.join(OUT, "axisym_ns.npz"), **out)
+    print("axisym_ns.npz")
+
+
 def gen_geometry():
     """Node orderings of sem/geometry.py (NCube hierarchical order :197-212,
     exterior/interior sets) and the DOFManagerSC condensation permutation
@@ -476,7 +557,7 @@ def gen_msh():
 
 GENERATORS = {"gll": gen_gll, "tensor_ops": gen_tensor_ops, "poisson_action": gen_poisson_action,
               "poisson_solution": gen_poisson_solution, "axisym": gen_axisym,
-              "geometry": gen_geometry, "msh": gen_msh}
+              "geometry": gen_geometry, "msh": gen_msh, "axisym_ns": gen_axisym_ns}
 
 
 def main(names=None):
