@@ -31,7 +31,7 @@ sys.path.insert(0, ROOT)
 
 from spectralelementmethod_amd import _lib  # noqa: E402
 from spectralelementmethod_amd.distributed import StripPartition, OverlappedOperator  # noqa: E402
-from spectralelementmethod_amd.operators import POISSON, AXISYM_STOKES  # noqa: E402
+from spectralelementmethod_amd.operators import POISSON, AXISYM_STOKES, AXISYM_NS  # noqa: E402
 
 METRIC = "global stiffness-action DOF-updates/s (and % HBM roofline), Poisson p=8"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
@@ -50,12 +50,14 @@ def alg_bytes(kind, ndof_nodes, n_elem, p, geometry="stored"):
     (u read, y written, 3 fp64 factors + one uint32 map entry per local
     node); with nodal geometry the factors are replaced by x_phys per global
     node: B = 32*ndof + 4*E*(p+1)^2; axisymmetric B = 32*n_nodes +
-    60*E*(p+1)^2."""
+    60*E*(p+1)^2 (Navier-Stokes residual: 9 factors, 76*E*(p+1)^2)."""
     n2 = (p + 1) ** 2
     if kind == POISSON and geometry == "nodal":
         return 32 * ndof_nodes + 4 * n_elem * n2
     if kind == POISSON:
         return 16 * ndof_nodes + 28 * n_elem * n2
+    if kind == AXISYM_NS:
+        return 32 * ndof_nodes + 76 * n_elem * n2
     return 32 * ndof_nodes + 60 * n_elem * n2
 
 
@@ -67,7 +69,7 @@ def alg_flops(kind, n_elem, p, geometry="stored"):
     if kind == POISSON:
         extra = 8 * n ** 3 + 15 * n ** 2 if geometry == "nodal" else 0
         return n_elem * (8 * n ** 3 + 7 * n ** 2 + extra)
-    return n_elem * (16 * n ** 3 + 22 * n ** 2)
+    return n_elem * (16 * n ** 3 + (30 if kind == AXISYM_NS else 22) * n ** 2)
 
 
 def cpu_baseline(p, warp, budget_s=20.0):
@@ -124,7 +126,8 @@ def main():
     ap.add_argument("--nex", type=int, default=1024, help="element columns per rank")
     ap.add_argument("--ney", type=int, default=1024)
     ap.add_argument("--warp", type=float, default=0.05)
-    ap.add_argument("--op", choices=["poisson", "axisym_stokes"], default="poisson")
+    ap.add_argument("--op", choices=["poisson", "axisym_stokes", "axisym_ns"], default="poisson")
+    ap.add_argument("--re", type=float, default=10.0, help="Reynolds number for --op axisym_ns")
     ap.add_argument("--geometry", choices=["auto", "nodal", "stored"], default="auto",
                     help="Poisson geometric factors: re-derived from x_phys per node, or "
                          "streamed; auto = nodal for p <= 8 (the library's default)")
@@ -148,7 +151,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
         dist.barrier()
 
-    kind = POISSON if args.op == "poisson" else AXISYM_STOKES
+    kind = {"poisson": POISSON, "axisym_stokes": AXISYM_STOKES, "axisym_ns": AXISYM_NS}[args.op]
     dpn = 1 if kind == POISSON else 2
     p = args.p
     nex_global = args.nex * world
@@ -168,6 +171,9 @@ def main():
     # interior elements run (one plain operator when there is no neighbour)
     op = OverlappedOperator(p, nodes, e2n, part.neighbors if world > 1 else {}, dpn, dev,
                             geometry=geometry, kind=kind, kernel=args.kernel)
+    if kind == AXISYM_NS:
+        for o in op.ops:
+            o.set_reynolds(args.re)
     plan = op.plan_info()
     if plan["kernel"] == "mfma":  # the MFMA kernel streams stored factors
         geometry = "stored"
@@ -229,8 +235,9 @@ def main():
         with open(traffic_src) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
     result = {
-        "metric": METRIC if kind == POISSON else METRIC.replace("Poisson p=8",
-                                                                 "axisymmetric Stokes p=%d" % p),
+        "metric": METRIC if kind == POISSON else METRIC.replace(
+            "Poisson p=8", ("axisymmetric Stokes p=%d" if kind == AXISYM_STOKES else
+                            "axisymmetric Navier-Stokes residual p=%d") % p),
         "value": value,
         "unit": "DOF/s",
         "n_gpus": world,

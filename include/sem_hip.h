@@ -42,8 +42,10 @@ extern "C" {
 /* ---- operator kinds ---- */
 #define SEM_OP_POISSON 0        /* scalar Laplacian Lse, examples/poisson.py:168-193 */
 #define SEM_OP_AXISYM_STOKES 1  /* [Lve.w ; E2e.psi - Me.w], squirmer-axisymmetric.py:193-254,278-295 (Re=0) */
+#define SEM_OP_AXISYM_NS 2      /* Re > 0 residual [Ae.w.psi + Lve.w ; E2e.psi - Me.w], squirmer:229-297 */
+#define SEM_OP_AXISYM_NS_JVP 3  /* its Newton Jacobian (jac_l, squirmer:272-291) times a direction */
 
-/* number of geometric factors per local node for an operator kind (3 or 7) */
+/* number of geometric factors per local node for an operator kind (3, 7 or 9) */
 int sem_op_ncomp(int op_kind);
 
 const char* sem_last_error(void);
@@ -192,8 +194,21 @@ int sem_set_geom(sem_ctx* ctx, const double* d_G, int op_kind, void* stream);
  * mode only) states that the caller already ran sem_zero_shared on y. */
 #define SEM_APPLY_ACCUMULATE 1
 #define SEM_APPLY_SKIP_ZERO 2
+#define SEM_APPLY_LINEARIZE 4  /* SEM_OP_AXISYM_NS: also record the Newton
+                                * linearisation at u for SEM_OP_AXISYM_NS_JVP */
 int sem_apply(sem_ctx* ctx, int op_kind, const double* d_u, double* d_y, int flags,
               void* stream);
+
+/* Reynolds number N_Re of the SEM_OP_AXISYM_NS residual and its Jacobian
+ * (the n_rey scaling of the advection operator Ae, squirmer:230-250).
+ * SEM_OP_AXISYM_NS with u = (psi, omega) interleaved gives
+ *   y[2k]   = Ae.omega.psi + Lve.omega,   y[2k+1] = E2e.psi - Me.omega
+ * (compute_local_system res_l, squirmer:259-297; Ae at quadrature node
+ * (m, n) = Re [w_m w_n (d0 psi d1 w - d1 psi d0 w) + (W/rho) w dpsi/dz]).
+ * With SEM_APPLY_LINEARIZE it also stores 5 coefficients per element node so
+ * that SEM_OP_AXISYM_NS_JVP applies the Jacobian at that state to any
+ * direction u -- the matrix-free form of jac_l (squirmer:272-291). */
+int sem_set_reynolds(sem_ctx* ctx, double re);
 
 /* Zero the entries of y that the overwrite-mode kernel does not store
  * (element-boundary and unreferenced nodes; all dpn components). */

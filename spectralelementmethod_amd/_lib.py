@@ -22,9 +22,12 @@ SEM_E_STATE = -5
 
 OP_POISSON = 0
 OP_AXISYM_STOKES = 1
+OP_AXISYM_NS = 2
+OP_AXISYM_NS_JVP = 3
 
 APPLY_ACCUMULATE = 1
 APPLY_SKIP_ZERO = 2
+APPLY_LINEARIZE = 4
 GEOM_STORED = 0
 GEOM_NODAL = 1
 GEOM_AUTO = 2
@@ -58,6 +61,7 @@ SIGNATURES = {
     "sem_set_geom": (C.c_int, [_vp, _vp, C.c_int, _vp]),
     "sem_set_geom_mode": (C.c_int, [_vp, C.c_int]),
     "sem_set_kernel": (C.c_int, [_vp, C.c_int]),
+    "sem_set_reynolds": (C.c_int, [_vp, C.c_double]),
     "sem_set_map_shared": (C.c_int, [_vp, _vp, _vp, _vp]),
     "sem_apply": (C.c_int, [_vp, C.c_int, _vp, _vp, C.c_int, _vp]),
     "sem_zero_shared": (C.c_int, [_vp, _vp, _vp]),

@@ -128,6 +128,9 @@ int sem_op_ncomp(int op_kind) {
       return 3;
     case SEM_OP_AXISYM_STOKES:
       return 7;
+    case SEM_OP_AXISYM_NS:
+    case SEM_OP_AXISYM_NS_JVP:
+      return 9;
     default:
       return sem::fail(SEM_E_INVALID, "unknown op_kind " + std::to_string(op_kind));
   }

@@ -281,7 +281,10 @@ struct sem_ctx {
   std::vector<int64_t> colour_start;  // chain ranges, one launch each
   int64_t n_atomic_groups = 0;        // groups in atomic-fallback chains
   bool conforming = true;
-  double* d_GP[2] = {nullptr, nullptr};
+  double* d_GP[3] = {nullptr, nullptr, nullptr};  // Poisson, axisym. Stokes, Navier-Stokes
+  double reynolds = 0.0;
+  double* d_lin = nullptr;  // Navier-Stokes linearisation, 5 per element node
+  bool lin_valid = false;
   // NODAL geometry (Poisson): x_phys per global node + the node's first element
   int geom_mode = SEM_GEOM_AUTO;
   // kernel family of the Poisson action (sem_set_kernel), fixed by
@@ -376,7 +379,8 @@ bool use_nodal(const sem_ctx* c, int op_kind) {
 }
 
 template <int N>
-int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc, hipStream_t st) {
+int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc, bool lin,
+                   hipStream_t st) {
   const DEO<N> D = make_deo<N>(c);
   WVec<N> w;
   std::memcpy(w.v, c->hw, sizeof(w.v));
@@ -403,9 +407,20 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
     else if (op_kind == SEM_OP_POISSON)
       hipLaunchKernelGGL((k_poisson_apply<N, false>), dim3(grid), dim3(CHAIN_BLOCK), 0, st,
                          c->d_mapP, c->d_GP[0], nullptr, u, y, c0, c1, c->rounds, acc, D, w);
-    else
-      hipLaunchKernelGGL((k_axisym_apply<N>), dim3(grid), dim3(CHAIN_BLOCK), 0, st, c->d_mapP,
-                         c->d_GP[1], u, y, c0, c1, c->rounds, acc, D);
+    else if (op_kind == SEM_OP_AXISYM_STOKES)
+      hipLaunchKernelGGL((k_axisym_apply<N, 0>), dim3(grid), dim3(CHAIN_BLOCK), 0, st, c->d_mapP,
+                         c->d_GP[1], u, y, c0, c1, c->rounds, acc, D, w, AxiNS());
+    else {
+      AxiNS ns;
+      ns.re = c->reynolds;
+      ns.lin = (op_kind == SEM_OP_AXISYM_NS_JVP || lin) ? c->d_lin : nullptr;
+      if (op_kind == SEM_OP_AXISYM_NS)
+        hipLaunchKernelGGL((k_axisym_apply<N, 1>), dim3(grid), dim3(CHAIN_BLOCK), 0, st,
+                           c->d_mapP, c->d_GP[2], u, y, c0, c1, c->rounds, acc, D, w, ns);
+      else
+        hipLaunchKernelGGL((k_axisym_apply<N, 2>), dim3(grid), dim3(CHAIN_BLOCK), 0, st,
+                           c->d_mapP, c->d_GP[2], u, y, c0, c1, c->rounds, acc, D, w, ns);
+    }
   }
   return SEM_OK;
 }
@@ -449,7 +464,8 @@ int check_op(sem_ctx* c, int op_kind) {
     if (c->dpn != 1) return fail(SEM_E_INVALID, "Poisson operator needs dofs_per_node == 1");
     return SEM_OK;
   }
-  if (op_kind == SEM_OP_AXISYM_STOKES) {
+  if (op_kind == SEM_OP_AXISYM_STOKES || op_kind == SEM_OP_AXISYM_NS ||
+      op_kind == SEM_OP_AXISYM_NS_JVP) {
     if (c->dpn != 2)
       return fail(SEM_E_INVALID, "axisymmetric Stokes block needs dofs_per_node == 2");
     return SEM_OK;
@@ -457,8 +473,13 @@ int check_op(sem_ctx* c, int op_kind) {
   return fail(SEM_E_INVALID, "unknown op_kind " + std::to_string(op_kind));
 }
 
+// factor slot of an operator kind: the two Navier-Stokes kinds share one
+int gp_slot(int op_kind) {
+  return op_kind == SEM_OP_POISSON ? 0 : (op_kind == SEM_OP_AXISYM_STOKES ? 1 : 2);
+}
+
 int ensure_gp(sem_ctx* c, int op_kind) {
-  const int slot = op_kind == SEM_OP_POISSON ? 0 : 1;
+  const int slot = gp_slot(op_kind);
   if (!c->d_GP[slot]) {
     const int ncomp = sem_op_ncomp(op_kind);
     const size_t bytes = (size_t)c->n_slots * ncomp * c->n * c->lw * sizeof(double);
@@ -837,8 +858,8 @@ void sem_ctx_destroy(sem_ctx* c) {
   (void)hipFree(c->d_mapP);
   (void)hipFree(c->d_gpos);
   (void)hipFree(c->d_zero);
-  (void)hipFree(c->d_GP[0]);
-  (void)hipFree(c->d_GP[1]);
+  for (double* g : c->d_GP) (void)hipFree(g);
+  (void)hipFree(c->d_lin);
   (void)hipFree(c->d_XG);
   (void)hipFree(c->d_owner);
   (void)hipFree(c->d_cg);
@@ -926,9 +947,13 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
   HIP_TRY(hipMemcpy(c->d_owner, P.owner.data(), P.owner.size() * sizeof(uint32_t),
                     hipMemcpyHostToDevice));
   // geometry was derived for the previous map
-  (void)hipFree(c->d_GP[0]);
-  (void)hipFree(c->d_GP[1]);
-  c->d_GP[0] = c->d_GP[1] = nullptr;
+  for (double*& g : c->d_GP) {
+    (void)hipFree(g);
+    g = nullptr;
+  }
+  (void)hipFree(c->d_lin);
+  c->d_lin = nullptr;
+  c->lin_valid = false;
   c->xg_valid = false;
   return SEM_OK;
 }
@@ -962,6 +987,14 @@ int sem_set_geom_mode(sem_ctx* c, int mode) {
   return SEM_OK;
 }
 
+int sem_set_reynolds(sem_ctx* c, double re) {
+  if (!c) return fail(SEM_E_INVALID, "null ctx");
+  if (!std::isfinite(re)) return fail(SEM_E_INVALID, "Reynolds number must be finite");
+  c->reynolds = re;
+  c->lin_valid = false;  // a recorded linearisation belongs to the old Re
+  return SEM_OK;
+}
+
 int sem_set_kernel(sem_ctx* c, int kernel) {
   if (!c) return fail(SEM_E_INVALID, "null ctx");
   if (kernel != SEM_KERNEL_COLUMN && kernel != SEM_KERNEL_MFMA && kernel != SEM_KERNEL_AUTO)
@@ -988,7 +1021,7 @@ int sem_geom_from_nodes(sem_ctx* c, const double* d_nodes, const double* h_Vinv,
     c->d_GP[0] = nullptr;
   } else {
     if ((rc = ensure_gp(c, op_kind))) return rc;
-    GP = c->d_GP[op_kind == SEM_OP_POISSON ? 0 : 1];
+    GP = c->d_GP[gp_slot(op_kind)];
   }
   hipStream_t st = S(stream);
   HIP_TRY(hipMemsetAsync(c->d_bad, 0, sizeof(unsigned long long), st));
@@ -1002,6 +1035,7 @@ int sem_geom_from_nodes(sem_ctx* c, const double* d_nodes, const double* h_Vinv,
   if (n_bad_nodes) *n_bad_nodes = (int64_t)bad;
   if (bad) return fail(SEM_E_DETJ, "detJ <= 0 at " + std::to_string(bad) + " quadrature nodes");
   if (op_kind == SEM_OP_POISSON) c->xg_valid = nodal;
+  if (gp_slot(op_kind) == 2) c->lin_valid = false;  // linearisation used the old factors
   return SEM_OK;
 }
 
@@ -1031,7 +1065,7 @@ int sem_set_geom(sem_ctx* c, const double* d_G, int op_kind, void* stream) {
   if (op_kind == SEM_OP_POISSON) c->xg_valid = false;  // caller's factors take over
   hipLaunchKernelGGL(k_pack_geom, dim3(grid_for(c->n_elem * ncomp * c->n * c->n)), dim3(BLOCK), 0,
                      S(stream), d_G, c->n_elem, c->n, ncomp, c->epw, c->d_gpos,
-                     c->d_GP[op_kind == SEM_OP_POISSON ? 0 : 1]);
+                     c->d_GP[gp_slot(op_kind)]);
   HIP_TRY(hipGetLastError());
   return SEM_OK;
 }
@@ -1049,21 +1083,29 @@ int sem_zero_shared(sem_ctx* c, double* y, void* stream) {
 
 int sem_apply(sem_ctx* c, int op_kind, const double* u, double* y, int flags, void* stream) {
   if (!c || !u || !y) return fail(SEM_E_INVALID, "null argument");
-  if (flags & ~(SEM_APPLY_ACCUMULATE | SEM_APPLY_SKIP_ZERO))
+  if (flags & ~(SEM_APPLY_ACCUMULATE | SEM_APPLY_SKIP_ZERO | SEM_APPLY_LINEARIZE))
     return fail(SEM_E_INVALID, "unknown sem_apply flags");
   int rc;
   if ((rc = check_op(c, op_kind))) return rc;
   if (!c->have_basis || !c->d_mapP) return fail(SEM_E_STATE, "basis and map must be set");
-  if (!use_nodal(c, op_kind) && !c->d_GP[op_kind == SEM_OP_POISSON ? 0 : 1])
+  if (!use_nodal(c, op_kind) && !c->d_GP[gp_slot(op_kind)])
     return fail(SEM_E_STATE, "geometry for this operator has not been computed");
+  const bool lin = flags & SEM_APPLY_LINEARIZE;
+  if (lin && op_kind != SEM_OP_AXISYM_NS)
+    return fail(SEM_E_INVALID, "SEM_APPLY_LINEARIZE applies to SEM_OP_AXISYM_NS only");
+  if (op_kind == SEM_OP_AXISYM_NS_JVP && !c->lin_valid)
+    return fail(SEM_E_STATE, "no linearisation: apply SEM_OP_AXISYM_NS with SEM_APPLY_LINEARIZE first");
+  if (lin && !c->d_lin)
+    HIP_TRY(hipMalloc(&c->d_lin, (size_t)c->n_slots * 5 * c->n * c->lw * sizeof(double)));
   DeviceGuard g(c->device);
   hipStream_t st = S(stream);
   const int accumulate = flags & SEM_APPLY_ACCUMULATE;
   if (!accumulate && !(flags & SEM_APPLY_SKIP_ZERO) && c->n_zero)
     hipLaunchKernelGGL(k_zero_list, dim3(grid_for(c->n_zero, BLOCK, 4096)), dim3(BLOCK), 0, st, y,
                        c->d_zero, c->n_zero, c->dpn);
-  SEM_DISPATCH_N(c->n, launch_apply_n, c, op_kind, u, y, accumulate, st);
+  SEM_DISPATCH_N(c->n, launch_apply_n, c, op_kind, u, y, accumulate, lin, st);
   HIP_TRY(hipGetLastError());
+  if (lin) c->lin_valid = true;
   return SEM_OK;
 }
 

@@ -669,19 +669,33 @@ __global__ void __launch_bounds__(CHAIN_BLOCK, SEM_POISSON_MIN_WAVES)
 //   y[2k+1] = E2e.psi - Me.omega = stiff_rho(psi) + 2W(iJ00 d0 + iJ10 d1)psi - rho^2 W omega
 // (examples/squirmer-axisymmetric.py:193-227, 253-254, 278-295)
 // factors: 0 G00rho 1 G01rho 2 G11rho 3 b0=2W iJ00 4 b1=2W iJ10 5 c=W/rho 6 m=rho^2 W
+// Navier-Stokes (MODE 1 residual, MODE 2 Jacobian-vector product) adds
+// 7 (W/rho) iJ01, 8 (W/rho) iJ11 and the advection term Ae (squirmer:229-250)
+// at test node (m, j) of the omega row:
+//   Re [ w_m w_j (d0 psi d1 w - d1 psi d0 w) + w (f7 d0 psi + f8 d1 psi) ]
+// MODE 1 can record its linearisation a0..a4 per element node (LIN):
+//   J.delta|omega row += a0 d0 dpsi + a1 d1 dpsi + a2 d0 dw + a3 d1 dw + a4 dw
 // ---------------------------------------------------------------------------
-template <int N>
+struct AxiNS {
+  double re = 0.0;
+  double* lin = nullptr;  // MODE 1: write, MODE 2: read; [slot][5][r][lane]
+};
+
+template <int N, int MODE>
 __device__ __forceinline__ void axisym_group(const uint32_t* __restrict__ mapP,
                                              const double* __restrict__ GP,
                                              const double* __restrict__ u, int64_t g, int lane,
                                              int j, bool in_wave, double* LP, double* LO,
-                                             const DEO<N>& D, uint32_t (&raw)[N],
+                                             const DEO<N>& D, const WVec<N>& w, double wj,
+                                             const AxiNS& ns, uint32_t (&raw)[N],
                                              double (&vo)[N], double (&vp)[N]) {
   using T = Tile<N>;
   constexpr int LW = T::LW;
   constexpr int RS = T::RS;
+  constexpr int NF = MODE ? 9 : 7;
   const uint32_t* mp = mapP + g * (int64_t)(N * LW) + lane;
-  const double* gp = GP + g * (int64_t)(7 * N * LW) + lane;
+  const double* gp = GP + g * (int64_t)(NF * N * LW) + lane;
+  double* lin = MODE ? ns.lin + g * (int64_t)(5 * N * LW) + lane : nullptr;
   const double2* u2 = reinterpret_cast<const double2*>(u);
   double ps[N], om[N];
 #pragma unroll
@@ -737,9 +751,28 @@ __device__ __forceinline__ void axisym_group(const uint32_t* __restrict__ mapP,
       w0o[m] = fma(g00, d0o[m], g01 * d1o);
       w1o[m] = fma(g01, d0o[m], g11 * d1o);
       // pointwise terms at test node (m, j): psi row 2W gx(psi) - rho^2 W omega,
-      // omega row (W/rho) omega
+      // omega row (W/rho) omega (+ the advection term for Navier-Stokes)
+      double adv = 0.0;
+      if constexpr (MODE == 1) {
+        const double f7 = gp[(7 * N + m) * LW], f8 = gp[(8 * N + m) * LW];
+        const double rw = ns.re * (w.v[m] * wj);
+        const double dz = fma(f7, d0p[m], f8 * d1p);  // (W/rho) dpsi/dz
+        adv = fma(rw, fma(d0p[m], d1o, -d1p * d0o[m]), ns.re * om[m] * dz);
+        if (lin && in_wave) {
+          lin[(0 * N + m) * LW] = fma(rw, d1o, ns.re * f7 * om[m]);
+          lin[(1 * N + m) * LW] = fma(-rw, d0o[m], ns.re * f8 * om[m]);
+          lin[(2 * N + m) * LW] = -rw * d1p;
+          lin[(3 * N + m) * LW] = rw * d0p[m];
+          lin[(4 * N + m) * LW] = ns.re * dz;
+        }
+      } else if constexpr (MODE == 2) {
+        adv = fma(lin[(0 * N + m) * LW], d0p[m],
+                  fma(lin[(1 * N + m) * LW], d1p,
+                      fma(lin[(2 * N + m) * LW], d0o[m],
+                          fma(lin[(3 * N + m) * LW], d1o, lin[(4 * N + m) * LW] * om[m]))));
+      }
       d0p[m] = fma(b0, d0p[m], fma(b1, d1p, -mm * om[m]));
-      d0o[m] = c * om[m];
+      d0o[m] = fma(c, om[m], adv);
     }
     deo_apply_t<N>(D, w0p, vp);
     deo_apply_t<N>(D, w0o, vo);
@@ -781,11 +814,11 @@ __device__ __forceinline__ void axisym_group(const uint32_t* __restrict__ mapP,
   wave_sync();
 }
 
-template <int N>
+template <int N, int MODE>
 __global__ void __launch_bounds__(CHAIN_BLOCK)
     k_axisym_apply(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
                    const double* __restrict__ u, double* __restrict__ y, int64_t c0, int64_t c1,
-                   int rounds, int accumulate, const DEO<N> D) {
+                   int rounds, int accumulate, const DEO<N> D, const WVec<N> w, const AxiNS ns) {
   using T = Tile<N>;
   __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * 2 * T::ES];
   __shared__ double carry[2][CHAIN_WAVES][2][N];
@@ -796,13 +829,15 @@ __global__ void __launch_bounds__(CHAIN_BLOCK)
   const int k = lane / N;
   const int j = lane - k * N;
   const bool in_wave = lane < T::LW;
+  const double wj = pick<N>(w, j);
   double* LP = lds + T::slot(wave, k, in_wave) * T::ES;  // psi tile plane
   double* LO = LP + T::TILE_SLOTS * T::ES;                // omega tile plane
   for (int rd = 0; rd < rounds; ++rd) {
     const int64_t g = (chain * rounds + rd) * CHAIN_WAVES + wave;
     uint32_t raw[N];
     double v[2][N];  // [0] omega row (y[2k]), [1] psi row (y[2k+1])
-    axisym_group<N>(mapP, GP, u, g, lane, j, in_wave, LP, LO, D, raw, v[0], v[1]);
+    axisym_group<N, MODE>(mapP, GP, u, g, lane, j, in_wave, LP, LO, D, w, wj, ns, raw, v[0],
+                          v[1]);
     chain_emit<N, 2>(y, raw, v, lane, wave, rd, in_wave, carry, accumulate);
   }
 }
@@ -1128,7 +1163,7 @@ __global__ void __launch_bounds__(GeomShape<N>::THREADS)
     const int64_t grp = e / epw;
     const int kk = (int)(e - grp * epw);
     const int64_t gg = gpos[grp];
-    const int ncomp = (op_kind == 0) ? 3 : 7;
+    const int ncomp = (op_kind == 0) ? 3 : (op_kind == 1 ? 7 : 9);
     double* o = GP + gg * (int64_t)(ncomp * N * LW) + m * LW + kk * N + nq;
     const double A00 = iJ00 * iJ00 + iJ01 * iJ01;
     const double A01 = iJ00 * iJ10 + iJ01 * iJ11;
@@ -1147,6 +1182,10 @@ __global__ void __launch_bounds__(GeomShape<N>::THREADS)
       o[4 * N * LW] = 2.0 * W * iJ10;
       o[5 * N * LW] = W / rho;
       o[6 * N * LW] = rW * rho;
+      if (ncomp == 9) {  // Navier-Stokes advection: (W/rho) iJ01, (W/rho) iJ11
+        o[7 * N * LW] = (W / rho) * iJ01;
+        o[8 * N * LW] = (W / rho) * iJ11;
+      }
     }
   }
 }

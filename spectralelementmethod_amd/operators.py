@@ -23,8 +23,11 @@ from .basis_functions import LagrangeGaussLobatto, TensorProductQS
 
 POISSON = _lib.OP_POISSON
 AXISYM_STOKES = _lib.OP_AXISYM_STOKES
+AXISYM_NS = _lib.OP_AXISYM_NS
+AXISYM_NS_JVP = _lib.OP_AXISYM_NS_JVP
 _KIND_NAMES = {"poisson": POISSON, "laplace": POISSON, "stiffness": POISSON,
-               "axisym_stokes": AXISYM_STOKES, "stokes_axisym": AXISYM_STOKES}
+               "axisym_stokes": AXISYM_STOKES, "stokes_axisym": AXISYM_STOKES,
+               "axisym_ns": AXISYM_NS, "axisym_ns_jvp": AXISYM_NS_JVP}
 
 
 def op_kind(kind):
@@ -33,9 +36,14 @@ def op_kind(kind):
             return _KIND_NAMES[kind.lower()]
         except KeyError:
             raise ValueError("unknown operator kind %r" % kind)
-    if kind not in (POISSON, AXISYM_STOKES):
+    if kind not in (POISSON, AXISYM_STOKES, AXISYM_NS, AXISYM_NS_JVP):
         raise ValueError("unknown operator kind %r" % kind)
     return int(kind)
+
+
+def _geom_key(kind):
+    """The two Navier-Stokes kinds share one set of geometric factors."""
+    return AXISYM_NS if kind == AXISYM_NS_JVP else kind
 
 
 def _device_index(device):
@@ -202,7 +210,7 @@ class SEMOperator(object):
             _lib.check(self._lib.sem_geom_from_nodes(self._ctx, _lib.tptr(self.nodes),
                                                      _lib.dptr(self.Vinv), kind, C.byref(bad),
                                                      self._stream(stream)))
-        self._geom_ready.add(kind)
+        self._geom_ready.add(_geom_key(kind))
         return self
 
     def set_geometry(self, G, kind=POISSON, stream=None):
@@ -216,7 +224,7 @@ class SEMOperator(object):
         with torch.cuda.device(self.device):
             _lib.check(self._lib.sem_set_geom(self._ctx, _lib.tptr(G), kind, self._stream(stream)))
             torch.cuda.current_stream().synchronize()
-        self._geom_ready.add(kind)
+        self._geom_ready.add(_geom_key(kind))
         return self
 
     def geometry_fields(self, stream=None):
@@ -249,10 +257,18 @@ class SEMOperator(object):
             raise ValueError("%s has %d entries, expected ndof = %d" % (name, v.numel(), self.ndof))
         return v
 
-    def apply(self, u, out=None, kind=POISSON, accumulate=False, stream=None):
-        """out (=|+=) K u for all elements in one launch (device tensors)."""
+    def set_reynolds(self, re):
+        """Reynolds number of the Navier-Stokes kinds (squirmer n_rey)."""
+        _lib.check(self._lib.sem_set_reynolds(self._ctx, float(re)))
+        return self
+
+    def apply(self, u, out=None, kind=POISSON, accumulate=False, stream=None, linearize=False):
+        """out (=|+=) K u for all elements in one launch (device tensors).
+        kind "axisym_ns": the Re > 0 residual at the state u = (psi, omega);
+        with linearize=True the Newton linearisation at u is recorded for
+        kind "axisym_ns_jvp" (Jacobian times the direction u)."""
         kind = op_kind(kind)
-        if kind not in self._geom_ready:
+        if _geom_key(kind) not in self._geom_ready:
             self.compute_geometry(kind, stream=stream)
         is_np = not isinstance(u, torch.Tensor)
         u = self._vec(u, "u")
@@ -265,15 +281,17 @@ class SEMOperator(object):
             raise TypeError("out must be a contiguous float64 tensor of %d entries on %s"
                             % (self.ndof, self.device))
         with torch.cuda.device(self.device):
-            _lib.check(self._lib.sem_apply(self._ctx, kind, _lib.tptr(u), _lib.tptr(out),
-                                           1 if accumulate else 0, self._stream(stream)))
+            flags = (_lib.APPLY_ACCUMULATE if accumulate else 0) | \
+                (_lib.APPLY_LINEARIZE if linearize else 0)
+            _lib.check(self._lib.sem_apply(self._ctx, kind, _lib.tptr(u), _lib.tptr(out), flags,
+                                           self._stream(stream)))
         if is_np:
             return out.cpu().numpy()
         return out
 
     def diag(self, kind=POISSON, stream=None):
         kind = op_kind(kind)
-        if kind not in self._geom_ready:
+        if _geom_key(kind) not in self._geom_ready:
             self.compute_geometry(kind, stream=stream)
         d = torch.empty(self.ndof, dtype=torch.float64, device=self.device)
         with torch.cuda.device(self.device):
@@ -286,7 +304,7 @@ class SEMOperator(object):
         with Jacobi-preconditioned CG on the device.  ``x`` (device tensor) is
         updated in place and returned with (iterations, relative residual)."""
         kind = op_kind(kind)
-        if kind not in self._geom_ready:
+        if _geom_key(kind) not in self._geom_ready:
             self.compute_geometry(kind, stream=stream)
         rhs = self._vec(rhs, "rhs")
         if not isinstance(x, torch.Tensor) or x.device != self.device:
