@@ -38,7 +38,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FP64_PEAK_TFLOPS = 78.6  # MI355X vector fp64 (256 CUs x 128 FLOP/clk x 2.4 GHz)
 # PMC-measured HBM bytes of the headline workload, per geometry mode
 DEFAULT_TRAFFIC = {"stored": "r01/pmc_traffic_p8_1024x1024.json",
-                   "nodal": "r01/pmc_traffic_nodal_p8_1024x1024.json"}
+                   "nodal": "r01b/pmc_traffic_nodal_p8_1024x1024.json"}
 
 
 def log(msg):
@@ -135,6 +135,8 @@ def main():
                     help="Poisson kernel family: LDS column kernel or fp64-MFMA element kernel; "
                          "auto = the library's measured choice")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-check", action="store_true",
+                    help="skip the finiteness check (timing-only diagnostic builds)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--traffic-json", default=None,
                     help="JSON with PMC-measured HBM bytes per launch (profiles/)")
@@ -216,7 +218,7 @@ def main():
 
     # correctness spot check of the timed output (cheap, outside the timing):
     # y must be finite and u.Ku > 0 on this rank's block
-    assert torch.isfinite(y).all().item()
+    assert args.no_check or torch.isfinite(y).all().item()
 
     n_nodes_local = op.ndof // dpn
     ndof_global = part.global_nodes * dpn if kind == POISSON else op.ndof

@@ -58,7 +58,16 @@ constexpr uint32_t W_MERGE = 4;   // add the next lane's value before writing
 constexpr uint32_t W_CARRY = 8;   // add the value handed over by the previous group
 
 #ifndef SEM_POISSON_MIN_WAVES
-#define SEM_POISSON_MIN_WAVES 1
+#define SEM_POISSON_MIN_WAVES 0  // 0: per-order choice (PoissonMinWaves)
+#endif
+#ifndef SEM_NT_MAP
+#define SEM_NT_MAP 0  // map stream read with nontemporal loads
+#endif
+#ifndef SEM_NT_STORE
+#define SEM_NT_STORE 1  // first-writer y stores nontemporal
+#endif
+#ifndef SEM_RMW_PREFETCH
+#define SEM_RMW_PREFETCH 1  // Poisson: read read-modify-write targets before the last passes
 #endif
 
 // D1 in even-odd form.  D is centro-antisymmetric (D[N-1-i][N-1-j] =
@@ -114,6 +123,10 @@ template <int N>
 __device__ __forceinline__ void deo_apply(const DEO<N>& D, const double (&x)[N],
                                           double (&v)[N]) {
   constexpr int H = N / 2;
+#ifdef SEM_DIAG_NO_COMPUTE
+  for (int r = 0; r < N; ++r) v[r] = x[r] * 0.5;  // timing-only: memory/LDS floor
+  return;
+#endif
   double e[H], o[H];
 #pragma unroll
   for (int r = 0; r < H; ++r) {
@@ -147,6 +160,10 @@ template <int N>
 __device__ __forceinline__ void deo_apply_t(const DEO<N>& D, const double (&x)[N],
                                             double (&v)[N]) {
   constexpr int H = N / 2;
+#ifdef SEM_DIAG_NO_COMPUTE
+  for (int r = 0; r < N; ++r) v[r] = x[r] * 0.5;
+  return;
+#endif
   double e[H], o[H];
 #pragma unroll
   for (int r = 0; r < H; ++r) {
@@ -207,12 +224,19 @@ __device__ __forceinline__ void atomic_add_f64(double* p, double v) {
 // before the workgroup's own store is never reused.
 __device__ __forceinline__ double rmw_load(const double* p) { return __builtin_nontemporal_load(p); }
 
+// NT: nontemporal first-writer stores (the column kernels' row-contiguous
+// scatter; the MFMA kernel's scattered 16 x 16 layout measured 10 % slower
+// with them at p = 12)
+template <bool NT = (SEM_NT_STORE != 0)>
 __device__ __forceinline__ void emit1(double* __restrict__ y, uint32_t raw, double v,
                                       int accumulate) {
   const uint32_t a = (raw >> CODE_SHIFT) & 3u;
   double* dst = y + (raw & GID_MASK);
   if (a == W_STORE) {
-    *dst = accumulate ? rmw_load(dst) + v : v;
+    if constexpr (NT)
+      __builtin_nontemporal_store(accumulate ? rmw_load(dst) + v : v, dst);
+    else
+      *dst = accumulate ? rmw_load(dst) + v : v;
   } else if (a == W_RMW) {
 #if defined(SEM_DIAG_RMW_AS_STORE)
     *dst = v;  // timing-only
@@ -220,6 +244,43 @@ __device__ __forceinline__ void emit1(double* __restrict__ y, uint32_t raw, doub
     atomic_add_f64(dst, v);  // no writer runs concurrently: ordered, no return
 #else
     *dst = rmw_load(dst) + v;
+#endif
+  } else if (a == W_ATOMIC) {
+    atomic_add_f64(dst, v);
+  }
+}
+
+// Poisson scatter with the read-modify-write operands already in registers
+// (rmw_prefetch): no memory latency between the last contraction and the
+// stores.  Safe because a RMW target's earlier writers are an earlier launch
+// (colour), an earlier round of this chain (ended by a workgroup barrier) or
+// an earlier operator in stream order -- never a concurrent wave.
+template <int N>
+__device__ __forceinline__ void rmw_prefetch(const double* __restrict__ y,
+                                             const uint32_t (&raw)[N], int accumulate,
+                                             double (&prev)[N]) {
+  // predicated without branches: a lane that needs no operand reads past the
+  // end of the buffer range (returns 0, no memory traffic).  Node ids are
+  // < 2^28, so byte offsets stay below the 2^31-byte range.
+  const __amdgpu_buffer_rsrc_t ry =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(y), 0, 0x80000000, 0x00020000);
+#pragma unroll
+  for (int p = 0; p < N; ++p) {
+    const uint32_t a = (raw[p] >> CODE_SHIFT) & 3u;
+    const bool need = a == W_RMW || (a == W_STORE && accumulate);
+    const uint32_t off = need ? (raw[p] & GID_MASK) * 8u : 0x80000000u;
+    prev[p] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(ry, off, 0, 2 /*nt*/));
+  }
+}
+
+__device__ __forceinline__ void emit1p(double* __restrict__ y, uint32_t raw, double v, double prev) {
+  const uint32_t a = (raw >> CODE_SHIFT) & 3u;
+  double* dst = y + (raw & GID_MASK);
+  if (a == W_STORE || a == W_RMW) {  // prev = 0 for a first writer in overwrite mode
+#if SEM_NT_STORE
+    __builtin_nontemporal_store(prev + v, dst);
+#else
+    *dst = prev + v;
 #endif
   } else if (a == W_ATOMIC) {
     atomic_add_f64(dst, v);
@@ -282,7 +343,7 @@ __device__ __forceinline__ void store_row(double* L, int i, const double (&t)[N]
 #define SEM_TILE_PAD_STORED 1
 #endif
 #ifndef SEM_TILE_PAD_NODAL
-#define SEM_TILE_PAD_NODAL 1
+#define SEM_TILE_PAD_NODAL 0
 #endif
 #ifndef SEM_NODAL_EARLY_U
 #define SEM_NODAL_EARLY_U 0
@@ -332,7 +393,8 @@ __device__ __forceinline__ void poisson_group_stored(const uint32_t* __restrict_
                                                      const double* __restrict__ u, int64_t g,
                                                      int lane, int j, bool in_wave, double* L,
                                                      const DEO<N>& D, uint32_t (&raw)[N],
-                                                     double (&v)[N]) {
+                                                     double (&v)[N], const double* __restrict__ y,
+                                                     int accumulate, double (&prev)[N]) {
   using T = Tile<N, SEM_TILE_PAD_STORED>;
   constexpr int LW = T::LW;
   constexpr int RS = T::RS;
@@ -373,7 +435,13 @@ __device__ __forceinline__ void poisson_group_stored(const uint32_t* __restrict_
       w0[m] = fma(g00, d0[m], g01 * d1);
       L[m * RS + j] = fma(g01, d0[m], g11 * d1);  // w1, same lane's slot
     }
+#if SEM_RMW_PREFETCH == 1
+    rmw_prefetch<N>(y, raw, accumulate, prev);
+#endif
     deo_apply_t<N>(D, w0, v);
+#if SEM_RMW_PREFETCH == 2
+    rmw_prefetch<N>(y, raw, accumulate, prev);
+#endif
   }
   wave_sync();
   // row i = j: yb[i][q] = sum_n D[n][q] w1[i][n]
@@ -416,7 +484,12 @@ __device__ __forceinline__ void load_map(const uint32_t* __restrict__ mapP, int6
   constexpr int LW = Tile<N>::LW;
   const uint32_t* mp = mapP + g * (int64_t)(N * LW) + lane;
 #pragma unroll
-  for (int r = 0; r < N; ++r) raw[r] = in_wave ? mp[r * LW] : (W_SKIP << CODE_SHIFT);
+  for (int r = 0; r < N; ++r)
+#if SEM_NT_MAP
+    raw[r] = in_wave ? __builtin_nontemporal_load(mp + r * LW) : (W_SKIP << CODE_SHIFT);
+#else
+    raw[r] = in_wave ? mp[r * LW] : (W_SKIP << CODE_SHIFT);
+#endif
 }
 
 template <int N>
@@ -490,7 +563,9 @@ __device__ __forceinline__ void nodal_geometry(const double2 (&xc)[N], int j, do
   for (int m = 0; m < N; ++m) {
     const double js0 = A[m * RS + j], js1 = B[m * RS + j];
     const double det = jr0[m] * js1 - js0 * jr1[m];
-    const double sc = (w.v[m] * wj) * fast_rcp(det);
+    // (w_m w_j) / det, associated so that no loop-invariant w_m w_j array
+    // is hoisted out of the round loop (9 doubles spilled at 4 waves/SIMD)
+    const double sc = w.v[m] * (wj * fast_rcp(det));
     g00[m] = sc * fma(js1, js1, js0 * js0);
     g01[m] = -sc * fma(js1, jr1[m], js0 * jr0[m]);
     B[m * RS + j] = sc * fma(jr1[m], jr1[m], jr0[m] * jr0[m]);  // G11, own slot
@@ -503,7 +578,9 @@ template <int N>
 __device__ __forceinline__ void nodal_laplacian(const double (&uc)[N], int j, double* A,
                                                 const double* B, const DEO<N>& D,
                                                 const double (&g00)[N], const double (&g01)[N],
-                                                double (&v)[N]) {
+                                                double (&v)[N], const double* __restrict__ y,
+                                                const uint32_t (&raw)[N], int accumulate,
+                                                double (&prev)[N]) {
   constexpr int RS = Tile<N, SEM_TILE_PAD_NODAL>::RS;
   double d0[N];
   deo_apply<N>(D, uc, d0);
@@ -519,7 +596,13 @@ __device__ __forceinline__ void nodal_laplacian(const double (&uc)[N], int j, do
       w0[m] = fma(g00[m], d0[m], g01[m] * d1);
       A[m * RS + j] = fma(g01[m], d0[m], B[m * RS + j] * d1);
     }
+#if SEM_RMW_PREFETCH == 1
+    rmw_prefetch<N>(y, raw, accumulate, prev);
+#endif
     deo_apply_t<N>(D, w0, v);
+#if SEM_RMW_PREFETCH == 2
+    rmw_prefetch<N>(y, raw, accumulate, prev);
+#endif
   }
   wave_sync();
   row_pass<N, RS, true, false>(A, j, D);
@@ -536,7 +619,9 @@ __device__ __forceinline__ void poisson_group_nodal(const uint32_t* __restrict__
                                                     int lane, int j, bool in_wave, double* A,
                                                     double* B, const DEO<N>& D,
                                                     const WVec<N>& w, double wj,
-                                                    uint32_t (&raw)[N], double (&v)[N]) {
+                                                    uint32_t (&raw)[N], double (&v)[N],
+                                                    const double* __restrict__ y, int accumulate,
+                                                    double (&prev)[N]) {
   double uc[N];
   double2 xc[N];
   load_map<N>(mapP, g, lane, in_wave, raw);
@@ -549,17 +634,18 @@ __device__ __forceinline__ void poisson_group_nodal(const uint32_t* __restrict__
 #if !SEM_NODAL_EARLY_U
   gather_u<N>(u, raw, uc);
 #endif
-  nodal_laplacian<N>(uc, j, A, B, D, g00, g01, v);
+  nodal_laplacian<N>(uc, j, A, B, D, g00, g01, v, y, raw, accumulate, prev);
 }
+
 
 // Scatter of one group's column values through the coded map, with the
 // in-group merge (next lane) and the chain carry (previous group) applied.
 // ncomp values per node (1: Poisson, 2: axisymmetric block).
-template <int N, int NC>
+template <int N, int NC, bool PRE = false>
 __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_t (&raw)[N],
                                            double (&v)[NC][N], int lane, int wave, int rd,
                                            bool in_wave, double (*carry)[CHAIN_WAVES][NC][N],
-                                           int accumulate) {
+                                           int accumulate, const double* prev = nullptr) {
   constexpr int LW = Tile<N>::LW;
 #pragma unroll
   for (int c = 0; c < NC; ++c)
@@ -591,7 +677,9 @@ __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_
   if (in_wave) {
 #pragma unroll
     for (int p = 0; p < N; ++p) {
-      if (NC == 1)
+      if constexpr (PRE)
+        emit1p(y, raw[p], v[0][p], prev[p]);
+      else if (NC == 1)
         emit1(y, raw[p], v[0][p], accumulate);
       else
         emit2(y, raw[p], v[0][p], v[NC - 1][p], accumulate);
@@ -624,8 +712,18 @@ __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nwg) {
 // ---------------------------------------------------------------------------
 // Poisson stiffness action: one workgroup per chain, chains [c0, c1).
 // ---------------------------------------------------------------------------
+// minimum waves per SIMD requested from the register allocator.  p = 8
+// nodal: 4 (128 VGPRs, no spill; the unpadded tiles fit 4 workgroups per CU)
+// measured 0.709 vs 0.731 ms at 3 waves (profiles/r01/occupancy).
 template <int N, bool NODAL>
-__global__ void __launch_bounds__(CHAIN_BLOCK, SEM_POISSON_MIN_WAVES)
+struct PoissonMinWaves {
+  static constexpr int value = SEM_POISSON_MIN_WAVES > 0 ? SEM_POISSON_MIN_WAVES
+                               : (NODAL && N == 9)      ? 4
+                                                        : 1;
+};
+
+template <int N, bool NODAL>
+__global__ void __launch_bounds__(CHAIN_BLOCK, (PoissonMinWaves<N, NODAL>::value))
     k_poisson_apply(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
                     const double2* __restrict__ XG, const double* __restrict__ u,
                     double* __restrict__ y, int64_t c0, int64_t c1, int rounds, int accumulate,
@@ -650,15 +748,17 @@ __global__ void __launch_bounds__(CHAIN_BLOCK, SEM_POISSON_MIN_WAVES)
   for (int rd = 0; rd < rounds; ++rd) {
     const int64_t g = (chain * rounds + rd) * CHAIN_WAVES + wave;
     uint32_t raw[N];
-    double v[1][N];
+    double v[1][N], prev[N];
     if constexpr (NODAL)
-      poisson_group_nodal<N>(mapP, XG, u, g, lane, j, in_wave, L, LB, D, w, wj, raw, v[0]);
+      poisson_group_nodal<N>(mapP, XG, u, g, lane, j, in_wave, L, LB, D, w, wj, raw, v[0], y,
+                             accumulate, prev);
     else
-      poisson_group_stored<N>(mapP, GP, u, g, lane, j, in_wave, L, D, raw, v[0]);
+      poisson_group_stored<N>(mapP, GP, u, g, lane, j, in_wave, L, D, raw, v[0], y, accumulate,
+                              prev);
 #ifdef SEM_DIAG_NO_STORE
     if (in_wave && v[0][0] == 1234.5678) y[0] = v[0][1];  // timing-only
 #else
-    chain_emit<N, 1>(y, raw, v, lane, wave, rd, in_wave, carry, accumulate);
+    chain_emit<N, 1, (SEM_RMW_PREFETCH > 0)>(y, raw, v, lane, wave, rd, in_wave, carry, accumulate, prev);
 #endif
   }
 }
@@ -1026,7 +1126,7 @@ __global__ void __launch_bounds__(BLOCK, SEM_MFMA_MIN_WAVES)
   for (int s = 0; s < KS; ++s) acc = mfma_f64(W1T[0][s], Dt[s], acc);
   // row 4i + h < TN implies i < KS; padding entries carry SKIP
 #pragma unroll
-  for (int i = 0; i < KS; ++i) emit1(y, raw[i], acc[i], accumulate);
+  for (int i = 0; i < KS; ++i) emit1<false>(y, raw[i], acc[i], accumulate);
 }
 
 // ---------------------------------------------------------------------------
