@@ -38,24 +38,30 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FP64_PEAK_TFLOPS = 78.6  # MI355X vector fp64 (256 CUs x 128 FLOP/clk x 2.4 GHz)
 # PMC-measured HBM bytes of the headline workload, per geometry mode
 DEFAULT_TRAFFIC = {"stored": "r01/pmc_traffic_p8_1024x1024.json",
-                   "nodal": "r01b/pmc_traffic_nodal_p8_1024x1024.json"}
+                   "nodal": "r01c/pmc_traffic_nodal_p8_1024x1024.json"}
 
 
 def log(msg):
     print("[bench] " + msg, file=sys.stderr, flush=True)
 
 
-def alg_bytes(kind, ndof_nodes, n_elem, p, geometry="stored"):
+def alg_bytes(kind, ndof_nodes, n_elem, p, geometry="stored", map_bytes=4):
     """Poisson with stored factors B = 16*ndof + 28*E*(p+1)^2
     (u read, y written, 3 fp64 factors + one uint32 map entry per local
     node); with nodal geometry the factors are replaced by x_phys per global
     node: B = 32*ndof + 4*E*(p+1)^2; axisymmetric B = 32*n_nodes +
-    60*E*(p+1)^2 (Navier-Stokes residual: 9 factors, 76*E*(p+1)^2)."""
-    n2 = (p + 1) ** 2
-    if kind == POISSON and geometry == "nodal":
-        return 32 * ndof_nodes + 4 * n_elem * n2
+    60*E*(p+1)^2 (Navier-Stokes residual: 9 factors, 76*E*(p+1)^2).
+    map_bytes = 2: the column kernel streams 16-bit map entries plus one
+    uint32 base per group row (4*(p+1) bytes per floor(64/(p+1)) elements)."""
+    n = p + 1
+    n2 = n * n
     if kind == POISSON:
-        return 16 * ndof_nodes + 28 * n_elem * n2
+        m = map_bytes * n_elem * n2
+        if map_bytes == 2:
+            m += 4 * n * n_elem // (64 // n)
+        if geometry == "nodal":
+            return 32 * ndof_nodes + m
+        return 16 * ndof_nodes + 24 * n_elem * n2 + m
     if kind == AXISYM_NS:
         return 32 * ndof_nodes + 76 * n_elem * n2
     return 32 * ndof_nodes + 60 * n_elem * n2
@@ -223,7 +229,13 @@ def main():
     n_nodes_local = op.ndof // dpn
     ndof_global = part.global_nodes * dpn if kind == POISSON else op.ndof
     value = ndof_global * args.steps / elapsed
+    map_bytes = plan.get("map_entry_bytes", 4) if (plan["kernel"] == "column"
+                                                  and kind == POISSON) else 4
+    # algorithmic bytes keep SURVEY.md §8(d)'s uint32 map (the problem's
+    # input); the bytes the kernel streams with a 16-bit packed map are
+    # reported beside them
     B = alg_bytes(kind, n_nodes_local, n_elem_local, p, geometry)
+    B_stream = alg_bytes(kind, n_nodes_local, n_elem_local, p, geometry, map_bytes)
     F = alg_flops(kind, n_elem_local, p, geometry)
     achieved = B / kern_avg_s / 1e9
     traffic = None
@@ -263,7 +275,7 @@ def main():
             "single GPU",
             "kernel_ms_avg": kern_avg_s * 1e3, "kernel_ms_min": float(np.min(kern_ms)),
             "gflops_kernel": F / kern_avg_s / 1e9,
-            "kernel_family": plan["kernel"],
+            "kernel_family": plan["kernel"], "map_entry_bytes": map_bytes,
             "scatter_plan": {k: plan[k] for k in ("colours", "chains_per_colour", "rounds", "zero_list",
                                                   "atomic_groups")},
         },
@@ -272,7 +284,7 @@ def main():
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
             "kernel": ("k_poisson_mfma<%d>" if plan["kernel"] == "mfma" else "k_poisson_apply<%d>")
                       % (p + 1) if kind == POISSON else "k_axisym_apply<%d>" % (p + 1),
-            "alg_bytes_per_launch": B,
+            "alg_bytes_per_launch": B, "streamed_bytes_per_launch": B_stream,
             "fp64_tflops": F / kern_avg_s / 1e12, "fp64_peak_tflops": FP64_PEAK_TFLOPS,
             "launch": "one sem_apply = %d colour launches" % plan["colours"],
             "traffic_source": os.path.relpath(traffic_src, ROOT) if traffic is not None else None,

@@ -124,7 +124,10 @@ int sem_set_map_shared(sem_ctx* ctx, const uint32_t* d_e2n, const uint8_t* d_nod
  * [5] colour classes, [6] rounds of 4 groups per chain (one workgroup per
  * chain), [7] packed group slots, [8..16] chains per colour class (one launch
  * each; elements for the MFMA kernel), [17] kernel family (SEM_KERNEL_COLUMN
- * or SEM_KERNEL_MFMA).  Writes min(n_info, 18) values. */
+ * or SEM_KERNEL_MFMA), [18] bytes per packed map entry the Poisson column
+ * kernel streams (2: 16-bit row offsets, used when every group row spans
+ * < 4096 node ids; 4 otherwise; SEM_MAP16=0 in the environment forces 4).
+ * Writes min(n_info, 19) values. */
 int sem_plan_info(sem_ctx* ctx, int64_t* info, int n_info);
 
 /* How the Poisson action obtains its geometric factors.

@@ -272,6 +272,9 @@ struct sem_ctx {
   double* d_Vinv = nullptr;
   double* d_deo = nullptr;  // even-odd D for n >= SEM_D_SCALAR_LOAD_N (scalar loads)
   uint32_t* d_mapP = nullptr;   // packed coded map, launch (colour) order
+  uint16_t* d_map16 = nullptr;  // the same map as 16-bit row offsets (column kernel)
+  uint32_t* d_mbase = nullptr;  // their per-(slot, row) 32-bit bases
+  bool map16 = false;
   int* d_gpos = nullptr;         // natural group -> packed slot
   const uint32_t* d_e2n = nullptr;
   uint32_t* d_zero = nullptr;    // y entries no kernel stores first (unreferenced / first-atomic)
@@ -401,12 +404,23 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
           hipLaunchKernelGGL((k_poisson_mfma<N, false>), g, dim3(BLOCK), 0, st, c->d_mapP,
                              c->d_GP[0], nullptr, u, y, c->d_D, w, c0, c1, acc);
       }
-    } else if (op_kind == SEM_OP_POISSON && nodal)
-      hipLaunchKernelGGL((k_poisson_apply<N, true>), dim3(grid), dim3(CHAIN_BLOCK), 0, st,
-                         c->d_mapP, nullptr, c->d_XG, u, y, c0, c1, c->rounds, acc, D, w);
-    else if (op_kind == SEM_OP_POISSON)
-      hipLaunchKernelGGL((k_poisson_apply<N, false>), dim3(grid), dim3(CHAIN_BLOCK), 0, st,
-                         c->d_mapP, c->d_GP[0], nullptr, u, y, c0, c1, c->rounds, acc, D, w);
+    } else if (op_kind == SEM_OP_POISSON) {
+      const MapRef mr{c->d_mapP, c->d_map16, c->d_mbase};
+      const double* GP = nodal ? nullptr : c->d_GP[0];
+      const double2* XG = nodal ? c->d_XG : nullptr;
+      if (nodal && c->map16)
+        hipLaunchKernelGGL((k_poisson_apply<N, true, true>), dim3(grid), dim3(CHAIN_BLOCK), 0, st,
+                           mr, GP, XG, u, y, c0, c1, c->rounds, acc, D, w);
+      else if (nodal)
+        hipLaunchKernelGGL((k_poisson_apply<N, true, false>), dim3(grid), dim3(CHAIN_BLOCK), 0,
+                           st, mr, GP, XG, u, y, c0, c1, c->rounds, acc, D, w);
+      else if (c->map16)
+        hipLaunchKernelGGL((k_poisson_apply<N, false, true>), dim3(grid), dim3(CHAIN_BLOCK), 0,
+                           st, mr, GP, XG, u, y, c0, c1, c->rounds, acc, D, w);
+      else
+        hipLaunchKernelGGL((k_poisson_apply<N, false, false>), dim3(grid), dim3(CHAIN_BLOCK), 0,
+                           st, mr, GP, XG, u, y, c0, c1, c->rounds, acc, D, w);
+    }
     else if (op_kind == SEM_OP_AXISYM_STOKES)
       hipLaunchKernelGGL((k_axisym_apply<N, 0>), dim3(grid), dim3(CHAIN_BLOCK), 0, st, c->d_mapP,
                          c->d_GP[1], u, y, c0, c1, c->rounds, acc, D, w, AxiNS());
@@ -694,6 +708,52 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
 }
 
 
+// 16-bit form of a column-kernel plan's packed map: one 32-bit
+// base per (slot, row) = the smallest node id of the row's real elements,
+// entries (gid - base) | code << 12, for rows spanning fewer than 4096 ids
+// (locality-ordered meshes; 57 consecutive ids per row at p = 8 on the
+// structured mesh); padding entries keep offset 0.  A group with a wider row
+// is flagged (base[slot][0] = M16_WIDE) and reads the 32-bit map; the form is
+// used only when at most 1 / 16 of the groups are flagged.
+static bool build_map16(const Plan& P, int64_t n_elem, int n, int epw, int64_t n_groups,
+                        std::vector<uint16_t>& m16, std::vector<uint32_t>& base) {
+  const int lw = epw * n;
+  std::vector<int64_t> slot_group(P.n_slots, -1);
+  for (int64_t g = 0; g < n_groups; ++g) slot_group[P.gpos[g]] = g;
+  m16.assign((size_t)P.n_slots * n * lw, (uint16_t)(W_SKIP << M16_CODE_SHIFT));
+  base.assign((size_t)P.n_slots * n, 0u);
+  int64_t wide = 0;
+  for (int64_t sl = 0; sl < P.n_slots; ++sl) {
+    const int64_t g = slot_group[sl];
+    if (g < 0) continue;
+    const int lanes = (int)std::min<int64_t>(epw, n_elem - g * epw) * n;
+    bool fits = true;
+    for (int r = 0; r < n && fits; ++r) {
+      const uint32_t* row = &P.mapP[((size_t)sl * n + r) * lw];
+      uint32_t lo = 0xFFFFFFFFu, hi = 0;
+      for (int l = 0; l < lanes; ++l) {
+        lo = std::min(lo, row[l] & GID_MASK);
+        hi = std::max(hi, row[l] & GID_MASK);
+      }
+      base[(size_t)sl * n + r] = lo;
+      fits = hi - lo <= M16_OFF_MASK;
+    }
+    if (!fits) {
+      base[(size_t)sl * n] = M16_WIDE;
+      ++wide;
+      continue;
+    }
+    for (int r = 0; r < n; ++r) {
+      const uint32_t* row = &P.mapP[((size_t)sl * n + r) * lw];
+      const uint32_t lo = base[(size_t)sl * n + r];
+      uint16_t* out = &m16[((size_t)sl * n + r) * lw];
+      for (int l = 0; l < lanes; ++l)
+        out[l] = (uint16_t)(((row[l] & GID_MASK) - lo) | ((row[l] >> CODE_SHIFT) << M16_CODE_SHIFT));
+    }
+  }
+  return wide * 16 <= n_groups;
+}
+
 // ---------------------------------------------------------------------------
 // Element-level plan for the MFMA kernel (one element per wavefront, no
 // chains): elements are greedily coloured so that elements of one colour
@@ -856,6 +916,8 @@ void sem_ctx_destroy(sem_ctx* c) {
   (void)hipFree(c->d_Vinv);
   (void)hipFree(c->d_deo);
   (void)hipFree(c->d_mapP);
+  (void)hipFree(c->d_map16);
+  (void)hipFree(c->d_mbase);
   (void)hipFree(c->d_gpos);
   (void)hipFree(c->d_zero);
   for (double* g : c->d_GP) (void)hipFree(g);
@@ -930,6 +992,27 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
   HIP_TRY(hipMalloc(&c->d_mapP, P.mapP.size() * sizeof(uint32_t)));
   HIP_TRY(hipMemcpy(c->d_mapP, P.mapP.data(), P.mapP.size() * sizeof(uint32_t),
                     hipMemcpyHostToDevice));
+  // 16-bit map for the column kernel (SEM_MAP16=0 keeps the 32-bit stream):
+  // measured at p = 8, 10^6 elements: see DESIGN.md §4.1
+  (void)hipFree(c->d_map16);
+  (void)hipFree(c->d_mbase);
+  c->d_map16 = nullptr;
+  c->d_mbase = nullptr;
+  c->map16 = false;
+  const char* m16env = std::getenv("SEM_MAP16");
+  if (!mfma && !(m16env && std::atoi(m16env) == 0)) {
+    std::vector<uint16_t> m16;
+    std::vector<uint32_t> mb;
+    if (build_map16(P, c->n_elem, n, c->epw, c->n_groups, m16, mb)) {
+      HIP_TRY(hipMalloc(&c->d_map16, m16.size() * sizeof(uint16_t)));
+      HIP_TRY(hipMemcpy(c->d_map16, m16.data(), m16.size() * sizeof(uint16_t),
+                        hipMemcpyHostToDevice));
+      HIP_TRY(hipMalloc(&c->d_mbase, mb.size() * sizeof(uint32_t)));
+      HIP_TRY(hipMemcpy(c->d_mbase, mb.data(), mb.size() * sizeof(uint32_t),
+                        hipMemcpyHostToDevice));
+      c->map16 = true;
+    }
+  }
   HIP_TRY(hipMalloc(&c->d_gpos, P.gpos.size() * sizeof(int)));
   HIP_TRY(hipMemcpy(c->d_gpos, P.gpos.data(), P.gpos.size() * sizeof(int), hipMemcpyHostToDevice));
   c->n_zero = (int64_t)P.zero.size();
@@ -961,12 +1044,13 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
 int sem_plan_info(sem_ctx* c, int64_t* info, int n_info) {
   if (!c || !info || n_info < 1) return fail(SEM_E_INVALID, "bad arguments");
   const int64_t nc = c->colour_start.empty() ? 0 : (int64_t)c->colour_start.size() - 1;
-  constexpr int NV = 8 + MAX_COLOURS + 1 + 1;
+  constexpr int NV = 8 + MAX_COLOURS + 1 + 1 + 1;
   int64_t vals[NV] = {c->n_groups, c->n_zero, c->n_atomic_groups, c->conforming ? 1 : 0,
                       c->epw,      nc,        c->rounds,          c->n_slots};
   for (int64_t q = 0; q < nc && q <= MAX_COLOURS; ++q)
     vals[8 + q] = c->colour_start[q + 1] - c->colour_start[q];
-  vals[NV - 1] = c->mfma ? SEM_KERNEL_MFMA : SEM_KERNEL_COLUMN;
+  vals[NV - 2] = c->mfma ? SEM_KERNEL_MFMA : SEM_KERNEL_COLUMN;
+  vals[NV - 1] = c->map16 ? 2 : 4;  // bytes per packed map entry
   for (int i = 0; i < n_info && i < NV; ++i) info[i] = vals[i];
   return SEM_OK;
 }

@@ -382,13 +382,67 @@ __device__ __forceinline__ void row_pass(double* L, int j, const DEO<N>& D) {
   wave_sync();
 }
 
+// The coded map of group g, row by row, as raw 32-bit entries gid | code << 28.
+// M16: the packed map holds 16-bit entries (gid - base) | code << 12 with one
+// 32-bit base per group row (a row of a group spans < 4096 node ids on a
+// locality-ordered mesh: 57 consecutive ids at p = 8 on the structured
+// mesh), read with scalar loads -- 2 B instead of 4 per element node.  A
+// group with a wider row (e.g. one that wraps into the next element column)
+// is flagged and reads the 32-bit map instead (uniform branch per wave).
+struct MapRef {
+  const uint32_t* __restrict__ p32;  // [slot][r][lane] gid | code << 28
+  const uint16_t* __restrict__ p16;  // [slot][r][lane] (gid - base) | code << 12
+  const uint32_t* __restrict__ base;  // [slot][r]
+};
+constexpr uint32_t M16_OFF_MASK = 0xFFFu;
+constexpr uint32_t M16_WIDE = 0xFFFFFFFFu;  // base[slot][0]: this group uses the 32-bit map
+constexpr int M16_CODE_SHIFT = 12;
+
+template <int N, bool M16 = false>
+__device__ __forceinline__ void load_map(const MapRef& m, int64_t g, int lane, bool in_wave,
+                                         uint32_t (&raw)[N]) {
+  constexpr int LW = Tile<N>::LW;
+  bool wide = !M16;
+  if constexpr (M16) {
+    // offsets and bases are issued together, ahead of the (rare, uniform)
+    // wide-group branch: a branch on the base before the offset loads
+    // serialised two memory latencies and measured 8 % slower
+    // padding lanes load a valid entry (lane clamped) and discard it: no
+    // load under a branch
+    const uint16_t* mp = m.p16 + g * (int64_t)(N * LW) + (in_wave ? lane : LW - 1);
+    const uint32_t* bp = m.base + g * N;  // g is wave-uniform: scalar loads
+    uint32_t o[N], b[N];
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      const uint32_t t = mp[r * LW];
+      o[r] = in_wave ? t : (W_SKIP << M16_CODE_SHIFT);
+    }
+#pragma unroll
+    for (int r = 0; r < N; ++r) b[r] = bp[r];
+#pragma unroll
+    for (int r = 0; r < N; ++r)
+      raw[r] = (b[r] + (o[r] & M16_OFF_MASK)) | ((o[r] >> M16_CODE_SHIFT) << CODE_SHIFT);
+    wide = b[0] == M16_WIDE;
+  }
+  if (wide) {  // 32-bit map (M16: a group whose rows span >= 4096 ids)
+    const uint32_t* mp = m.p32 + g * (int64_t)(N * LW) + lane;
+#pragma unroll
+    for (int r = 0; r < N; ++r)
+#if SEM_NT_MAP
+      raw[r] = in_wave ? __builtin_nontemporal_load(mp + r * LW) : (W_SKIP << CODE_SHIFT);
+#else
+      raw[r] = in_wave ? mp[r * LW] : (W_SKIP << CODE_SHIFT);
+#endif
+  }
+}
+
 // ---------------------------------------------------------------------------
 // One group of the Poisson action with STORED factors: returns y_e[p][j]
 // (p = 0..N-1) of the lane's column j in v[], and the raw coded map entries.
 //   mapP[g][r][k*N + j] = map[e][r][j] | code,  GP[g][c][r][k*N + j] = G_c(e; r, j)
 // ---------------------------------------------------------------------------
-template <int N>
-__device__ __forceinline__ void poisson_group_stored(const uint32_t* __restrict__ mapP,
+template <int N, bool M16>
+__device__ __forceinline__ void poisson_group_stored(const MapRef& mref,
                                                      const double* __restrict__ GP,
                                                      const double* __restrict__ u, int64_t g,
                                                      int lane, int j, bool in_wave, double* L,
@@ -398,11 +452,9 @@ __device__ __forceinline__ void poisson_group_stored(const uint32_t* __restrict_
   using T = Tile<N, SEM_TILE_PAD_STORED>;
   constexpr int LW = T::LW;
   constexpr int RS = T::RS;
-  const uint32_t* mp = mapP + g * (int64_t)(N * LW) + lane;
   const double* gp = GP + g * (int64_t)(3 * N * LW) + lane;
   double uc[N];
-#pragma unroll
-  for (int r = 0; r < N; ++r) raw[r] = in_wave ? mp[r * LW] : (W_SKIP << CODE_SHIFT);
+  load_map<N, M16>(mref, g, lane, in_wave, raw);
 #pragma unroll
   for (int r = 0; r < N; ++r) {
 #ifdef SEM_DIAG_NO_U
@@ -478,19 +530,6 @@ __device__ __forceinline__ double fast_rcp(double x) {
 // transposed together) beats the fully fused order (u/x/y/w1 one tile pass
 // each, no factor arrays): 0.684 vs 0.714 ms.
 // ---------------------------------------------------------------------------
-template <int N>
-__device__ __forceinline__ void load_map(const uint32_t* __restrict__ mapP, int64_t g, int lane,
-                                         bool in_wave, uint32_t (&raw)[N]) {
-  constexpr int LW = Tile<N>::LW;
-  const uint32_t* mp = mapP + g * (int64_t)(N * LW) + lane;
-#pragma unroll
-  for (int r = 0; r < N; ++r)
-#if SEM_NT_MAP
-    raw[r] = in_wave ? __builtin_nontemporal_load(mp + r * LW) : (W_SKIP << CODE_SHIFT);
-#else
-    raw[r] = in_wave ? mp[r * LW] : (W_SKIP << CODE_SHIFT);
-#endif
-}
 
 template <int N>
 __device__ __forceinline__ void gather_x(const double2* __restrict__ XG, const uint32_t (&raw)[N],
@@ -612,8 +651,8 @@ __device__ __forceinline__ void nodal_laplacian(const double (&uc)[N], int j, do
 }
 
 // One group of the Poisson action with NODAL geometry (no prefetch).
-template <int N>
-__device__ __forceinline__ void poisson_group_nodal(const uint32_t* __restrict__ mapP,
+template <int N, bool M16>
+__device__ __forceinline__ void poisson_group_nodal(const MapRef& mref,
                                                     const double2* __restrict__ XG,
                                                     const double* __restrict__ u, int64_t g,
                                                     int lane, int j, bool in_wave, double* A,
@@ -624,7 +663,7 @@ __device__ __forceinline__ void poisson_group_nodal(const uint32_t* __restrict__
                                                     double (&prev)[N]) {
   double uc[N];
   double2 xc[N];
-  load_map<N>(mapP, g, lane, in_wave, raw);
+  load_map<N, M16>(mref, g, lane, in_wave, raw);
   gather_x<N>(XG, raw, j, xc);
 #if SEM_NODAL_EARLY_U
   gather_u<N>(u, raw, uc);
@@ -722,9 +761,9 @@ struct PoissonMinWaves {
                                                         : 1;
 };
 
-template <int N, bool NODAL>
+template <int N, bool NODAL, bool M16>
 __global__ void __launch_bounds__(CHAIN_BLOCK, (PoissonMinWaves<N, NODAL>::value))
-    k_poisson_apply(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
+    k_poisson_apply(const MapRef mref, const double* __restrict__ GP,
                     const double2* __restrict__ XG, const double* __restrict__ u,
                     double* __restrict__ y, int64_t c0, int64_t c1, int rounds, int accumulate,
                     const DEO<N> D, const WVec<N> w) {
@@ -734,7 +773,7 @@ __global__ void __launch_bounds__(CHAIN_BLOCK, (PoissonMinWaves<N, NODAL>::value
   __shared__ double carry[2][CHAIN_WAVES][1][N];
   const int64_t chain = c0 + xcd_block(blockIdx.x, gridDim.x);
   if (chain >= c1) return;  // uniform over the workgroup
-  const int wave = threadIdx.x / WAVE;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);  // provably uniform
   const int lane = threadIdx.x % WAVE;
   const int k = lane / N;
   const int j = lane - k * N;
@@ -750,11 +789,11 @@ __global__ void __launch_bounds__(CHAIN_BLOCK, (PoissonMinWaves<N, NODAL>::value
     uint32_t raw[N];
     double v[1][N], prev[N];
     if constexpr (NODAL)
-      poisson_group_nodal<N>(mapP, XG, u, g, lane, j, in_wave, L, LB, D, w, wj, raw, v[0], y,
-                             accumulate, prev);
+      poisson_group_nodal<N, M16>(mref, XG, u, g, lane, j, in_wave, L, LB, D, w, wj, raw, v[0],
+                                  y, accumulate, prev);
     else
-      poisson_group_stored<N>(mapP, GP, u, g, lane, j, in_wave, L, D, raw, v[0], y, accumulate,
-                              prev);
+      poisson_group_stored<N, M16>(mref, GP, u, g, lane, j, in_wave, L, D, raw, v[0], y,
+                                   accumulate, prev);
 #ifdef SEM_DIAG_NO_STORE
     if (in_wave && v[0][0] == 1234.5678) y[0] = v[0][1];  // timing-only
 #else

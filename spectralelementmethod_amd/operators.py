@@ -188,8 +188,8 @@ class SEMOperator(object):
 
     def plan_info(self):
         """Setup plan of the scatter (see include/sem_hip.h sem_plan_info)."""
-        info = (C.c_int64 * 18)()
-        _lib.check(self._lib.sem_plan_info(self._ctx, info, 18))
+        info = (C.c_int64 * 19)()
+        _lib.check(self._lib.sem_plan_info(self._ctx, info, 19))
         v = list(info)
         counts = [x for x in v[8:8 + v[5]]]
         while counts and counts[-1] == 0:
@@ -197,7 +197,8 @@ class SEMOperator(object):
         return dict(groups=v[0], zero_list=v[1], atomic_groups=v[2], conforming=bool(v[3]),
                     elements_per_group=v[4], colours=len(counts), rounds=v[6], slots=v[7],
                     chains_per_colour=counts,
-                    kernel="mfma" if v[17] == _lib.KERNEL_MFMA else "column")
+                    kernel="mfma" if v[17] == _lib.KERNEL_MFMA else "column",
+                    map_entry_bytes=v[18])
 
     # ------------------------------------------------------------------
     def compute_geometry(self, kind=POISSON, stream=None):

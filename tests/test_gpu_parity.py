@@ -151,6 +151,35 @@ def test_poisson_all_orders_vs_oracle(sem, gll, p):
     assert_parity(y, prob.apply(u), y_ext, TOL_ACTION)
 
 
+@pytest.mark.parametrize("geometry", GEOMETRY)
+@pytest.mark.parametrize("p,ney", [(8, 14), (8, 143), (4, 36), (6, 27)])
+def test_map16_matches_32bit_map(sem, gll, monkeypatch, p, ney, geometry):
+    """16-bit packed map (one base per group row) against the
+    32-bit map: the same arithmetic in the same order (the two kernel
+    instantiations may contract FMAs differently: agreement to 1e-14), both
+    within tolerance of the oracle.  ney = 143 at p = 8 makes ~5 % of the
+    groups wrap into the next element column: those read the 32-bit map
+    inside the same launch (per-group fallback)."""
+    import sem_oracle
+    from spectralelementmethod_amd import meshgen
+    nodes, e2n = meshgen.structured_square(max(6, ney // 4), ney, p, warp=0.05)
+    u = np.random.default_rng(p + ney).standard_normal(nodes.shape[1])
+    op16 = sem.SEMOperator(p, e2n, nodes, geometry=geometry)
+    assert op16.plan_info()["map_entry_bytes"] == 2
+    y16 = op16.apply(torch.from_numpy(u).cuda()).cpu().numpy()
+    monkeypatch.setenv("SEM_MAP16", "0")
+    op32 = sem.SEMOperator(p, e2n, nodes, geometry=geometry)
+    assert op32.plan_info()["map_entry_bytes"] == 4
+    y32 = op32.apply(torch.from_numpy(u).cuda()).cpu().numpy()
+    assert rel_l2(y16, y32) < 1e-14
+    ref = sem_oracle.PoissonProblem(nodes, e2n, gll["half_%d" % p]).apply(u)
+    # small elements: the oracle's float64 geometry (O(1) coordinates, as in
+    # the reference) loses digits; judge both against extended precision
+    y_ext = sem_oracle.poisson_apply_extended(nodes, e2n, gll["half_%d" % p], u)
+    assert_parity(y16, ref, y_ext, TOL_ACTION)
+    assert_parity(y32, ref, y_ext, TOL_ACTION)
+
+
 def test_properties_full_size(sem):
     """Size-independent properties on a 512 x 512 p = 8 mesh (16.8M DOF):
     constants in the kernel, symmetry, linearity, run-to-run agreement."""
