@@ -183,10 +183,7 @@ def main():
         for o in op.ops:
             o.set_reynolds(args.re)
     plan = op.plan_info()
-    if plan["kernel"] == "mfma":  # the MFMA kernel streams stored factors
-        geometry = "stored"
-    elif geometry == "auto":  # as resolved by the library (SEM_GEOM_AUTO)
-        geometry = "nodal" if p <= 8 else "stored"
+    geometry = plan["geometry"] if kind == POISSON else "stored"  # as the library resolved it
     log("rank %d: plan %s; %d interface + %d interior elements" % (
         rank, plan, op.n_iface_elem, op.n_interior_elem))
     n_elem_local = op.n_elem

@@ -127,13 +127,15 @@ int sem_set_map_shared(sem_ctx* ctx, const uint32_t* d_e2n, const uint8_t* d_nod
  * or SEM_KERNEL_MFMA), [18] bytes per packed map entry the Poisson column
  * kernel streams (2: 16-bit row offsets, used when every group row spans
  * < 4096 node ids; 4 otherwise; SEM_MAP16=0 in the environment forces 4).
- * Writes min(n_info, 19) values. */
+ * [19] the Poisson geometry mode the action uses (SEM_GEOM_NODAL or
+ * SEM_GEOM_STORED, AUTO resolved).  Writes min(n_info, 20) values. */
 int sem_plan_info(sem_ctx* ctx, int64_t* info, int n_info);
 
 /* How the Poisson action obtains its geometric factors.
- *  SEM_GEOM_AUTO (default): NODAL for p <= 8, STORED above (measured on
- *    MI355X at ~10^7 DOF: NODAL wins at p = 2, 4, 8, STORED at p = 12, 16
- *    where the nodal kernel's register demand halves occupancy).
+ *  SEM_GEOM_AUTO (default): NODAL for p = 1, 2, 4, 5, 8, STORED otherwise
+ *    (per-order MI355X sweep at ~10^7 DOF, DESIGN.md §7: STORED wins at
+ *    p = 3, 6, 7 and above 8, where the nodal kernel's register demand
+ *    halves occupancy).
  *  SEM_GEOM_NODAL: sem_geom_from_nodes keeps x_phys per global node
  *    (16 B/node) and the action re-derives J, det, invJ and detJxW at every
  *    quadrature node from it -- the reference's own order of work, which
@@ -159,7 +161,7 @@ int sem_set_geom_mode(sem_ctx* ctx, int mode);
  *    per element, no LDS); element-level colouring; stored factors only
  *    (a NODAL request is ignored); n = p + 1 <= 16 and dpn = 1, else
  *    SEM_E_NOTIMPL.
- *  SEM_KERNEL_AUTO (default): MFMA for 12 <= p <= 15 unless NODAL geometry
+ *  SEM_KERNEL_AUTO (default): MFMA for 13 <= p <= 15 unless NODAL geometry
  *    was requested, COLUMN otherwise (measured on MI355X, DESIGN.md §4.6;
  *    the threshold SEM_MFMA_MIN_N is a build knob).
  * The environment variable SEM_KERNEL (0/1/2) sets the initial value. */

@@ -357,18 +357,26 @@ void upload_deo(sem_ctx* c, hipError_t* err) {
 
 // the Poisson action recomputes its factors from x_phys per node (NODAL)
 // unless the stored-factor mode was chosen or the caller supplied factors
+// AUTO geometry of the column kernel, per order from the MI355X sweep at
+// ~1e7 DOF (profiles/r01c/geosweep): nodal at p = 2, 4, 5, 8
+// (and p = 1, unmeasured), stored factors at p = 3, 6, 7 and above 8
+bool auto_nodal_order(int n) { return n == 2 || n == 3 || n == 5 || n == 6 || n == 9; }
+
 bool nodal_mode(const sem_ctx* c) {
   if (c->mfma) return c->geom_mode == SEM_GEOM_NODAL;  // AUTO: stored factors
-  return c->geom_mode == SEM_GEOM_NODAL || (c->geom_mode == SEM_GEOM_AUTO && c->n <= 9);
+  return c->geom_mode == SEM_GEOM_NODAL ||
+         (c->geom_mode == SEM_GEOM_AUTO && auto_nodal_order(c->n));
 }
 
 // AUTO: the MFMA element kernel from SEM_MFMA_MIN_N nodes per line up,
 // Poisson only (dpn = 1), one 16 x 16 tile (n <= 16), and not when nodal
 // geometry was requested explicitly.  Measured on MI355X at ~1e7 DOF
-// (profiles/r01/mfma_v2): the MFMA kernel wins from p = 12
-// (n = 13) to p = 15, the column kernel up to p = 11.
+// (profiles/r01/mfma_v2, profiles/r01c/geosweep): after the
+// column kernel's latency work (4 waves, RMW prefetch, 16-bit map) it wins
+// up to p = 12 (0.139 vs 0.155 ms), the MFMA kernel from p = 13 (n = 14)
+// to p = 15.
 #ifndef SEM_MFMA_MIN_N
-#define SEM_MFMA_MIN_N 13
+#define SEM_MFMA_MIN_N 14
 #endif
 bool want_mfma(const sem_ctx* c) {
   if (c->dpn != 1 || c->n > 16) return false;
@@ -1044,13 +1052,14 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
 int sem_plan_info(sem_ctx* c, int64_t* info, int n_info) {
   if (!c || !info || n_info < 1) return fail(SEM_E_INVALID, "bad arguments");
   const int64_t nc = c->colour_start.empty() ? 0 : (int64_t)c->colour_start.size() - 1;
-  constexpr int NV = 8 + MAX_COLOURS + 1 + 1 + 1;
+  constexpr int NV = 8 + MAX_COLOURS + 1 + 1 + 1 + 1;
   int64_t vals[NV] = {c->n_groups, c->n_zero, c->n_atomic_groups, c->conforming ? 1 : 0,
                       c->epw,      nc,        c->rounds,          c->n_slots};
   for (int64_t q = 0; q < nc && q <= MAX_COLOURS; ++q)
     vals[8 + q] = c->colour_start[q + 1] - c->colour_start[q];
-  vals[NV - 2] = c->mfma ? SEM_KERNEL_MFMA : SEM_KERNEL_COLUMN;
-  vals[NV - 1] = c->map16 ? 2 : 4;  // bytes per packed map entry
+  vals[NV - 3] = c->mfma ? SEM_KERNEL_MFMA : SEM_KERNEL_COLUMN;
+  vals[NV - 2] = c->map16 ? 2 : 4;  // bytes per packed map entry
+  vals[NV - 1] = nodal_mode(c) ? SEM_GEOM_NODAL : SEM_GEOM_STORED;  // Poisson geometry
   for (int i = 0; i < n_info && i < NV; ++i) info[i] = vals[i];
   return SEM_OK;
 }

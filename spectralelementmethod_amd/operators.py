@@ -91,7 +91,7 @@ class SEMOperator(object):
         How the Poisson action gets its geometric factors: re-derived per
         quadrature node from x_phys per global node ("nodal", least HBM
         traffic) or streamed from precomputed per-element factors ("stored");
-        "auto" (default) picks nodal for p <= 8.  See include/sem_hip.h
+        "auto" (default) picks per order (nodal at p = 1, 2, 4, 5, 8).  See include/sem_hip.h
         sem_set_geom_mode.
     kernel : {"auto", "column", "mfma"}
         Kernel family of the Poisson action: the LDS column kernel or the
@@ -188,8 +188,8 @@ class SEMOperator(object):
 
     def plan_info(self):
         """Setup plan of the scatter (see include/sem_hip.h sem_plan_info)."""
-        info = (C.c_int64 * 19)()
-        _lib.check(self._lib.sem_plan_info(self._ctx, info, 19))
+        info = (C.c_int64 * 20)()
+        _lib.check(self._lib.sem_plan_info(self._ctx, info, 20))
         v = list(info)
         counts = [x for x in v[8:8 + v[5]]]
         while counts and counts[-1] == 0:
@@ -198,7 +198,8 @@ class SEMOperator(object):
                     elements_per_group=v[4], colours=len(counts), rounds=v[6], slots=v[7],
                     chains_per_colour=counts,
                     kernel="mfma" if v[17] == _lib.KERNEL_MFMA else "column",
-                    map_entry_bytes=v[18])
+                    map_entry_bytes=v[18],
+                    geometry="nodal" if v[19] == _lib.GEOM_NODAL else "stored")
 
     # ------------------------------------------------------------------
     def compute_geometry(self, kind=POISSON, stream=None):

@@ -376,9 +376,15 @@ def test_poisson_all_orders_mfma(sem, gll, p, geometry):
 
 def test_mfma_auto_selection_and_limits(sem, poisson_action):
     from spectralelementmethod_amd import meshgen
-    for p, expect in ((8, "column"), (11, "column"), (12, "mfma"), (15, "mfma"), (16, "column")):
+    for p, expect in ((8, "column"), (11, "column"), (12, "column"), (13, "mfma"), (15, "mfma"),
+                      (16, "column")):
         nodes, e2n = meshgen.structured_square(3, 2, p)
         assert sem.SEMOperator(p, e2n, nodes).plan_info()["kernel"] == expect, p
+    # AUTO geometry per order (the column kernel's measured table)
+    for p, expect in ((2, "nodal"), (3, "stored"), (4, "nodal"), (7, "stored"), (8, "nodal"),
+                      (12, "stored")):
+        nodes, e2n = meshgen.structured_square(3, 2, p)
+        assert sem.SEMOperator(p, e2n, nodes).plan_info()["geometry"] == expect, p
     # nodal geometry requested explicitly keeps the column kernel under auto
     nodes, e2n = meshgen.structured_square(3, 2, 12)
     assert sem.SEMOperator(12, e2n, nodes, geometry="nodal").plan_info()["kernel"] == "column"
