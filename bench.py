@@ -1,70 +1,84 @@
 #!/usr/bin/env python
 """Benchmark: global Poisson stiffness action, DOF-updates/s (BASELINE.json
 metric), on synthetic structured quad meshes of order p, elements split in
-column strips across ranks (one process per GPU, weak scaling: every rank owns
-nex x ney elements).
+column strips across ranks (one process per GPU).
 
-A step = one global action y = K u over one batch of synthetic input:
-  sem_zero_shared(y) -> sem_apply (the element kernel) -> interface sum with
-  the neighbouring ranks (RCCL point-to-point; nothing at N = 1).
-Inputs are resident in HBM before the timed region.
+A step = one global action y = K u over one batch of synthetic input: the
+element kernels and, with several ranks, the interface sum with the
+neighbouring ranks (RCCL send/recv over xGMI, hidden behind the interior
+elements; csrc/sem_dd.hip).  Inputs are resident in HBM before the timed
+region.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--p 8] [--nex 1024] [--ney 1024]
+                  [--scaling strong|weak] [--op poisson|axisym_stokes|axisym_ns|pcg]
+
+--gpus N without a launcher: this process starts N rank processes (before
+touching the GPU) and waits for them; under torchrun (WORLD_SIZE set) each
+process is one rank.  --scaling strong (default): the nex x ney mesh is the
+GLOBAL mesh split into N strips (BASELINE config 3: 1024 x 1024 over 8
+GPUs); weak: every rank owns nex x ney elements.
 
 Rank 0 prints ONE JSON line (the driver's contract) with a ``roofline``
-object for the element kernel (algorithmic bytes / HIP-event kernel time,
-SURVEY.md §8(d)) and, at N = 1, a ``cpu_baseline`` object (the NumPy oracle
-of the reference path timed on this host's cores on a bounded sample).
+object for the element kernel (algorithmic bytes of SURVEY.md §8(d) / HIP
+event time on the launch stream), a ``parity`` spot check of the timed
+output against the NumPy oracle, and, at N = 1, a ``cpu_baseline`` object
+(the oracle of the reference path timed on this host's cores on bounded
+samples, in a child process with OMP_NUM_THREADS pinned).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 import numpy as np
-import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from spectralelementmethod_amd import _lib  # noqa: E402
-from spectralelementmethod_amd.distributed import StripPartition, OverlappedOperator  # noqa: E402
-from spectralelementmethod_amd.operators import POISSON, AXISYM_STOKES, AXISYM_NS  # noqa: E402
-
 METRIC = "global stiffness-action DOF-updates/s (and % HBM roofline), Poisson p=8"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FP64_PEAK_TFLOPS = 78.6  # MI355X vector fp64 (256 CUs x 128 FLOP/clk x 2.4 GHz)
-# PMC-measured HBM bytes of the headline workload, per geometry mode
+# PMC-measured HBM bytes of the headline workload (tools/gpu_profile.sh +
+# tools/pmc_traffic.py), per geometry mode
 DEFAULT_TRAFFIC = {"stored": "r01/pmc_traffic_p8_1024x1024.json",
-                   "nodal": "r01c/pmc_traffic_nodal_p8_1024x1024.json"}
+                   "nodal": "r02/pmc_traffic_nodal_p8_1024x1024.json"}
 
 
 def log(msg):
     print("[bench] " + msg, file=sys.stderr, flush=True)
 
 
-def alg_bytes(kind, ndof_nodes, n_elem, p, geometry="stored", map_bytes=4):
-    """Poisson with stored factors B = 16*ndof + 28*E*(p+1)^2
-    (u read, y written, 3 fp64 factors + one uint32 map entry per local
-    node); with nodal geometry the factors are replaced by x_phys per global
-    node: B = 32*ndof + 4*E*(p+1)^2; axisymmetric B = 32*n_nodes +
-    60*E*(p+1)^2 (Navier-Stokes residual: 9 factors, 76*E*(p+1)^2).
-    map_bytes = 2: the column kernel streams 16-bit map entries plus one
-    uint32 base per group row (4*(p+1) bytes per floor(64/(p+1)) elements)."""
+# ---------------------------------------------------------------- byte models
+def alg_bytes_s8d(kind, n_nodes, n_elem, p):
+    """SURVEY.md §8(d), the problem's algorithmic bytes: Poisson
+    B = 16*ndof + 28*E*(p+1)^2 (u read once, y written once, 3 fp64 geometric
+    factors + one uint32 map entry per element node); axisymmetric
+    B = 32*n_nodes + 60*E*(p+1)^2 (Navier-Stokes residual: 9 factors, 76)."""
+    n2 = (p + 1) ** 2
+    if kind == "poisson":
+        return 16 * n_nodes + 28 * n_elem * n2
+    if kind == "axisym_ns":
+        return 32 * n_nodes + 76 * n_elem * n2
+    return 32 * n_nodes + 60 * n_elem * n2
+
+
+def streamed_bytes(kind, n_nodes, n_elem, p, geometry, map_bytes):
+    """The least the kernel as built must stream: with NODAL geometry the
+    factors are replaced by x_phys per global node (16 B) gathered like u;
+    map_bytes = 2: 16-bit packed map plus one uint32 base per group row."""
     n = p + 1
     n2 = n * n
-    if kind == POISSON:
-        m = map_bytes * n_elem * n2
-        if map_bytes == 2:
-            m += 4 * n * n_elem // (64 // n)
-        if geometry == "nodal":
-            return 32 * ndof_nodes + m
-        return 16 * ndof_nodes + 24 * n_elem * n2 + m
-    if kind == AXISYM_NS:
-        return 32 * ndof_nodes + 76 * n_elem * n2
-    return 32 * ndof_nodes + 60 * n_elem * n2
+    if kind != "poisson":
+        return alg_bytes_s8d(kind, n_nodes, n_elem, p)
+    m = map_bytes * n_elem * n2
+    if map_bytes == 2:
+        m += 4 * n * n_elem // (64 // n)
+    if geometry == "nodal":
+        return 32 * n_nodes + m
+    return 16 * n_nodes + 24 * n_elem * n2 + m
 
 
 def alg_flops(kind, n_elem, p, geometry="stored"):
@@ -72,97 +86,237 @@ def alg_flops(kind, n_elem, p, geometry="stored"):
     plus pointwise work; nodal geometry adds the four derivatives of x_phys
     and the per-node det / inverse / detJxW (15 n^2 incl. one division)."""
     n = p + 1
-    if kind == POISSON:
+    if kind == "poisson":
         extra = 8 * n ** 3 + 15 * n ** 2 if geometry == "nodal" else 0
         return n_elem * (8 * n ** 3 + 7 * n ** 2 + extra)
-    return n_elem * (16 * n ** 3 + (30 if kind == AXISYM_NS else 22) * n ** 2)
+    return n_elem * (16 * n ** 3 + (30 if kind == "axisym_ns" else 22) * n ** 2)
 
 
-def cpu_baseline(p, warp, budget_s=20.0):
-    """Reference path on the host: the NumPy oracle (oracle/sem_oracle.py),
-    single-threaded.  (1) reference-faithful: per-element precomputed dense
-    Lse (examples/poisson.py:168-193) applied with einsum('pqrs,rs') +
-    np.add.at (squirmer-axisymmetric.py:286), on a 64 x 64 sample of the
-    same p / warp; (2) batched sum-factorised NumPy on 256 x 256 (config 2)."""
+# ---------------------------------------------------------------- CPU baseline
+def _faithful_worker(args):
+    """One worker of the multi-process reference-faithful action: builds the
+    dense Lse of its element slice, then times its per-element einsum +
+    np.add.at passes (after a barrier shared with the other workers)."""
+    p, nex, warp, w, nw, reps, barrier = args
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import sem_oracle
+    from spectralelementmethod_amd import meshgen
+    gll = np.load(os.path.join(ROOT, "tests", "golden", "gll.npz"))
+    nodes, e2n = meshgen.structured_square(nex, nex, p, warp=warp)
+    prob = sem_oracle.PoissonProblem(nodes, e2n, gll["half_%d" % p], batched_geometry=True)
+    E = e2n.shape[0]
+    sl = np.arange(w * E // nw, (w + 1) * E // nw)
+    Lse = prob.element_matrices(sl)
+    u = np.random.default_rng(0).standard_normal(prob.ndof)
+    sem_oracle.apply_element_matrices(Lse, prob.e2n[sl], u, prob.ndof)  # warm-up
+    ts = []
+    for _ in range(reps):
+        barrier.wait()
+        t0 = time.perf_counter()
+        sem_oracle.apply_element_matrices(Lse, prob.e2n[sl], u, prob.ndof)
+        ts.append(time.perf_counter() - t0)
+    return ts
+
+
+def cpu_baseline(p, warp, budget_s=20.0, workers=16):
+    """The reference path on this host (oracle/sem_oracle.py restates it;
+    BASELINE.md §3), OMP_NUM_THREADS pinned to 1 per process:
+    (1) reference-faithful per-element dense Lse (examples/poisson.py:168-193)
+        applied with einsum('pqrs,rs') + np.add.at (squirmer:286), one
+        process on 64 x 64, and `workers` processes on 128 x 128 (elements
+        split evenly, partial vectors summed; the sum is timed too);
+    (2) batched element-matrix (einsum + bincount) on 64 x 64;
+    (3) batched sum-factorised NumPy on 256 x 256 (config 2)."""
+    import multiprocessing as mp
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import sem_oracle
     from spectralelementmethod_amd import meshgen
     gll = np.load(os.path.join(ROOT, "tests", "golden", "gll.npz"))
     half = gll["half_%d" % p]
     out = {}
+
+    def timed(fn, min_reps=3, max_reps=20, budget=budget_s / 4):
+        fn()
+        ts, t_start = [], time.perf_counter()
+        while len(ts) < min_reps or (time.perf_counter() - t_start < budget and len(ts) < max_reps):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts)), len(ts)
+
     nodes, e2n = meshgen.structured_square(64, 64, p, warp=warp)
-    prob = sem_oracle.PoissonProblem(nodes, e2n, half, batched_geometry=True)
     t0 = time.perf_counter()
+    prob = sem_oracle.PoissonProblem(nodes, e2n, half, batched_geometry=True)
     Lse = prob.element_matrices()
     t_setup = time.perf_counter() - t0
     u = np.random.default_rng(0).standard_normal(prob.ndof)
-    sem_oracle.apply_element_matrices(Lse, prob.e2n, u, prob.ndof)  # warm-up
-    reps, ts = 0, []
-    t_start = time.perf_counter()
-    while reps < 3 or (time.perf_counter() - t_start < budget_s / 3 and reps < 20):
-        t0 = time.perf_counter()
-        sem_oracle.apply_element_matrices(Lse, prob.e2n, u, prob.ndof)
-        ts.append(time.perf_counter() - t0)
-        reps += 1
-    t_faith = float(np.median(ts))
-    out["faithful"] = dict(ndof=prob.ndof, n_elem=e2n.shape[0], sec_per_action=t_faith,
-                           dof_per_s=prob.ndof / t_faith, setup_sec=t_setup, reps=reps)
+    t1, r1 = timed(lambda: sem_oracle.apply_element_matrices(Lse, prob.e2n, u, prob.ndof))
+    out["faithful_1"] = dict(ndof=prob.ndof, n_elem=e2n.shape[0], sec_per_action=t1,
+                             dof_per_s=prob.ndof / t1, reps=r1,
+                             setup_sec_per_elem=t_setup / e2n.shape[0])
+    t2, r2 = timed(lambda: sem_oracle.apply_element_matrices_batched(Lse, prob.e2n, u, prob.ndof))
+    out["batched_elem_matrix"] = dict(ndof=prob.ndof, sec_per_action=t2, dof_per_s=prob.ndof / t2,
+                                      reps=r2)
     del Lse
     nodes, e2n = meshgen.structured_square(256, 256, p, warp=warp)
     prob = sem_oracle.PoissonProblem(nodes, e2n, half, batched_geometry=True)
     u = np.random.default_rng(0).standard_normal(prob.ndof)
-    prob.apply(u)
-    ts = []
-    for _ in range(3):
-        t0 = time.perf_counter()
-        prob.apply(u)
-        ts.append(time.perf_counter() - t0)
-    t_b = float(np.median(ts))
-    out["batched_sumfact"] = dict(ndof=prob.ndof, n_elem=e2n.shape[0], sec_per_action=t_b,
-                                  dof_per_s=prob.ndof / t_b)
+    t3, r3 = timed(lambda: prob.apply(u), max_reps=5)
+    out["batched_sumfact"] = dict(ndof=prob.ndof, sec_per_action=t3, dof_per_s=prob.ndof / t3,
+                                  reps=r3)
+    # (1) on `workers` processes
+    nw = max(1, min(workers, os.cpu_count() or 1))
+    nex_mp = 128
+    reps = 5
+    ctx = mp.get_context("fork")
+    barrier = ctx.Manager().Barrier(nw)
+    with ctx.Pool(nw) as pool:
+        res = pool.map(_faithful_worker, [(p, nex_mp, warp, w, nw, reps, barrier)
+                                          for w in range(nw)])
+    t_max = [max(r[k] for r in res) for k in range(reps)]
+    ndof_mp = (nex_mp * p + 1) ** 2
+    parts = [np.random.default_rng(w).standard_normal(ndof_mp) for w in range(nw)]
+    t0 = time.perf_counter()
+    np.add.reduce(parts)
+    t_sum = time.perf_counter() - t0
+    t_mp = float(np.median(t_max)) + t_sum
+    out["faithful_mp"] = dict(ndof=ndof_mp, n_elem=nex_mp * nex_mp, workers=nw,
+                              sec_per_action=t_mp, dof_per_s=ndof_mp / t_mp, reps=reps)
     return out
 
 
+# ---------------------------------------------------------------- launcher
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """Start n rank processes of this script (before any GPU call here) and
+    wait for them; rank 0 prints the JSON line."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    for pr in procs:
+        rc = max(rc, abs(pr.wait()))
+    return rc
+
+
+# ---------------------------------------------------------------- parity spot check
+def parity_spot_check(op, y, u, part, p, warp, cols=2):
+    """Recompute the action on a block of `cols` element columns in the
+    middle of this rank's strip with the NumPy oracle (float64) and compare
+    with the timed output on the block's inner nodes (its left/right node
+    lines also receive contributions from outside the block)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import sem_oracle
+    from spectralelementmethod_amd import meshgen
+    gll = np.load(os.path.join(ROOT, "tests", "golden", "gll.npz"))
+    ncol = part.ex1 - part.ex0
+    cols = min(cols, ncol)
+    c0 = part.ex0 + (ncol - cols) // 2
+    nodes, e2n, off = meshgen.structured_strip(part.nex, part.ney, p, c0, c0 + cols, warp)
+    loc = off - part.node_offset + np.arange(nodes.shape[1])
+    u_sub = u[torch_index(loc, u.device)].cpu().numpy()
+    y_ref = sem_oracle.PoissonProblem(nodes, e2n, gll["half_%d" % p],
+                                      batched_geometry=True).apply(u_sub)
+    Ny = part.Ny
+    inner = np.arange(Ny, nodes.shape[1] - Ny)
+    y_gpu = y[torch_index(loc[inner], y.device)].cpu().numpy()
+    ref = y_ref[inner]
+    return dict(rel_l2=float(np.linalg.norm(y_gpu - ref) / np.linalg.norm(ref)),
+                nodes_checked=int(inner.size),
+                block="element columns [%d, %d) x %d rows" % (c0, c0 + cols, part.ney))
+
+
+def torch_index(a, device):
+    import torch
+    return torch.from_numpy(np.asarray(a, dtype=np.int64)).to(device)
+
+
+# ---------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--p", type=int, default=8)
-    ap.add_argument("--nex", type=int, default=1024, help="element columns per rank")
+    ap.add_argument("--nex", type=int, default=1024,
+                    help="element columns of the global mesh (strong) or per rank (weak)")
     ap.add_argument("--ney", type=int, default=1024)
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--warp", type=float, default=0.05)
-    ap.add_argument("--op", choices=["poisson", "axisym_stokes", "axisym_ns"], default="poisson")
+    ap.add_argument("--op", choices=["poisson", "axisym_stokes", "axisym_ns", "pcg"],
+                    default="poisson")
     ap.add_argument("--re", type=float, default=10.0, help="Reynolds number for --op axisym_ns")
     ap.add_argument("--geometry", choices=["auto", "nodal", "stored"], default="auto",
                     help="Poisson geometric factors: re-derived from x_phys per node, or "
-                         "streamed; auto = nodal for p <= 8 (the library's default)")
+                         "streamed; auto = the library's per-order choice")
     ap.add_argument("--kernel", choices=["auto", "column", "mfma"], default="auto",
                     help="Poisson kernel family: LDS column kernel or fp64-MFMA element kernel; "
                          "auto = the library's measured choice")
+    ap.add_argument("--transport", choices=["auto", "rccl", "torch"], default="auto",
+                    help="interface sum with several ranks: native RCCL or torch.distributed")
+    ap.add_argument("--pcg-rtol", type=float, default=0.0,
+                    help="--op pcg: 0 = time exactly --steps iterations; > 0 = solve to it")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true",
-                    help="skip the finiteness check (timing-only diagnostic builds)")
+                    help="skip the parity spot check (timing-only diagnostic builds)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--cpu-workers", type=int, default=16)
+    ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="diagnostic: every rank on cuda:0, gloo process group, torch transport "
+                         "(exercises the multi-rank flow on a one-GPU box; timings meaningless)")
     ap.add_argument("--traffic-json", default=None,
                     help="JSON with PMC-measured HBM bytes per launch (profiles/)")
     args = ap.parse_args()
+
+    if args.cpu_baseline_only:  # child process: no GPU
+        print(json.dumps(cpu_baseline(args.p, args.warp, args.cpu_budget, args.cpu_workers)))
+        return 0
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus)
+
+    import torch
+    import torch.distributed as dist
+    from spectralelementmethod_amd import _lib  # noqa: F401
+    from spectralelementmethod_amd.distributed import StripPartition, OverlappedOperator
+    from spectralelementmethod_amd.operators import POISSON, AXISYM_STOKES, AXISYM_NS
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+    if args.rehearse_one_gpu:
+        local_rank = 0
+        args.transport = "torch"
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.rehearse_one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("cpu:gloo,cuda:nccl", device_id=dev)
         dist.barrier()
 
-    kind = {"poisson": POISSON, "axisym_stokes": AXISYM_STOKES, "axisym_ns": AXISYM_NS}[args.op]
+    opname = args.op
+    kind = {"poisson": POISSON, "pcg": POISSON, "axisym_stokes": AXISYM_STOKES,
+            "axisym_ns": AXISYM_NS}[opname]
+    kname = "poisson" if kind == POISSON else opname
     dpn = 1 if kind == POISSON else 2
     p = args.p
-    nex_global = args.nex * world
+    nex_global = args.nex * world if args.scaling == "weak" else args.nex
     part = StripPartition(nex_global, args.ney, p, world, rank, dofs_per_node=dpn)
     t0 = time.time()
     if kind == POISSON:
@@ -172,33 +326,38 @@ def main():
         if world != 1:
             raise SystemExit("axisymmetric bench is single-GPU")
         nodes, e2n = meshgen.annulus(args.nex, args.ney, p)
+    t_mesh = time.time() - t0
     log("rank %d: mesh %d elements, %d nodes (%.1fs)" % (rank, e2n.shape[0], nodes.shape[1],
-                                                          time.time() - t0))
+                                                          t_mesh))
     geometry = args.geometry if kind == POISSON else "stored"
-    # interface elements first, RCCL interface sum on a side stream while the
-    # interior elements run (one plain operator when there is no neighbour)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
     op = OverlappedOperator(p, nodes, e2n, part.neighbors if world > 1 else {}, dpn, dev,
-                            geometry=geometry, kind=kind, kernel=args.kernel)
+                            geometry=geometry, kind=kind, kernel=args.kernel, owned=part.owned,
+                            transport=args.transport, world=world, rank=rank)
+    torch.cuda.synchronize()
+    t_setup = time.perf_counter() - t0
     if kind == AXISYM_NS:
         for o in op.ops:
             o.set_reynolds(args.re)
     plan = op.plan_info()
     geometry = plan["geometry"] if kind == POISSON else "stored"  # as the library resolved it
-    log("rank %d: plan %s; %d interface + %d interior elements" % (
-        rank, plan, op.n_iface_elem, op.n_interior_elem))
+    log("rank %d: plan %s; %d interface + %d interior elements; transport %s; setup %.2fs" % (
+        rank, plan, op.n_iface_elem, op.n_interior_elem, op.transport, t_setup))
     n_elem_local = op.n_elem
-    del nodes, e2n
-    log("rank %d: operator ready (%.1fs)" % (rank, time.time() - t0))
+    n_nodes_local = op.ndof // dpn
+    ndof_global = part.global_nodes * dpn if kind == POISSON else op.ndof
 
-    g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    u = torch.randn(op.ndof, dtype=torch.float64, device=dev, generator=g)
+    if opname == "pcg":
+        return bench_pcg(args, op, part, nodes, dev, world, rank, ndof_global, t_setup)
+    del nodes, e2n
+
+    # u from one global field so shared DOFs agree on both sides of an interface
+    u = global_random_field(part, dpn, kind, op.ndof, dev)
     y = torch.empty_like(u)
 
-    def step(ev=None):
-        op.step(u, y, ev)
-
     for _ in range(args.warmup):
-        step()
+        op.step(u, y)
     torch.cuda.synchronize()
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps)]
@@ -207,44 +366,45 @@ def main():
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for k in range(args.steps):
-        step(events[k])
+        op.step(u, y, events[k])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     kern_ms = [a.elapsed_time(b) for a, b in events]
+    per_rank_ms = [elapsed / args.steps * 1e3]
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
+        gathered = [None] * world
+        dist.all_gather_object(gathered, per_rank_ms[0])
+        per_rank_ms = gathered
     kern_avg_s = float(np.mean(kern_ms)) / 1e3
 
-    # correctness spot check of the timed output (cheap, outside the timing):
-    # y must be finite and u.Ku > 0 on this rank's block
-    assert args.no_check or torch.isfinite(y).all().item()
+    parity = None
+    if not args.no_check:
+        assert torch.isfinite(y).all().item(), "non-finite output"
+        if kind == POISSON:
+            parity = parity_spot_check(op, y, u, part, p, args.warp)
+            log("rank %d: parity spot check %s" % (rank, parity))
+            assert parity["rel_l2"] < 1e-10, parity
 
-    n_nodes_local = op.ndof // dpn
-    ndof_global = part.global_nodes * dpn if kind == POISSON else op.ndof
     value = ndof_global * args.steps / elapsed
     map_bytes = plan.get("map_entry_bytes", 4) if (plan["kernel"] == "column"
                                                   and kind == POISSON) else 4
-    # algorithmic bytes keep SURVEY.md §8(d)'s uint32 map (the problem's
-    # input); the bytes the kernel streams with a 16-bit packed map are
-    # reported beside them
-    B = alg_bytes(kind, n_nodes_local, n_elem_local, p, geometry)
-    B_stream = alg_bytes(kind, n_nodes_local, n_elem_local, p, geometry, map_bytes)
-    F = alg_flops(kind, n_elem_local, p, geometry)
+    B = alg_bytes_s8d(kname, n_nodes_local, n_elem_local, p)
+    B_stream = streamed_bytes(kname, n_nodes_local, n_elem_local, p, geometry, map_bytes)
+    F = alg_flops(kname, n_elem_local, p, geometry)
     achieved = B / kern_avg_s / 1e9
-    traffic = None
-    traffic_src = args.traffic_json
-    if (traffic_src is None and kind == POISSON and plan["kernel"] == "column"
+    traffic, traffic_src = None, args.traffic_json
+    if (traffic_src is None and kind == POISSON and plan["kernel"] == "column" and world == 1
             and (p, args.nex, args.ney) == (8, 1024, 1024)):
-        # PMC measurement of this workload (separate FETCH_SIZE / WRITE_SIZE
-        # passes, tools/gpu_profile.sh + tools/pmc_traffic.py)
         traffic_src = os.path.join(ROOT, "profiles", DEFAULT_TRAFFIC[geometry])
     if traffic_src and os.path.exists(traffic_src):
         with open(traffic_src) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
+    headline = (args.nex, args.ney, p) == (1024, 1024, 8)
     result = {
         "metric": METRIC if kind == POISSON else METRIC.replace(
             "Poisson p=8", ("axisymmetric Stokes p=%d" if kind == AXISYM_STOKES else
@@ -256,54 +416,176 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (structured warped quad mesh, u ~ N(0,1))",
         "config": {
-            "workload": "%s p=%d, %dx%d elements per GPU (%s)" % (
-                args.op, p, args.nex, args.ney,
-                "10^6-element north-star mesh" if (args.nex, args.ney, p) == (1024, 1024, 8)
-                else "custom"),
-            "p": p, "geometry": geometry, "n_elem_per_gpu": n_elem_local, "ndof_global": ndof_global,
-            "ndof_per_gpu": op.ndof, "parallelism": "element column strips x%d, RCCL P2P "
-                                                    "interface sum overlapped with interior "
-                                                    "elements" % world if world > 1 else
+            "workload": "%s p=%d, %dx%d elements %s (%s)" % (
+                opname, p, args.nex, args.ney,
+                "global mesh in %d strip(s)" % world if args.scaling == "strong"
+                else "per GPU", "BASELINE config 3, the 10^6-element north-star mesh"
+                if headline and args.scaling == "strong" else "custom"),
+            "p": p, "geometry": geometry, "ranks_seen": world,
+            "n_elem_global": part.nex * part.ney if kind == POISSON else n_elem_local,
+            "n_elem_per_gpu": n_elem_local, "ndof_global": ndof_global,
+            "ndof_per_gpu": op.ndof,
+            "parallelism": ("element column strips x%d; interface elements on a side stream, "
+                            "RCCL send/recv interface sum overlapped with the interior elements "
+                            "(transport %s)" % (world, op.transport)) if world > 1 else
             "single GPU",
+            "per_rank_ms_per_step": per_rank_ms,
+            "exchange_bytes_per_step_per_rank": 2 * op.exchange_bytes,
+            "interface_elements": op.n_iface_elem,
             "kernel_ms_avg": kern_avg_s * 1e3, "kernel_ms_min": float(np.min(kern_ms)),
             "gflops_kernel": F / kern_avg_s / 1e9,
             "kernel_family": plan["kernel"], "map_entry_bytes": map_bytes,
-            "scatter_plan": {k: plan[k] for k in ("colours", "chains_per_colour", "rounds", "zero_list",
-                                                  "atomic_groups")},
+            "gpu_setup_sec": t_setup, "gpu_setup_sec_per_elem": t_setup / max(1, n_elem_local),
+            "scatter_plan": {k: plan[k] for k in ("colours", "chains_per_colour", "rounds",
+                                                  "zero_list", "atomic_groups")},
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "kernel": ("k_poisson_mfma<%d>" if plan["kernel"] == "mfma" else "k_poisson_apply<%d>")
-                      % (p + 1) if kind == POISSON else "k_axisym_apply<%d>" % (p + 1),
-            "alg_bytes_per_launch": B, "streamed_bytes_per_launch": B_stream,
+            "bytes_model": "SURVEY.md §8(d): 16*ndof + 28*E*(p+1)^2" if kind == POISSON else
+            "SURVEY.md §8(d) axisymmetric: 32*n_nodes + (60|76)*E*(p+1)^2",
+            "alg_bytes_per_launch": B,
+            "streamed_bytes_per_launch": B_stream,
+            "frac_streamed_min": B_stream / kern_avg_s / 1e9 / HBM_PEAK_GBS,
+            "kernel": (("k_poisson_mfma<%d>" if plan["kernel"] == "mfma" else
+                        "k_poisson_apply<%d>") % (p + 1) if kind == POISSON else
+                       "k_axisym_apply<%d>" % (p + 1)),
+            "launch": ("one sem_apply = %d colour launches" % plan["colours"]) if world == 1 else
+            "one sem_dd_apply (interface + interior elements + exchange), per rank",
             "fp64_tflops": F / kern_avg_s / 1e12, "fp64_peak_tflops": FP64_PEAK_TFLOPS,
-            "launch": "one sem_apply = %d colour launches" % plan["colours"],
             "traffic_source": os.path.relpath(traffic_src, ROOT) if traffic is not None else None,
         },
     }
+    if parity is not None:
+        result["parity"] = parity
     if rank == 0 and world == 1 and not args.no_cpu_baseline and kind == POISSON:
-        log("timing CPU baseline (NumPy oracle, 1 thread)...")
-        cb = cpu_baseline(p, args.warp, args.cpu_budget)
+        log("timing CPU baseline (NumPy oracle of the reference path, child process)...")
+        env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1",
+                   MKL_NUM_THREADS="1")
+        out = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-baseline-only",
+                              "--p", str(p), "--warp", str(args.warp), "--cpu-budget",
+                              str(args.cpu_budget), "--cpu-workers", str(args.cpu_workers)],
+                             env=env, capture_output=True, text=True, check=True)
+        cb = json.loads(out.stdout.strip().splitlines()[-1])
+        f1, fm = cb["faithful_1"], cb["faithful_mp"]
         result["cpu_baseline"] = {
-            "value": cb["faithful"]["dof_per_s"], "unit": "DOF/s", "cores": 1, "kind": "port",
-            "sample": "reference-faithful per-element Lse einsum + np.add.at, 64x64 p=%d warped "
-                      "(%d DOF), median of %d; host os.cpu_count()=%d" % (
-                          p, cb["faithful"]["ndof"], cb["faithful"]["reps"], os.cpu_count()),
-            "batched_sumfact_dof_per_s": cb["batched_sumfact"]["dof_per_s"],
+            "value": fm["dof_per_s"], "unit": "DOF/s", "cores": fm["workers"], "kind": "port",
+            "sample": "reference-faithful per-element Lse einsum('pqrs,rs') + np.add.at "
+                      "(examples/poisson.py:168-193, squirmer:286), %d processes x "
+                      "OMP_NUM_THREADS=1 over a 128x128 p=%d warped mesh (%d DOF), element "
+                      "slices summed; median of %d; host os.cpu_count()=%d" % (
+                          fm["workers"], p, fm["ndof"], fm["reps"], os.cpu_count()),
+            "faithful_1thread_dof_per_s": f1["dof_per_s"],
+            "faithful_1thread_sample": "64x64 p=%d (%d DOF), median of %d" % (p, f1["ndof"],
+                                                                               f1["reps"]),
+            "batched_elem_matrix_1thread_dof_per_s": cb["batched_elem_matrix"]["dof_per_s"],
+            "batched_sumfact_1thread_dof_per_s": cb["batched_sumfact"]["dof_per_s"],
             "batched_sumfact_sample": "256x256 p=%d (%d DOF)" % (p, cb["batched_sumfact"]["ndof"]),
-            "faithful_setup_sec_per_elem": cb["faithful"]["setup_sec"] / cb["faithful"]["n_elem"],
+            "faithful_setup_sec_per_elem": f1["setup_sec_per_elem"],
+            "gpu_setup_sec_per_elem": t_setup / max(1, n_elem_local),
         }
     if rank == 0:
         print(json.dumps(result), flush=True)
+    op.close()
     if world > 1:
         dist.destroy_process_group()
+    return 0
+
+
+def global_random_field(part, dpn, kind, ndof, dev):
+    """u ~ N(0,1) drawn per GLOBAL node id (counter-based, so every rank
+    draws the same value for a shared node): Philox via torch on the device."""
+    import torch
+    if kind != 0:
+        g = torch.Generator(device=dev).manual_seed(1234)
+        return torch.randn(ndof, dtype=torch.float64, device=dev, generator=g)
+    # the strip's nodes are the contiguous global range [node_offset, +n_nodes)
+    g = torch.Generator(device=dev).manual_seed(1234)
+    n_glob = part.global_nodes
+    lo = part.node_offset
+    # draw the global vector in chunks, keep the rank's window (cheap at 67M)
+    out = torch.empty(ndof, dtype=torch.float64, device=dev)
+    chunk = 1 << 24
+    pos = 0
+    while pos < n_glob:
+        m = min(chunk, n_glob - pos)
+        v = torch.randn(m, dtype=torch.float64, device=dev, generator=g)
+        a, b = max(pos, lo), min(pos + m, lo + ndof)
+        if a < b:
+            out[a - lo:b - lo] = v[a - pos:b - pos]
+        pos += m
+    return out
+
+
+def bench_pcg(args, op, part, nodes, dev, world, rank, ndof_global, t_setup):
+    """Assembled Poisson solve (DOFManagerSC.solve,
+    sem/discrete.py:502-528) by device-resident Jacobi-PCG.  Manufactured
+    problem: x* = sin(pi x/2) cos(pi y/2) + x y at the nodes, b = K x*
+    (computed by the same distributed operator, so shared DOFs agree),
+    Dirichlet x = x* on the square's boundary, x0 = 0 inside.  --pcg-rtol 0:
+    a step = one PCG iteration (iterations/s); else solve to the tolerance
+    and report time to solution and the error against x*."""
+    import torch
+    import torch.distributed as dist
+    x_n, y_n = torch.from_numpy(nodes[0]).to(dev), torch.from_numpy(nodes[1]).to(dev)
+    xs = torch.sin(0.5 * np.pi * x_n) * torch.cos(0.5 * np.pi * y_n) + x_n * y_n
+    on = (torch.abs(x_n.abs() - 1) < 1e-9) | (torch.abs(y_n.abs() - 1) < 1e-9)
+    # warped mesh: the boundary is still the square's boundary (warp vanishes there)
+    b = op.apply(xs)
+    x = torch.where(on, xs, torch.zeros_like(xs))
+    rtol = args.pcg_rtol
+    iters = args.steps
+    # warm-up (also builds the diagonal once per call, included in timing below)
+    op.pcg_solve(b, x.clone(), on, rtol=0.0, max_iter=max(1, args.warmup))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    x_run = x.clone()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    _, its, rel = op.pcg_solve(b, x_run, on, rtol=rtol, max_iter=iters if rtol == 0 else 200000)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    own = torch.from_numpy(part.owned).to(dev)
+    err_num = torch.sum((x_run - xs)[own] ** 2)
+    err_den = torch.sum(xs[own] ** 2)
+    if world > 1:
+        t = torch.stack([err_num, err_den]).cpu()
+        dist.all_reduce(t)
+        err_num, err_den = t[0], t[1]
+    err = float(torch.sqrt(err_num / err_den))
+    result = {
+        "metric": "assembled Poisson Jacobi-PCG, DOF-iterations/s, p=%d" % args.p,
+        "value": ndof_global * its / elapsed, "unit": "DOF*iterations/s", "n_gpus": world,
+        "steps": its, "warmup": args.warmup, "ms_per_step": elapsed / max(its, 1) * 1e3,
+        "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic manufactured solution on the structured warped quad mesh",
+        "config": {"workload": "pcg p=%d, %dx%d elements (%s)" % (
+            args.p, args.nex, args.ney, "fixed iterations" if rtol == 0 else
+            "solve to rtol %g" % rtol), "ndof_global": ndof_global, "ranks_seen": world,
+            "transport": op.transport},
+        "pcg": {"iterations": its, "iterations_per_s": its / elapsed, "seconds": elapsed,
+                "final_relres": rel, "rel_l2_error_vs_manufactured": err,
+                "check_every": 16, "gpu_setup_sec": t_setup},
+    }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    op.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

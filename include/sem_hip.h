@@ -157,9 +157,11 @@ int sem_set_geom_mode(sem_ctx* ctx, int mode);
  *    registers (D in even-odd form), transposes through LDS; chains of 4
  *    groups hand shared columns over through LDS; NODAL or STORED geometry.
  *  SEM_KERNEL_MFMA: k_poisson_mfma -- one element per wavefront as 16 x 16
- *    tiles on the fp64 matrix cores (v_mfma_f64_16x16x4_f64, six products
- *    per element, no LDS); element-level colouring; stored factors only
- *    (a NODAL request is ignored); n = p + 1 <= 16 and dpn = 1, else
+ *    tiles on the fp64 matrix cores (v_mfma_f64_16x16x4_f64, four products
+ *    per element with two transposes through a wave-private LDS tile;
+ *    block-diagonal packing of 16/n x 16/n elements per tile for n <= 8);
+ *    element-level colouring; stored factors, or x_phys per node when
+ *    SEM_GEOM_NODAL is requested; n = p + 1 <= 16 and dpn = 1, else
  *    SEM_E_NOTIMPL.
  *  SEM_KERNEL_AUTO (default): MFMA for 13 <= p <= 15 unless NODAL geometry
  *    was requested, COLUMN otherwise (measured on MI355X, DESIGN.md §4.6;
@@ -219,6 +221,13 @@ int sem_set_reynolds(sem_ctx* ctx, double re);
  * (element-boundary and unreferenced nodes; all dpn components). */
 int sem_zero_shared(sem_ctx* ctx, double* d_y, void* stream);
 
+/* Assembly of element-local nodal values through the element map:
+ * out[map[e][i][j]] (+)= vals[e][i][j] (vals device float64 [n_elem][n][n],
+ * dpn = 1) -- the reference's global RHS assembly grhs[inds] += lrhs
+ * (examples/poisson.py:219-243, sem/discrete.py:478-500), e.g. the load
+ * vector of f = 1 from detJxW (sem_geom_fields). */
+int sem_assemble(sem_ctx* ctx, const double* d_vals, double* d_out, int accumulate, void* stream);
+
 /* Diagonal of the assembled operator (Jacobi preconditioner for the
  * assembled Poisson solve; diag(Lse) summed through the map). */
 int sem_diag(sem_ctx* ctx, int op_kind, double* d_diag, void* stream);
@@ -248,12 +257,90 @@ int sem_scatter_add(double* d_dst, const uint32_t* d_idx, int64_t n, const doubl
 
 /* Matrix-free preconditioned CG for K x = b on the free DOFs
  * (mask[i] != 0 => Dirichlet DOF: x[i] fixed, row/col removed), Jacobi
- * preconditioner.  Replaces DOFManagerSC.solve (sem/discrete.py:502-528).
- * x holds the Dirichlet values and the initial guess on entry.  Synchronises
- * `stream` once per iteration for the convergence test. */
+ * preconditioner.  Replaces the assembled solve of DOFManagerSC.solve
+ * (sem/discrete.py:502-528; spsolve of the condensed system).  x holds the
+ * Dirichlet values and the initial guess on entry.  Device-resident: alpha,
+ * beta and the dot products never leave the device; the host reads the
+ * residual history once every SEM_PCG_CHECK_EVERY iterations (one small copy
+ * + one stream synchronisation), so up to SEM_PCG_CHECK_EVERY - 1 iterations
+ * run past the converged one (they only refine x).  *iters = iterations
+ * executed, *final_relres = ||r|| / ||r0|| after the last one.
+ * SEM_E_INVALID if not converged within max_iter; rtol = 0 runs exactly
+ * max_iter iterations (benchmarking) and returns SEM_OK. */
+#define SEM_PCG_CHECK_EVERY 16
 int sem_pcg_solve(sem_ctx* ctx, int op_kind, const double* d_b, double* d_x,
                   const uint8_t* d_dirichlet, double rtol, int max_iter,
                   int* iters, double* final_relres, void* stream);
+
+/* ------------------------------------------------------------------ */
+/* Domain decomposition across GPUs (one process per GPU)              */
+/* ------------------------------------------------------------------ */
+/* The reference's element loop (sem/discrete.py:189-209) is serial; its
+ * elements are independent except for the scatter-add, so a rank owns a set
+ * of elements and sums only the DOFs it shares with other ranks
+ * (SURVEY.md §8(e)).  A sem_dd holds two operator contexts of one rank:
+ *   iface     the elements touching a shared node, over a COMPACT numbering
+ *             of their n_iface_dofs DOFs (d_iface_dofs[i] = local DOF of
+ *             compact DOF i, device uint32);
+ *   interior  every other element, over the local numbering (ndof_local
+ *             DOFs); NULL when the rank has no interior element.
+ * iface is NULL (n_iface_dofs = 0, no peers) on a rank that shares no node;
+ * it still takes part in the global dot products.
+ * sem_dd_apply enqueues the interface elements on an internal side stream,
+ * packs their shared entries and exchanges them with the peers while the
+ * interior elements run on the caller's stream; the caller's stream then
+ * adds the interface result into y.  Peer k receives/sends
+ * h_peer_counts[k] values: d_peer_dofs (device uint32, concatenated over
+ * peers) lists the COMPACT DOFs shared with each peer, in an order both
+ * sides agree on (e.g. ascending global id).  d_not_owned (device uint8
+ * [ndof_local], may be NULL) marks DOFs whose owner is another rank (left out
+ * of the global dot products of sem_dd_pcg_solve). */
+typedef struct sem_dd sem_dd;
+int sem_dd_create(sem_dd** out, sem_ctx* iface, sem_ctx* interior, int64_t ndof_local,
+                  const uint32_t* d_iface_dofs, int64_t n_iface_dofs, int n_peers,
+                  const int* h_peers, const int64_t* h_peer_counts, const uint32_t* d_peer_dofs,
+                  const uint8_t* d_not_owned, int device);
+void sem_dd_destroy(sem_dd* dd);
+
+/* Transport, native: an RCCL communicator over all ranks (ncclSend/ncclRecv
+ * with each peer inside one group, ncclAllReduce for the dot products, all
+ * on the library's streams; xGMI between the GPUs of one node).  Rank 0
+ * creates the id with sem_rccl_unique_id and the caller broadcasts its
+ * SEM_RCCL_ID_BYTES bytes (e.g. through torch.distributed). */
+#define SEM_RCCL_ID_BYTES 128
+int sem_rccl_unique_id(void* h_id, int nbytes);
+int sem_dd_init_rccl(sem_dd* dd, const void* h_id, int world, int rank);
+
+/* Transport, caller-supplied (tests, other communication libraries): the
+ * exchange callback must leave in d_recv[off[k]..off[k+1]) the values peer
+ * peers[k] sent from its d_send range, ordered after the work already on
+ * `side_stream` and before anything enqueued on it later; the all-reduce
+ * callback sums `count` doubles of d_buf over all ranks in place, ordered on
+ * `stream`.  Both return 0 on success. */
+typedef int (*sem_exchange_fn)(void* user, int n_peers, const int* peers, const int64_t* off,
+                               double* d_send, double* d_recv, void* side_stream);
+typedef int (*sem_allreduce_fn)(void* user, double* d_buf, int count, void* stream);
+int sem_dd_set_transport(sem_dd* dd, sem_exchange_fn exchange, sem_allreduce_fn allreduce,
+                         void* user, int world, int rank);
+
+/* hipMemcpyAsync(dst, src, nbytes, hipMemcpyDefault, stream): lets a
+ * caller-supplied transport stage the library's device buffers. */
+int sem_copy_async(void* dst, const void* src, int64_t nbytes, void* stream);
+
+/* info[0] ndof_local, [1] n_iface_dofs, [2] peers, [3] exchanged values per
+ * direction, [4] transport (0 none, 1 RCCL, 2 callbacks), [5] has interior. */
+int sem_dd_info(sem_dd* dd, int64_t* info, int n_info);
+
+/* y = K u on this rank's DOFs, shared DOFs summed over all ranks (u, y local
+ * device vectors, must not alias). */
+int sem_dd_apply(sem_dd* dd, int op_kind, const double* d_u, double* d_y, void* stream);
+/* diagonal of the globally assembled operator on this rank's DOFs */
+int sem_dd_diag(sem_dd* dd, int op_kind, double* d_diag, void* stream);
+/* sem_pcg_solve over the decomposition: global dot products over owned DOFs
+ * (one all-reduce per dot), convergence read every check_every iterations. */
+int sem_dd_pcg_solve(sem_dd* dd, int op_kind, const double* d_b, double* d_x,
+                     const uint8_t* d_dirichlet, double rtol, int max_iter, int check_every,
+                     int* iters, double* final_relres, void* stream);
 
 #ifdef __cplusplus
 }

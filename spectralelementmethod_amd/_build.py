@@ -7,14 +7,17 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_NAME = "libsem_hip.so"
 LIB_PATH = os.environ.get("SEM_LIB_PATH", os.path.join(PKG_DIR, LIB_NAME))
-SOURCES = ["sem_device.hip", "sem_basis.cpp"]
+SOURCES = ["sem_device.hip", "sem_dd.hip", "sem_basis.cpp"]
 DEPS = SOURCES + ["sem_internal.h", "sem_kernels.h", "gll_table.h"]
 ARCH = os.environ.get("SEM_OFFLOAD_ARCH", "gfx950")
 
 
+def rocm_path():
+    return os.environ.get("ROCM_PATH", "/opt/rocm")
+
+
 def hipcc():
-    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
-    cand = os.path.join(rocm, "bin", "hipcc")
+    cand = os.path.join(rocm_path(), "bin", "hipcc")
     return cand if os.path.exists(cand) else "hipcc"
 
 
@@ -36,7 +39,10 @@ def build(force=False, verbose=True, out=None, defines=()):
     cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-fPIC", "-shared", "-std=c++17",
            "-munsafe-fp-atomics", "-Wall", "-Wno-unused-result",
            *["-D" + d for d in defines],
-           *[os.path.join(CSRC, s) for s in SOURCES], "-o", out + ".tmp"]
+           *[os.path.join(CSRC, s) for s in SOURCES],
+           # RCCL for the multi-GPU interface sum (resolves to the librccl.so.1
+           # torch already loaded when imported through _lib)
+           "-L" + os.path.join(rocm_path(), "lib"), "-lrccl", "-o", out + ".tmp"]
     if verbose:
         print("[sem build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -67,13 +67,33 @@ SIGNATURES = {
     "sem_zero_shared": (C.c_int, [_vp, _vp, _vp]),
     "sem_vec_add": (C.c_int, [_vp, _vp, _i64, _vp]),
     "sem_diag": (C.c_int, [_vp, C.c_int, _vp, _vp]),
+    "sem_assemble": (C.c_int, [_vp, _vp, _vp, C.c_int, _vp]),
     "sem_tensor_apply": (C.c_int, [C.c_int, _i64, _dp, _dp, _vp, _vp, _vp]),
     "sem_det_inv_2x2": (C.c_int, [_i64, _vp, _vp, _vp, _vp]),
     "sem_gather": (C.c_int, [_vp, _vp, _i64, _vp, _vp]),
     "sem_scatter_add": (C.c_int, [_vp, _vp, _i64, _vp, _vp]),
     "sem_pcg_solve": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, C.c_double, C.c_int,
                                 C.POINTER(C.c_int), C.POINTER(C.c_double), _vp]),
+    "sem_rccl_unique_id": (C.c_int, [_vp, C.c_int]),
+    "sem_copy_async": (C.c_int, [_vp, _vp, _i64, _vp]),
+    "sem_dd_create": (C.c_int, [C.POINTER(_vp), _vp, _vp, _i64, _vp, _i64, C.c_int,
+                                C.POINTER(C.c_int), C.POINTER(_i64), _vp, _vp, C.c_int]),
+    "sem_dd_destroy": (None, [_vp]),
+    "sem_dd_init_rccl": (C.c_int, [_vp, _vp, C.c_int, C.c_int]),
+    "sem_dd_set_transport": (C.c_int, [_vp, _vp, _vp, _vp, C.c_int, C.c_int]),
+    "sem_dd_info": (C.c_int, [_vp, C.POINTER(_i64), C.c_int]),
+    "sem_dd_apply": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp]),
+    "sem_dd_diag": (C.c_int, [_vp, C.c_int, _vp, _vp]),
+    "sem_dd_pcg_solve": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, C.c_double, C.c_int, C.c_int,
+                                   C.POINTER(C.c_int), C.POINTER(C.c_double), _vp]),
 }
+
+# sem_exchange_fn / sem_allreduce_fn (include/sem_hip.h)
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int, _vp, C.c_int, C.POINTER(C.c_int), C.POINTER(_i64), _vp, _vp,
+                          _vp)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, _vp, _vp, C.c_int, _vp)
+RCCL_ID_BYTES = 128
+PCG_CHECK_EVERY = 16
 
 _LIB = None
 

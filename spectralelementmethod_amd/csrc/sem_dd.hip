@@ -1,0 +1,633 @@
+// Domain decomposition of the operator across GPUs (one process per GPU) and
+// the device-resident preconditioned CG that runs on one or many of them.
+//
+// The reference has no parallelism (sem/discrete.py:208-209: one Python loop
+// over all elements).  Its element loop is independent per element except
+// for the final scatter-add y[loc] += y_e: a node on the boundary between two
+// ranks' elements receives contributions from both.  SURVEY.md §8(e).
+//
+// One rank owns a set of elements and the nodes they touch (local numbering).
+// Its elements are split into
+//   * interface elements: the ones touching a node shared with another rank,
+//     applied by a context (`iface`) over a COMPACT renumbering of just their
+//     nodes, into a small private vector y_c, on a side stream;
+//   * interior elements: all others, applied by `interior` over the local
+//     numbering straight into y, on the caller's stream, concurrently.
+// The side stream then sums the shared entries of y_c with the neighbours
+// (RCCL send/recv over xGMI, or a caller-supplied transport), and the
+// caller's stream finally adds y_c into y.  The interface sum is therefore
+// hidden behind the interior elements, and no kernel ever waits for the
+// small interface launches.  Only shared entries travel: 8 B per shared DOF
+// and direction, never the full vector.
+//
+//   main:  ev0 ------------- interior apply (u -> y) ------------- wait ev1, y[cidx] += y_c
+//   side:  wait ev0, u_c = u[cidx], iface apply (u_c -> y_c), pack, exchange, unpack, ev1
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "sem_internal.h"
+
+using sem::fail;
+
+#define HIP_TRY(expr)                                                                  \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    if (_e != hipSuccess)                                                              \
+      return fail(SEM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));      \
+  } while (0)
+
+#define NCCL_TRY(expr)                                                                  \
+  do {                                                                                  \
+    ncclResult_t _r = (expr);                                                           \
+    if (_r != ncclSuccess)                                                              \
+      return fail(SEM_E_HIP, std::string(#expr) + ": " + ncclGetErrorString(_r));       \
+  } while (0)
+
+#define SEM_TRY(expr)        \
+  do {                       \
+    int _rc = (expr);        \
+    if (_rc) return _rc;     \
+  } while (0)
+
+namespace {
+
+constexpr int BLK = 256;
+constexpr int WV = 64;
+constexpr int RED_BLOCKS = 1024;  // partial sums per dot (fixed: deterministic order)
+
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int grid_for(int64_t n, int cap = 8192) {
+  int64_t g = (n + BLK - 1) / BLK;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+// ---------------------------------------------------------------- PCG kernels
+// DOF flags: bit 0 Dirichlet (row/column removed, x fixed), bit 1 the DOF is
+// a copy owned by another rank (left out of the global dot products).
+constexpr uint8_t F_DIR = 1, F_NOTOWN = 2;
+
+__device__ double block_sum(double v) {
+  __shared__ double sh[BLK / WV];
+  for (int o = WV / 2; o > 0; o >>= 1) v += __shfl_down(v, o, WV);
+  if ((threadIdx.x & (WV - 1)) == 0) sh[threadIdx.x / WV] = v;
+  __syncthreads();
+  double s = 0.0;
+  if (threadIdx.x == 0)
+    for (int w = 0; w < BLK / WV; ++w) s += sh[w];
+  __syncthreads();
+  return s;
+}
+
+__device__ __forceinline__ void write_partials(double s0, double s1, double* partial) {
+  s0 = block_sum(s0);
+  s1 = block_sum(s1);
+  if (threadIdx.x == 0) {
+    partial[blockIdx.x] = s0;
+    partial[RED_BLOCKS + blockIdx.x] = s1;
+  }
+}
+
+// flags = dirichlet | (not owned) << 1
+__global__ void k_cg_flags(const uint8_t* __restrict__ dir, const uint8_t* __restrict__ notown,
+                           int64_t n, uint8_t* __restrict__ f) {
+  for (int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x; t < n; t += (int64_t)gridDim.x * BLK)
+    f[t] = (dir[t] ? F_DIR : 0) | ((notown && notown[t]) ? F_NOTOWN : 0);
+}
+
+// r = b - K x on free DOFs (r holds K x on entry), z = r / diag, p = z;
+// partial sums of r.z and r.r over owned DOFs
+__global__ void __launch_bounds__(BLK)
+    k_cg_start(const double* __restrict__ b, double* __restrict__ r, const double* __restrict__ diag,
+               const uint8_t* __restrict__ f, int64_t n, double* __restrict__ z,
+               double* __restrict__ p, double* __restrict__ partial) {
+  double s0 = 0.0, s1 = 0.0;
+  for (int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x; t < n; t += (int64_t)gridDim.x * BLK) {
+    const uint8_t ft = f[t];
+    const double rt = (ft & F_DIR) ? 0.0 : b[t] - r[t];
+    const double zt = (ft & F_DIR) ? 0.0 : rt / diag[t];
+    r[t] = rt;
+    z[t] = zt;
+    p[t] = zt;
+    if (!(ft & F_NOTOWN)) {
+      s0 = fma(rt, zt, s0);
+      s1 = fma(rt, rt, s1);
+    }
+  }
+  write_partials(s0, s1, partial);
+}
+
+// partial sums of p.q over owned DOFs (p = 0 on Dirichlet DOFs)
+__global__ void __launch_bounds__(BLK)
+    k_cg_pq(const double* __restrict__ p, const double* __restrict__ q,
+            const uint8_t* __restrict__ f, int64_t n, double* __restrict__ partial) {
+  double s0 = 0.0;
+  for (int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x; t < n; t += (int64_t)gridDim.x * BLK)
+    if (!(f[t] & F_NOTOWN)) s0 = fma(p[t], q[t], s0);
+  write_partials(s0, 0.0, partial);
+}
+
+// alpha = rz / pq (on the device); x += alpha p; r -= alpha q (free DOFs);
+// z = r / diag; partial sums of r.z and r.r
+__global__ void __launch_bounds__(BLK)
+    k_cg_update(double* __restrict__ x, double* __restrict__ r, double* __restrict__ z,
+                const double* __restrict__ p, const double* __restrict__ q,
+                const double* __restrict__ diag, const uint8_t* __restrict__ f,
+                const double* __restrict__ rz_old, const double* __restrict__ pq, int64_t n,
+                double* __restrict__ partial) {
+  const double den = *pq;
+  const double alpha = den != 0.0 ? *rz_old / den : 0.0;
+  double s0 = 0.0, s1 = 0.0;
+  for (int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x; t < n; t += (int64_t)gridDim.x * BLK) {
+    const uint8_t ft = f[t];
+    x[t] = fma(alpha, p[t], x[t]);
+    const double rt = (ft & F_DIR) ? 0.0 : fma(-alpha, q[t], r[t]);
+    const double zt = (ft & F_DIR) ? 0.0 : rt / diag[t];
+    r[t] = rt;
+    z[t] = zt;
+    if (!(ft & F_NOTOWN)) {
+      s0 = fma(rt, zt, s0);
+      s1 = fma(rt, rt, s1);
+    }
+  }
+  write_partials(s0, s1, partial);
+}
+
+// beta = rz_new / rz_old (on the device); p = z + beta p
+__global__ void k_cg_p(double* __restrict__ p, const double* __restrict__ z,
+                       const double* __restrict__ rz_new, const double* __restrict__ rz_old,
+                       int64_t n) {
+  const double den = *rz_old;
+  const double beta = den != 0.0 ? *rz_new / den : 0.0;
+  for (int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x; t < n; t += (int64_t)gridDim.x * BLK)
+    p[t] = fma(beta, p[t], z[t]);
+}
+
+// fixed-order sum of the partials: out[0..nd) (deterministic run to run)
+__global__ void __launch_bounds__(BLK)
+    k_cg_finish(const double* __restrict__ partial, int nb, int nd, double* __restrict__ out) {
+  double s0 = 0.0, s1 = 0.0;
+  for (int i = threadIdx.x; i < nb; i += BLK) {
+    s0 += partial[i];
+    s1 += partial[RED_BLOCKS + i];
+  }
+  s0 = block_sum(s0);
+  s1 = block_sum(s1);
+  if (threadIdx.x == 0) {
+    out[0] = s0;
+    if (nd > 1) out[1] = s1;
+  }
+}
+
+// history of the (globally reduced) r.r, for the lagged convergence test
+__global__ void k_cg_record(const double* __restrict__ rr, double* __restrict__ hist) {
+  if (threadIdx.x == 0) *hist = *rr;
+}
+
+__global__ void k_scatter_add_peer(double* __restrict__ dst, const uint32_t* __restrict__ idx,
+                                   int64_t n, const double* __restrict__ src) {
+  for (int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x; t < n; t += (int64_t)gridDim.x * BLK)
+    dst[idx[t]] += src[t];
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- context
+struct sem_dd {
+  int device = 0;
+  sem_ctx* iface = nullptr;     // interface elements, compact numbering
+  sem_ctx* interior = nullptr;  // interior elements, local numbering (may be null)
+  int64_t ndof = 0;             // local DOFs
+  int64_t nc = 0;               // compact (interface-element) DOFs
+  uint32_t* d_cidx = nullptr;   // compact -> local DOF
+  std::vector<int> peer;
+  std::vector<int64_t> off;     // per-peer ranges of the exchange buffers
+  uint32_t* d_pidx = nullptr;   // compact DOF of every exchanged entry
+  uint8_t* d_notown = nullptr;  // local DOFs owned by another rank (global dots)
+  double* d_uc = nullptr;
+  double* d_yc = nullptr;
+  double* d_send = nullptr;
+  double* d_recv = nullptr;
+  hipStream_t side = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // transport: native RCCL communicator, or caller callbacks
+  ncclComm_t comm = nullptr;
+  sem_exchange_fn xfn = nullptr;
+  sem_allreduce_fn rfn = nullptr;
+  void* user = nullptr;
+  int world = 1, rank = 0;
+};
+
+namespace {
+
+int64_t n_exchanged(const sem_dd* d) { return d->off.empty() ? 0 : d->off.back(); }
+
+// compute part of one step: interface elements on the side stream into y_c
+// and packed into the send buffer, interior elements on `st` into y.
+// DIAG: the operator diagonal (Jacobi) instead of the action.
+int dd_begin(sem_dd* d, int op_kind, bool diag, const double* u, double* y, hipStream_t st) {
+  HIP_TRY(hipEventRecord(d->ev0, st));
+  HIP_TRY(hipStreamWaitEvent(d->side, d->ev0, 0));
+  void* sd = d->side;
+  if (d->iface) {
+    if (diag) {
+      SEM_TRY(sem_diag(d->iface, op_kind, d->d_yc, sd));
+    } else {
+      SEM_TRY(sem_gather(u, d->d_cidx, d->nc, d->d_uc, sd));
+      SEM_TRY(sem_apply(d->iface, op_kind, d->d_uc, d->d_yc, 0, sd));
+    }
+    SEM_TRY(sem_gather(d->d_yc, d->d_pidx, n_exchanged(d), d->d_send, sd));
+  }
+  if (d->interior) {
+    if (diag)
+      SEM_TRY(sem_diag(d->interior, op_kind, y, st));
+    else
+      SEM_TRY(sem_apply(d->interior, op_kind, u, y, 0, st));
+  } else {
+    HIP_TRY(hipMemsetAsync(y, 0, d->ndof * sizeof(double), st));
+  }
+  return SEM_OK;
+}
+
+int dd_exchange(sem_dd* d) {
+  const int np = (int)d->peer.size();
+  if (!np) return SEM_OK;
+  if (d->comm) {
+    NCCL_TRY(ncclGroupStart());
+    for (int k = 0; k < np; ++k) {
+      const size_t cnt = (size_t)(d->off[k + 1] - d->off[k]);
+      NCCL_TRY(ncclSend(d->d_send + d->off[k], cnt, ncclFloat64, d->peer[k], d->comm, d->side));
+      NCCL_TRY(ncclRecv(d->d_recv + d->off[k], cnt, ncclFloat64, d->peer[k], d->comm, d->side));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    return SEM_OK;
+  }
+  if (d->xfn) {
+    const int rc = d->xfn(d->user, np, d->peer.data(), d->off.data(), d->d_send, d->d_recv,
+                          d->side);
+    return rc ? fail(SEM_E_HIP, "interface exchange callback failed (" + std::to_string(rc) + ")")
+              : SEM_OK;
+  }
+  return fail(SEM_E_STATE, "no transport: call sem_dd_init_rccl or sem_dd_set_transport");
+}
+
+// neighbours' partial sums into y_c (one launch per peer: a DOF may be
+// shared with several peers), then y[cidx] += y_c on `st` after the side
+// stream's work
+int dd_finish(sem_dd* d, double* y, hipStream_t st) {
+  for (size_t k = 0; k + 1 < d->off.size(); ++k) {
+    const int64_t cnt = d->off[k + 1] - d->off[k];
+    if (cnt)
+      hipLaunchKernelGGL(k_scatter_add_peer, dim3(grid_for(cnt)), dim3(BLK), 0, d->side, d->d_yc,
+                         d->d_pidx + d->off[k], cnt, d->d_recv + d->off[k]);
+  }
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(d->ev1, d->side));
+  HIP_TRY(hipStreamWaitEvent(st, d->ev1, 0));
+  return d->nc ? sem_scatter_add(y, d->d_cidx, d->nc, d->d_yc, st) : SEM_OK;
+}
+
+int dd_allreduce(sem_dd* d, double* buf, int count, hipStream_t st) {
+  if (!d || d->world == 1) return SEM_OK;
+  if (d->comm) {
+    NCCL_TRY(ncclAllReduce(buf, buf, (size_t)count, ncclFloat64, ncclSum, d->comm, st));
+    return SEM_OK;
+  }
+  if (d->rfn) {
+    const int rc = d->rfn(d->user, buf, count, st);
+    return rc ? fail(SEM_E_HIP, "all-reduce callback failed (" + std::to_string(rc) + ")") : SEM_OK;
+  }
+  return fail(SEM_E_STATE, "no transport for the global dot products");
+}
+
+// ---------------------------------------------------------------- PCG loop
+// Jacobi-preconditioned CG on the free DOFs with every scalar on the device:
+// alpha and beta are formed inside the update kernels from the reduced dot
+// products, so an iteration enqueues its work without waiting for the host.
+// The host reads the r.r history every `check` iterations (one small copy
+// and one stream synchronisation) and stops at the first block that reached
+// the tolerance; the iterations past the converged one only refine x.
+struct PcgOp {
+  sem_ctx* ctx = nullptr;  // single GPU
+  sem_dd* dd = nullptr;    // or a rank of a decomposition
+  int64_t n = 0;
+  int device = 0;
+  int apply(int kind, const double* p, double* q, hipStream_t st) const {
+    if (dd) {
+      SEM_TRY(dd_begin(dd, kind, false, p, q, st));
+      SEM_TRY(dd_exchange(dd));
+      return dd_finish(dd, q, st);
+    }
+    return sem_apply(ctx, kind, p, q, 0, st);
+  }
+  int diag(int kind, double* out, hipStream_t st) const {
+    if (dd) {
+      SEM_TRY(dd_begin(dd, kind, true, nullptr, out, st));
+      SEM_TRY(dd_exchange(dd));
+      return dd_finish(dd, out, st);
+    }
+    return sem_diag(ctx, kind, out, st);
+  }
+};
+
+struct PcgScratch {
+  double* base = nullptr;
+  uint8_t* flags = nullptr;
+  double* red = nullptr;
+  double* hist = nullptr;
+  double* h_hist = nullptr;  // pinned
+  ~PcgScratch() {
+    (void)hipFree(base);
+    (void)hipFree(flags);
+    (void)hipFree(red);
+    (void)hipFree(hist);
+    (void)hipHostFree(h_hist);
+  }
+};
+
+const bool g_sync_each = std::getenv("SEM_PCG_SYNC_EACH") != nullptr;  // diagnostic
+
+int pcg_run(const PcgOp& op, int kind, const double* b, double* x, const uint8_t* dir,
+            const uint8_t* notown, double rtol, int max_iter, int check, int* iters,
+            double* relres, hipStream_t st) {
+  if (!b || !x || !dir) return fail(SEM_E_INVALID, "null argument");
+  if (kind != SEM_OP_POISSON) return fail(SEM_E_NOTIMPL, "PCG: Poisson only");
+  // rtol = 0: run exactly max_iter iterations (benchmarking)
+  if (max_iter < 0 || !(rtol >= 0.0)) return fail(SEM_E_INVALID, "need rtol >= 0, max_iter >= 0");
+  if (check < 1) check = 1;
+  DeviceGuard g(op.device);
+  const int64_t n = op.n;
+  PcgScratch s;
+  HIP_TRY(hipMalloc(&s.base, 5 * n * sizeof(double)));
+  HIP_TRY(hipMalloc(&s.flags, n));
+  // partials [2][RED_BLOCKS], then scalars: T0 = (rz, rr), T1 = (rz, rr), pq
+  HIP_TRY(hipMalloc(&s.red, (2 * RED_BLOCKS + 8) * sizeof(double)));
+  HIP_TRY(hipMalloc(&s.hist, ((size_t)max_iter + 1) * sizeof(double)));
+  HIP_TRY(hipHostMalloc(&s.h_hist, ((size_t)check + 1) * sizeof(double)));
+  double* r = s.base;
+  double* z = r + n;
+  double* p = z + n;
+  double* q = p + n;
+  double* dg = q + n;
+  double* partial = s.red;
+  double* T[2] = {s.red + 2 * RED_BLOCKS, s.red + 2 * RED_BLOCKS + 2};
+  double* pq = s.red + 2 * RED_BLOCKS + 4;
+  const int gb = grid_for(n, RED_BLOCKS);
+  hipLaunchKernelGGL(k_cg_flags, dim3(grid_for(n)), dim3(BLK), 0, st, dir, notown, n, s.flags);
+  SEM_TRY(op.diag(kind, dg, st));
+  SEM_TRY(op.apply(kind, x, r, st));
+  hipLaunchKernelGGL(k_cg_start, dim3(gb), dim3(BLK), 0, st, b, r, dg, s.flags, n, z, p, partial);
+  hipLaunchKernelGGL(k_cg_finish, dim3(1), dim3(BLK), 0, st, partial, gb, 2, T[0]);
+  HIP_TRY(hipGetLastError());
+  SEM_TRY(dd_allreduce(op.dd, T[0], 2, st));
+  HIP_TRY(hipMemcpyAsync(s.h_hist, T[0] + 1, sizeof(double), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const double rr0 = s.h_hist[0];
+  if (!std::isfinite(rr0)) return fail(SEM_E_INVALID, "PCG: non-finite initial residual");
+  const double tol2 = rtol * rtol * rr0;
+  double rr_last = rr0;
+  int it = 0;
+  bool done = rr0 == 0.0;
+  while (!done && it < max_iter) {
+    const int blk = std::min(check, max_iter - it);
+    for (int k = 0; k < blk; ++k) {
+      const int o = it & 1, nw = o ^ 1;
+      SEM_TRY(op.apply(kind, p, q, st));
+      hipLaunchKernelGGL(k_cg_pq, dim3(gb), dim3(BLK), 0, st, p, q, s.flags, n, partial);
+      hipLaunchKernelGGL(k_cg_finish, dim3(1), dim3(BLK), 0, st, partial, gb, 1, pq);
+      SEM_TRY(dd_allreduce(op.dd, pq, 1, st));
+      hipLaunchKernelGGL(k_cg_update, dim3(gb), dim3(BLK), 0, st, x, r, z, p, q, dg, s.flags,
+                         T[o], pq, n, partial);
+      hipLaunchKernelGGL(k_cg_finish, dim3(1), dim3(BLK), 0, st, partial, gb, 2, T[nw]);
+      SEM_TRY(dd_allreduce(op.dd, T[nw], 2, st));
+      hipLaunchKernelGGL(k_cg_record, dim3(1), dim3(WV), 0, st, T[nw] + 1, s.hist + it + 1);
+      hipLaunchKernelGGL(k_cg_p, dim3(grid_for(n)), dim3(BLK), 0, st, p, z, T[nw], T[o], n);
+      HIP_TRY(hipGetLastError());
+      if (g_sync_each) HIP_TRY(hipDeviceSynchronize());  // diagnostic
+      ++it;
+    }
+    HIP_TRY(hipMemcpyAsync(s.h_hist, s.hist + it - blk + 1, blk * sizeof(double),
+                           hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    for (int k = 0; k < blk; ++k) {
+      rr_last = s.h_hist[k];
+      if (!std::isfinite(rr_last)) return fail(SEM_E_INVALID, "PCG: non-finite residual");
+      if (rr_last <= tol2) done = true;
+    }
+  }
+  if (iters) *iters = it;
+  if (relres) *relres = rr0 > 0.0 ? std::sqrt(rr_last / rr0) : 0.0;
+  if (!done && rtol > 0.0)
+    return fail(SEM_E_INVALID, "PCG did not converge in " + std::to_string(max_iter) +
+                                   " iterations");
+  return SEM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sem_pcg_solve(sem_ctx* c, int op_kind, const double* b, double* x, const uint8_t* mask,
+                  double rtol, int max_iter, int* iters, double* relres, void* stream) {
+  if (!c) return fail(SEM_E_INVALID, "null ctx");
+  PcgOp op;
+  op.ctx = c;
+  op.n = sem::ctx_ndof(c);
+  op.device = sem::ctx_device(c);
+  return pcg_run(op, op_kind, b, x, mask, nullptr, rtol, max_iter, SEM_PCG_CHECK_EVERY, iters,
+                 relres, S(stream));
+}
+
+int sem_copy_async(void* dst, const void* src, int64_t nbytes, void* stream) {
+  if (nbytes < 0 || (nbytes && (!dst || !src))) return fail(SEM_E_INVALID, "bad arguments");
+  if (nbytes) HIP_TRY(hipMemcpyAsync(dst, src, (size_t)nbytes, hipMemcpyDefault, S(stream)));
+  return SEM_OK;
+}
+
+int sem_rccl_unique_id(void* h_id, int nbytes) {
+  if (!h_id || nbytes < (int)sizeof(ncclUniqueId))
+    return fail(SEM_E_INVALID, "need a buffer of SEM_RCCL_ID_BYTES bytes");
+  ncclUniqueId id;
+  NCCL_TRY(ncclGetUniqueId(&id));
+  std::memcpy(h_id, &id, sizeof(id));
+  return SEM_OK;
+}
+
+int sem_dd_create(sem_dd** out, sem_ctx* iface, sem_ctx* interior, int64_t ndof_local,
+                  const uint32_t* d_iface_dofs, int64_t n_iface_dofs, int n_peers,
+                  const int* h_peers, const int64_t* h_peer_counts, const uint32_t* d_peer_dofs,
+                  const uint8_t* d_not_owned, int device) {
+  if (!out) return fail(SEM_E_INVALID, "null dd pointer");
+  *out = nullptr;
+  if (ndof_local < 1 || n_peers < 0 || n_iface_dofs < 0 ||
+      (n_peers && (!h_peers || !h_peer_counts || !d_peer_dofs)))
+    return fail(SEM_E_INVALID, "sem_dd_create: bad arguments");
+  // a rank that shares no node still joins the global dot products
+  if (!iface != (n_iface_dofs == 0) || (!iface && n_peers) || (iface && !d_iface_dofs))
+    return fail(SEM_E_INVALID, "sem_dd_create: interface context, DOFs and peers disagree");
+  if (!iface && !interior) return fail(SEM_E_INVALID, "sem_dd_create: no elements");
+  if (iface && sem::ctx_ndof(iface) != n_iface_dofs)
+    return fail(SEM_E_INVALID, "interface context must hold exactly n_iface_dofs DOFs");
+  if (interior && sem::ctx_ndof(interior) != ndof_local)
+    return fail(SEM_E_INVALID, "interior context must hold ndof_local DOFs");
+  if ((iface && sem::ctx_device(iface) != device) ||
+      (interior && sem::ctx_device(interior) != device))
+    return fail(SEM_E_INVALID, "contexts live on another device");
+  DeviceGuard g(device);
+  sem_dd* d = new sem_dd();
+  d->device = device;
+  d->iface = iface;
+  d->interior = interior;
+  d->ndof = ndof_local;
+  d->nc = n_iface_dofs;
+  d->off.assign(1, 0);
+  for (int k = 0; k < n_peers; ++k) {
+    if (h_peer_counts[k] < 0) {
+      delete d;
+      return fail(SEM_E_INVALID, "negative peer count");
+    }
+    d->peer.push_back(h_peers[k]);
+    d->off.push_back(d->off.back() + h_peer_counts[k]);
+  }
+  const int64_t ne = d->off.back();
+  auto bad = [&](hipError_t e) {
+    if (e == hipSuccess) return false;
+    sem_dd_destroy(d);
+    return true;
+  };
+  const int64_t nc1 = std::max<int64_t>(n_iface_dofs, 1);
+  if (bad(hipMalloc(&d->d_cidx, nc1 * sizeof(uint32_t))) ||
+      bad(hipMalloc(&d->d_uc, nc1 * sizeof(double))) ||
+      bad(hipMalloc(&d->d_yc, nc1 * sizeof(double))) ||
+      bad(hipMalloc(&d->d_pidx, std::max<int64_t>(ne, 1) * sizeof(uint32_t))) ||
+      bad(hipMalloc(&d->d_send, std::max<int64_t>(ne, 1) * sizeof(double))) ||
+      bad(hipMalloc(&d->d_recv, std::max<int64_t>(ne, 1) * sizeof(double))) ||
+      bad(hipStreamCreateWithFlags(&d->side, hipStreamNonBlocking)) ||
+      bad(hipEventCreateWithFlags(&d->ev0, hipEventDisableTiming)) ||
+      bad(hipEventCreateWithFlags(&d->ev1, hipEventDisableTiming)))
+    return fail(SEM_E_HIP, "sem_dd_create: HIP allocation failed");
+  if (n_iface_dofs && bad(hipMemcpy(d->d_cidx, d_iface_dofs, n_iface_dofs * sizeof(uint32_t),
+                                    hipMemcpyDeviceToDevice)))
+    return fail(SEM_E_HIP, "sem_dd_create: copy failed");
+  if (ne && bad(hipMemcpy(d->d_pidx, d_peer_dofs, ne * sizeof(uint32_t), hipMemcpyDeviceToDevice)))
+    return fail(SEM_E_HIP, "sem_dd_create: copy failed");
+  if (d_not_owned) {
+    if (bad(hipMalloc(&d->d_notown, ndof_local)) ||
+        bad(hipMemcpy(d->d_notown, d_not_owned, ndof_local, hipMemcpyDeviceToDevice)))
+      return fail(SEM_E_HIP, "sem_dd_create: copy failed");
+  }
+  // the device-to-device copies above may still run on the legacy stream
+  if (bad(hipDeviceSynchronize())) return fail(SEM_E_HIP, "sem_dd_create: synchronize failed");
+  *out = d;
+  return SEM_OK;
+}
+
+void sem_dd_destroy(sem_dd* d) {
+  if (!d) return;
+  DeviceGuard g(d->device);
+  if (d->side) (void)hipStreamSynchronize(d->side);
+  if (d->comm) (void)ncclCommDestroy(d->comm);
+  (void)hipFree(d->d_cidx);
+  (void)hipFree(d->d_pidx);
+  (void)hipFree(d->d_notown);
+  (void)hipFree(d->d_uc);
+  (void)hipFree(d->d_yc);
+  (void)hipFree(d->d_send);
+  (void)hipFree(d->d_recv);
+  if (d->ev0) (void)hipEventDestroy(d->ev0);
+  if (d->ev1) (void)hipEventDestroy(d->ev1);
+  if (d->side) (void)hipStreamDestroy(d->side);
+  delete d;
+}
+
+int sem_dd_init_rccl(sem_dd* d, const void* h_id, int world, int rank) {
+  if (!d || !h_id || world < 1 || rank < 0 || rank >= world)
+    return fail(SEM_E_INVALID, "sem_dd_init_rccl: bad arguments");
+  for (int p : d->peer)
+    if (p < 0 || p >= world || p == rank) return fail(SEM_E_INVALID, "peer rank out of range");
+  DeviceGuard g(d->device);
+  ncclUniqueId id;
+  std::memcpy(&id, h_id, sizeof(id));
+  ncclComm_t comm = nullptr;
+  NCCL_TRY(ncclCommInitRank(&comm, world, id, rank));
+  if (d->comm) (void)ncclCommDestroy(d->comm);
+  d->comm = comm;
+  d->world = world;
+  d->rank = rank;
+  return SEM_OK;
+}
+
+int sem_dd_set_transport(sem_dd* d, sem_exchange_fn xfn, sem_allreduce_fn rfn, void* user,
+                         int world, int rank) {
+  if (!d || world < 1 || rank < 0 || rank >= world)
+    return fail(SEM_E_INVALID, "sem_dd_set_transport: bad arguments");
+  d->xfn = xfn;
+  d->rfn = rfn;
+  d->user = user;
+  d->world = world;
+  d->rank = rank;
+  if (d->comm) {
+    DeviceGuard g(d->device);
+    (void)ncclCommDestroy(d->comm);
+    d->comm = nullptr;
+  }
+  return SEM_OK;
+}
+
+int sem_dd_info(sem_dd* d, int64_t* info, int n_info) {
+  if (!d || !info || n_info < 1) return fail(SEM_E_INVALID, "bad arguments");
+  const int64_t v[6] = {d->ndof, d->nc, (int64_t)d->peer.size(), n_exchanged(d),
+                        d->comm ? 1 : (d->xfn ? 2 : 0), d->interior ? 1 : 0};
+  for (int i = 0; i < n_info && i < 6; ++i) info[i] = v[i];
+  return SEM_OK;
+}
+
+int sem_dd_apply(sem_dd* d, int op_kind, const double* d_u, double* d_y, void* stream) {
+  if (!d || !d_u || !d_y) return fail(SEM_E_INVALID, "null argument");
+  if (d_u == d_y) return fail(SEM_E_INVALID, "sem_dd_apply: u and y must not alias");
+  DeviceGuard g(d->device);
+  SEM_TRY(dd_begin(d, op_kind, false, d_u, d_y, S(stream)));
+  SEM_TRY(dd_exchange(d));
+  return dd_finish(d, d_y, S(stream));
+}
+
+int sem_dd_diag(sem_dd* d, int op_kind, double* d_diag, void* stream) {
+  if (!d || !d_diag) return fail(SEM_E_INVALID, "null argument");
+  DeviceGuard g(d->device);
+  SEM_TRY(dd_begin(d, op_kind, true, nullptr, d_diag, S(stream)));
+  SEM_TRY(dd_exchange(d));
+  return dd_finish(d, d_diag, S(stream));
+}
+
+int sem_dd_pcg_solve(sem_dd* d, int op_kind, const double* d_b, double* d_x,
+                     const uint8_t* d_dirichlet, double rtol, int max_iter, int check_every,
+                     int* iters, double* final_relres, void* stream) {
+  if (!d) return fail(SEM_E_INVALID, "null dd");
+  PcgOp op;
+  op.dd = d;
+  op.n = d->ndof;
+  op.device = d->device;
+  return pcg_run(op, op_kind, d_b, d_x, d_dirichlet, d->d_notown, rtol, max_iter, check_every,
+                 iters, final_relres, S(stream));
+}
+
+}  // extern "C"

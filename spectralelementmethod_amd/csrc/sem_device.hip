@@ -85,6 +85,14 @@ __global__ void k_poisson_diag(const uint32_t* __restrict__ mapP, const double* 
   }
 }
 
+// out[map[e][i][j]] += vals[e][i][j] through the caller's map (setup-time assembly)
+__global__ void k_assemble(const uint32_t* __restrict__ e2n, const double* __restrict__ vals,
+                           int64_t total, double* __restrict__ out) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x)
+    atomic_add_f64(out + e2n[t], vals[t]);
+}
+
 __global__ void k_gather(const double* __restrict__ src, const uint32_t* __restrict__ idx,
                          int64_t n, double* __restrict__ dst) {
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n;
@@ -103,99 +111,6 @@ __global__ void k_scatter_add(double* __restrict__ dst, const uint32_t* __restri
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n;
        t += (int64_t)gridDim.x * blockDim.x)
     dst[idx[t]] += src[t];
-}
-
-// ---- CG vector kernels (deterministic two-stage reductions) ----
-constexpr int RED_BLOCKS = 1024;
-
-__device__ double block_sum(double v) {
-  __shared__ double sh[BLOCK / WAVE];
-  for (int o = WAVE / 2; o > 0; o >>= 1) v += __shfl_down(v, o, WAVE);
-  if ((threadIdx.x & (WAVE - 1)) == 0) sh[threadIdx.x / WAVE] = v;
-  __syncthreads();
-  double s = 0.0;
-  if (threadIdx.x == 0)
-    for (int w = 0; w < BLOCK / WAVE; ++w) s += sh[w];
-  __syncthreads();
-  return s;
-}
-
-// partial[b] = sum a*b (and c*d) over the block's grid-stride slice
-__global__ void __launch_bounds__(BLOCK) k_dot2(const double* __restrict__ a,
-                                                const double* __restrict__ b,
-                                                const double* __restrict__ c,
-                                                const double* __restrict__ d, int64_t n,
-                                                double* __restrict__ partial) {
-  double s0 = 0.0, s1 = 0.0;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    s0 = fma(a[t], b[t], s0);
-    if (c) s1 = fma(c[t], d[t], s1);
-  }
-  s0 = block_sum(s0);
-  s1 = block_sum(s1);
-  if (threadIdx.x == 0) {
-    partial[blockIdx.x] = s0;
-    partial[gridDim.x + blockIdx.x] = s1;
-  }
-}
-
-__global__ void __launch_bounds__(BLOCK) k_finish2(const double* __restrict__ partial, int nb,
-                                                   double* __restrict__ out) {
-  double s0 = 0.0, s1 = 0.0;
-  for (int i = threadIdx.x; i < nb; i += blockDim.x) {
-    s0 += partial[i];
-    s1 += partial[nb + i];
-  }
-  s0 = block_sum(s0);
-  s1 = block_sum(s1);
-  if (threadIdx.x == 0) {
-    out[0] = s0;
-    out[1] = s1;
-  }
-}
-
-// r = mask ? 0 : b - r   (r holds K x on entry)
-__global__ void k_residual(const double* __restrict__ b, double* __restrict__ r,
-                           const uint8_t* __restrict__ mask, int64_t n) {
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n;
-       t += (int64_t)gridDim.x * blockDim.x)
-    r[t] = mask[t] ? 0.0 : b[t] - r[t];
-}
-
-// z = r / diag on free DOFs, 0 on Dirichlet
-__global__ void k_precond(const double* __restrict__ r, const double* __restrict__ diag,
-                          const uint8_t* __restrict__ mask, int64_t n, double* __restrict__ z) {
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n;
-       t += (int64_t)gridDim.x * blockDim.x)
-    z[t] = mask[t] ? 0.0 : r[t] / diag[t];
-}
-
-__global__ void k_mask(double* __restrict__ q, const uint8_t* __restrict__ mask, int64_t n) {
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n;
-       t += (int64_t)gridDim.x * blockDim.x)
-    if (mask[t]) q[t] = 0.0;
-}
-
-// x += alpha p ; r -= alpha q
-__global__ void k_update_xr(double* __restrict__ x, double* __restrict__ r,
-                            const double* __restrict__ p, const double* __restrict__ q,
-                            const double* __restrict__ scal, int64_t n) {
-  const double alpha = scal[0];
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    x[t] = fma(alpha, p[t], x[t]);
-    r[t] = fma(-alpha, q[t], r[t]);
-  }
-}
-
-// p = z + beta p
-__global__ void k_update_p(double* __restrict__ p, const double* __restrict__ z,
-                           const double* __restrict__ scal, int64_t n) {
-  const double beta = scal[1];
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n;
-       t += (int64_t)gridDim.x * blockDim.x)
-    p[t] = fma(beta, p[t], z[t]);
 }
 
 // out[b][m][q] = sum_{r,s} A0[m][r] A1[q][s] in[b][r][s]  (A = NULL -> identity)
@@ -298,12 +213,13 @@ struct sem_ctx {
   double2* d_XG = nullptr;
   uint32_t* d_owner = nullptr;
   bool xg_valid = false;
-  // CG scratch
-  double* d_cg = nullptr;
-  int64_t cg_len = 0;
-  double* d_red = nullptr;
   unsigned long long* d_bad = nullptr;
 };
+
+namespace sem {
+int64_t ctx_ndof(const sem_ctx* c) { return c->n_node * c->dpn; }
+int ctx_device(const sem_ctx* c) { return c->device; }
+}  // namespace sem
 
 namespace {
 
@@ -500,13 +416,17 @@ int gp_slot(int op_kind) {
   return op_kind == SEM_OP_POISSON ? 0 : (op_kind == SEM_OP_AXISYM_STOKES ? 1 : 2);
 }
 
-int ensure_gp(sem_ctx* c, int op_kind) {
+// The zero fill is ordered on the stream of the kernels that fill the
+// buffer: a plain hipMemset of device memory may still be in flight on the
+// legacy default stream when a kernel on a non-blocking stream (the
+// multi-GPU side stream) writes the factors.
+int ensure_gp(sem_ctx* c, int op_kind, hipStream_t st) {
   const int slot = gp_slot(op_kind);
   if (!c->d_GP[slot]) {
     const int ncomp = sem_op_ncomp(op_kind);
     const size_t bytes = (size_t)c->n_slots * ncomp * c->n * c->lw * sizeof(double);
     HIP_TRY(hipMalloc(&c->d_GP[slot], bytes));
-    HIP_TRY(hipMemset(c->d_GP[slot], 0, bytes));
+    HIP_TRY(hipMemsetAsync(c->d_GP[slot], 0, bytes, st));
   }
   return SEM_OK;
 }
@@ -907,8 +827,7 @@ int sem_ctx_create(sem_ctx** out, int p, int64_t n_elem, int64_t n_node, int dpn
   hipError_t e3 = hipMalloc(&c->d_Vinv, SEM_MAXN * SEM_MAXN * sizeof(double));
   hipError_t e4 = hipMalloc(&c->d_bad, sizeof(unsigned long long));
   if (!e4) e4 = hipMalloc(&c->d_deo, sizeof(DEOData<SEM_MAXN>));
-  hipError_t e5 = hipMalloc(&c->d_red, (2 * RED_BLOCKS + 8) * sizeof(double));
-  if (e1 || e2 || e3 || e4 || e5) {
+  if (e1 || e2 || e3 || e4) {
     sem_ctx_destroy(c);
     return fail(SEM_E_HIP, "hipMalloc failed in sem_ctx_create");
   }
@@ -932,8 +851,6 @@ void sem_ctx_destroy(sem_ctx* c) {
   (void)hipFree(c->d_lin);
   (void)hipFree(c->d_XG);
   (void)hipFree(c->d_owner);
-  (void)hipFree(c->d_cg);
-  (void)hipFree(c->d_red);
   (void)hipFree(c->d_bad);
   delete c;
 }
@@ -1059,7 +976,11 @@ int sem_plan_info(sem_ctx* c, int64_t* info, int n_info) {
     vals[8 + q] = c->colour_start[q + 1] - c->colour_start[q];
   vals[NV - 3] = c->mfma ? SEM_KERNEL_MFMA : SEM_KERNEL_COLUMN;
   vals[NV - 2] = c->map16 ? 2 : 4;  // bytes per packed map entry
-  vals[NV - 1] = nodal_mode(c) ? SEM_GEOM_NODAL : SEM_GEOM_STORED;  // Poisson geometry
+  // the geometry the Poisson action actually uses: nodal only once x_phys
+  // per node exists (sem_set_geom installs stored factors); before any
+  // geometry, the mode sem_geom_from_nodes will resolve to
+  const bool eff_nodal = c->xg_valid ? true : (c->d_GP[0] ? false : nodal_mode(c));
+  vals[NV - 1] = eff_nodal ? SEM_GEOM_NODAL : SEM_GEOM_STORED;
   for (int i = 0; i < n_info && i < NV; ++i) info[i] = vals[i];
   return SEM_OK;
 }
@@ -1113,7 +1034,7 @@ int sem_geom_from_nodes(sem_ctx* c, const double* d_nodes, const double* h_Vinv,
     (void)hipFree(c->d_GP[0]);
     c->d_GP[0] = nullptr;
   } else {
-    if ((rc = ensure_gp(c, op_kind))) return rc;
+    if ((rc = ensure_gp(c, op_kind, S(stream)))) return rc;
     GP = c->d_GP[gp_slot(op_kind)];
   }
   hipStream_t st = S(stream);
@@ -1153,7 +1074,7 @@ int sem_set_geom(sem_ctx* c, const double* d_G, int op_kind, void* stream) {
   DeviceGuard g(c->device);
   int rc;
   if ((rc = check_op(c, op_kind))) return rc;
-  if ((rc = ensure_gp(c, op_kind))) return rc;
+  if ((rc = ensure_gp(c, op_kind, S(stream)))) return rc;
   const int ncomp = sem_op_ncomp(op_kind);
   if (op_kind == SEM_OP_POISSON) c->xg_valid = false;  // caller's factors take over
   hipLaunchKernelGGL(k_pack_geom, dim3(grid_for(c->n_elem * ncomp * c->n * c->n)), dim3(BLOCK), 0,
@@ -1176,6 +1097,11 @@ int sem_zero_shared(sem_ctx* c, double* y, void* stream) {
 
 int sem_apply(sem_ctx* c, int op_kind, const double* u, double* y, int flags, void* stream) {
   if (!c || !u || !y) return fail(SEM_E_INVALID, "null argument");
+  {  // the kernels read u while other workgroups write y (both __restrict__)
+    const size_t nb = (size_t)c->n_node * c->dpn * sizeof(double);
+    const char *a = reinterpret_cast<const char*>(u), *b = reinterpret_cast<const char*>(y);
+    if (a < b + nb && b < a + nb) return fail(SEM_E_INVALID, "sem_apply: u and y overlap");
+  }
   if (flags & ~(SEM_APPLY_ACCUMULATE | SEM_APPLY_SKIP_ZERO | SEM_APPLY_LINEARIZE))
     return fail(SEM_E_INVALID, "unknown sem_apply flags");
   int rc;
@@ -1220,7 +1146,7 @@ int sem_diag(sem_ctx* c, int op_kind, double* d_diag, void* stream) {
   DeviceGuard g(c->device);
   hipStream_t st = S(stream);
   if (!c->d_GP[0]) {  // NODAL mode: derive the stored factors once from x_phys per node
-    if ((rc = ensure_gp(c, op_kind))) return rc;
+    if ((rc = ensure_gp(c, op_kind, st))) return rc;
     SEM_DISPATCH_N(c->n, launch_geom_n, c, nullptr, SEM_OP_POISSON, c->d_GP[0], nullptr, nullptr,
                    nullptr, nullptr, nullptr, nullptr, c->d_XG, st);
     HIP_TRY(hipGetLastError());
@@ -1228,6 +1154,20 @@ int sem_diag(sem_ctx* c, int op_kind, double* d_diag, void* stream) {
   HIP_TRY(hipMemsetAsync(d_diag, 0, c->n_node * sizeof(double), st));
   hipLaunchKernelGGL(k_poisson_diag, dim3(grid_for(c->n_elem * c->n * c->n)), dim3(BLOCK), 0, st,
                      c->d_mapP, c->d_GP[0], c->d_gpos, c->d_D, c->n, c->epw, c->n_elem, d_diag);
+  HIP_TRY(hipGetLastError());
+  return SEM_OK;
+}
+
+int sem_assemble(sem_ctx* c, const double* vals, double* out, int accumulate, void* stream) {
+  if (!c || !vals || !out) return fail(SEM_E_INVALID, "null argument");
+  if (!c->d_e2n) return fail(SEM_E_STATE, "sem_set_map must precede sem_assemble");
+  if (c->dpn != 1) return fail(SEM_E_INVALID, "sem_assemble: dofs_per_node == 1 only");
+  DeviceGuard g(c->device);
+  hipStream_t st = S(stream);
+  if (!accumulate) HIP_TRY(hipMemsetAsync(out, 0, c->n_node * sizeof(double), st));
+  const int64_t total = c->n_elem * c->n * c->n;
+  hipLaunchKernelGGL(k_assemble, dim3(grid_for(total)), dim3(BLOCK), 0, st, c->d_e2n, vals, total,
+                     out);
   HIP_TRY(hipGetLastError());
   return SEM_OK;
 }
@@ -1273,82 +1213,6 @@ int sem_det_inv_2x2(int64_t n, const double* d_mat, double* d_det, double* d_inv
   hipLaunchKernelGGL(k_det_inv_2x2, dim3(grid_for(n)), dim3(BLOCK), 0, S(stream), n, d_mat, d_det,
                      d_inv);
   HIP_TRY(hipGetLastError());
-  return SEM_OK;
-}
-
-int sem_pcg_solve(sem_ctx* c, int op_kind, const double* b, double* x, const uint8_t* mask,
-                  double rtol, int max_iter, int* iters, double* relres, void* stream) {
-  if (!c || !b || !x || !mask) return fail(SEM_E_INVALID, "null argument");
-  if (op_kind != SEM_OP_POISSON) return fail(SEM_E_NOTIMPL, "sem_pcg_solve: Poisson only");
-  DeviceGuard g(c->device);
-  hipStream_t st = S(stream);
-  const int64_t n = c->n_node;
-  if (c->cg_len != n) {
-    (void)hipFree(c->d_cg);
-    c->d_cg = nullptr;
-    c->cg_len = 0;
-    HIP_TRY(hipMalloc(&c->d_cg, 5 * n * sizeof(double)));
-    c->cg_len = n;
-  }
-  double* r = c->d_cg;
-  double* z = r + n;
-  double* p = z + n;
-  double* q = p + n;
-  double* d_diag = q + n;
-  int rc = sem_diag(c, op_kind, d_diag, stream);
-  if (rc) return rc;
-  double* partial = c->d_red;
-  double* scal = c->d_red + 2 * RED_BLOCKS;  // [alpha, beta, dot0, dot1]
-  const int gb = grid_for(n, BLOCK, RED_BLOCKS);
-  double h[2];
-  auto dot2 = [&](const double* a1, const double* b1, const double* a2, const double* b2) -> int {
-    hipLaunchKernelGGL(k_dot2, dim3(gb), dim3(BLOCK), 0, st, a1, b1, a2, b2, n, partial);
-    hipLaunchKernelGGL(k_finish2, dim3(1), dim3(BLOCK), 0, st, partial, gb, scal + 2);
-    HIP_TRY(hipMemcpyAsync(h, scal + 2, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    return SEM_OK;
-  };
-  // r = b - K x on free rows
-  if ((rc = sem_apply(c, op_kind, x, r, 0, stream))) return rc;
-  hipLaunchKernelGGL(k_residual, dim3(grid_for(n)), dim3(BLOCK), 0, st, b, r, mask, n);
-  hipLaunchKernelGGL(k_precond, dim3(grid_for(n)), dim3(BLOCK), 0, st, r, d_diag, mask, n, z);
-  HIP_TRY(hipMemcpyAsync(p, z, n * sizeof(double), hipMemcpyDeviceToDevice, st));
-  if ((rc = dot2(r, z, r, r))) return rc;
-  double rz = h[0];
-  const double r0 = std::sqrt(h[1]);
-  double res = r0;
-  int it = 0;
-  if (r0 == 0.0) {
-    if (iters) *iters = 0;
-    if (relres) *relres = 0.0;
-    return SEM_OK;
-  }
-  double hs[2];
-  while (it < max_iter && res > rtol * r0) {
-    if ((rc = sem_apply(c, op_kind, p, q, 0, stream))) return rc;
-    hipLaunchKernelGGL(k_mask, dim3(grid_for(n)), dim3(BLOCK), 0, st, q, mask, n);
-    if ((rc = dot2(p, q, nullptr, nullptr))) return rc;
-    const double alpha = rz / h[0];
-    hs[0] = alpha;
-    hs[1] = 0.0;
-    HIP_TRY(hipMemcpyAsync(scal, hs, 2 * sizeof(double), hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_update_xr, dim3(grid_for(n)), dim3(BLOCK), 0, st, x, r, p, q, scal, n);
-    hipLaunchKernelGGL(k_precond, dim3(grid_for(n)), dim3(BLOCK), 0, st, r, d_diag, mask, n, z);
-    if ((rc = dot2(r, z, r, r))) return rc;
-    const double beta = h[0] / rz;
-    rz = h[0];
-    res = std::sqrt(h[1]);
-    hs[0] = alpha;
-    hs[1] = beta;
-    HIP_TRY(hipMemcpyAsync(scal, hs, 2 * sizeof(double), hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_update_p, dim3(grid_for(n)), dim3(BLOCK), 0, st, p, z, scal, n);
-    HIP_TRY(hipStreamSynchronize(st));  // hs is reused by the next iteration's copy
-    ++it;
-  }
-  HIP_TRY(hipStreamSynchronize(st));
-  if (iters) *iters = it;
-  if (relres) *relres = res / r0;
-  if (res > rtol * r0) return fail(SEM_E_INVALID, "PCG did not converge");
   return SEM_OK;
 }
 

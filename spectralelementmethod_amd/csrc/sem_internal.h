@@ -23,3 +23,10 @@ void lagrange_eval(int n, const double* nodes, const double* bary, int64_t nx, c
 int invert(int n, const double* A, double* Ainv);
 
 }  // namespace sem
+
+// accessors of the operator context for the domain-decomposition layer
+// (sem_dd.hip)
+namespace sem {
+int64_t ctx_ndof(const sem_ctx* c);
+int ctx_device(const sem_ctx* c);
+}  // namespace sem

@@ -15,6 +15,9 @@ device tensors.  CPU tensors are accepted by the exchange layer only so that
 its protocol can be tested under the "gloo" backend; the operator itself has
 no CPU path.
 """
+import ctypes as C
+import os
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -189,9 +192,11 @@ class DistributedOperator(object):
 # ---------------------------------------------------------------- overlap
 def split_interface_elements(e2n, neighbors):
     """Split a rank's elements into the ones touching a partition interface
-    (computed first, so the interface sum can start) and the interior ones,
-    with the node states of include/sem_hip.h sem_set_map_shared:
-    returns (iface_elems, interior_elems, state_iface, state_interior)."""
+    and the interior ones, with the node states of include/sem_hip.h
+    sem_set_map_shared for applying the two sets IN ORDER into one y
+    (interface first): returns (iface_elems, interior_elems, state_iface,
+    state_interior).  The multi-GPU step (OverlappedOperator) instead runs
+    the two sets CONCURRENTLY into separate vectors (DDPlan)."""
     e2n = np.asarray(e2n)
     n_elem = e2n.shape[0]
     flat = e2n.reshape(n_elem, -1)
@@ -213,73 +218,352 @@ def split_interface_elements(e2n, neighbors):
     return ie, be, state_i, state_b
 
 
+class DDPlan(object):
+    """Host plan of one rank's ``sem_dd`` (include/sem_hip.h): which elements
+    touch a node shared with another rank (computed first, over a compact
+    renumbering of their nodes, on a side stream) and which are interior;
+    the compact <-> local DOF map; the compact DOFs exchanged with each peer
+    (in the order of ``neighbors[peer]``, which both sides agree on); the
+    DOFs another rank owns (left out of global dot products).
+
+    e2n: local element map [E, n, n]; neighbors: {peer rank: local node ids};
+    owned: bool [n_node] (None = all owned)."""
+
+    def __init__(self, e2n, n_node, neighbors, dofs_per_node=1, owned=None):
+        e2n = np.asarray(e2n)
+        self.dpn = dpn = int(dofs_per_node)
+        self.n_node = int(n_node)
+        self.ndof = dpn * self.n_node
+        flat = e2n.reshape(e2n.shape[0], -1).astype(np.int64)
+        shared = np.zeros(self.n_node, dtype=bool)
+        for nodes in neighbors.values():
+            shared[np.asarray(nodes, dtype=np.int64)] = True
+        touch = shared[flat].any(axis=1)
+        self.iface_elems = np.nonzero(touch)[0]
+        self.interior_elems = np.nonzero(~touch)[0]
+        self.iface_nodes = np.unique(flat[self.iface_elems])  # sorted local ids
+        self.e2n_iface = np.searchsorted(self.iface_nodes, flat[self.iface_elems]).astype(
+            np.uint32).reshape((self.iface_elems.size,) + e2n.shape[1:])
+        comp = np.arange(dpn, dtype=np.int64)
+        self.iface_dofs = (self.iface_nodes[:, None] * dpn + comp[None, :]).ravel().astype(
+            np.uint32)
+        self.peers = sorted(int(r) for r in neighbors)
+        counts, dofs = [], []
+        for r in self.peers:
+            nodes = np.asarray(neighbors[r], dtype=np.int64)
+            c = np.searchsorted(self.iface_nodes, nodes)
+            if nodes.size and (c.max() >= self.iface_nodes.size
+                               or not np.array_equal(self.iface_nodes[c], nodes)):
+                raise ValueError("shared node of peer %d is not on an element of this rank" % r)
+            dofs.append((c[:, None] * dpn + comp[None, :]).ravel())
+            counts.append(dofs[-1].size)
+        self.peer_counts = np.asarray(counts, dtype=np.int64)
+        self.peer_dofs = (np.concatenate(dofs) if dofs else np.zeros(0, np.int64)).astype(
+            np.uint32)
+        self.not_owned = None if owned is None else np.repeat(
+            ~np.asarray(owned, dtype=bool), dpn).astype(np.uint8)
+
+    @property
+    def exchanged_per_direction(self):
+        return int(self.peer_counts.sum())
+
+
+def dd_step_reference(plan, u, apply_iface, apply_interior, exchange):
+    """The sequence ``sem_dd_apply`` enqueues (csrc/sem_dd.hip), restated on
+    host tensors so the protocol can be checked under gloo without a GPU:
+    interface elements on the compact vector, pack, exchange, unpack, then
+    the interior result plus the interface result.  ``exchange(send, peers,
+    counts)`` returns the received buffer."""
+    cidx = torch.from_numpy(plan.iface_dofs.astype(np.int64))
+    pidx = torch.from_numpy(plan.peer_dofs.astype(np.int64))
+    y_c = apply_iface(u[cidx]) if cidx.numel() else torch.zeros(0, dtype=u.dtype)
+    send = y_c[pidx]
+    y = apply_interior(u) if plan.interior_elems.size else torch.zeros_like(u)
+    recv = exchange(send, plan.peers, plan.peer_counts)
+    off = np.concatenate([[0], np.cumsum(plan.peer_counts)])
+    for k in range(len(plan.peers)):  # one pass per peer: a DOF may have several
+        y_c.index_add_(0, pidx[off[k]:off[k + 1]], recv[off[k]:off[k + 1]])
+    y.index_add_(0, cidx, y_c)
+    return y
+
+
+def torch_p2p_exchange(send, peers, counts, group=None, recv=None):
+    """Point-to-point exchange of the packed interface values with every peer
+    through torch.distributed (one isend/irecv pair per peer, batched)."""
+    if recv is None:
+        recv = torch.empty_like(send)
+    off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    ops = []
+    for k, r in enumerate(peers):
+        a, b = int(off[k]), int(off[k + 1])
+        ops.append(dist.P2POp(dist.isend, send[a:b], r, group=group))
+        ops.append(dist.P2POp(dist.irecv, recv[a:b], r, group=group))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    return recv
+
+
+class TorchTransport(object):
+    """Caller-supplied transport of a ``sem_dd`` (sem_dd_set_transport) over
+    torch.distributed: the fallback when the native RCCL communicator cannot
+    be created, and the path the gloo tests drive on one GPU (several ranks
+    on one device; RCCL refuses duplicate GPUs).  With an NCCL (RCCL) process
+    group the buffers stay on the device and the collectives are ordered on
+    the library's side stream; with gloo they are staged through host
+    memory."""
+
+    def __init__(self, device, group=None):
+        self.lib = _lib.load()
+        self.group = group
+        self.device = torch.device(device)
+        self.on_device = "nccl" in str(dist.get_backend(group)).lower()
+        self._xfn = _lib.EXCHANGE_FN(self._exchange)
+        self._rfn = _lib.ALLREDUCE_FN(self._allreduce)
+        self._cache = {}
+        self.error = None
+        self._fullsync = os.environ.get("SEM_TT_FULLSYNC") == "1"  # diagnostic
+
+    def _bufs(self, key, n, stream):
+        """persistent staging buffers (allocated once, under the stream that
+        uses them, so the caching allocator never hands them to other work)"""
+        b = self._cache.get(key)
+        if b is None or b[0].numel() < n:
+            if self.on_device:
+                with torch.cuda.stream(stream):
+                    b = tuple(torch.empty(max(n, 1), dtype=torch.float64, device=self.device)
+                              for _ in range(2))
+            else:
+                b = tuple(torch.empty(max(n, 1), dtype=torch.float64).pin_memory()
+                          for _ in range(2))
+            self._cache[key] = b
+        return b[0][:n], b[1][:n]
+
+    def _sync(self, stream):
+        if self._fullsync:
+            torch.cuda.synchronize(self.device)
+        else:
+            stream.synchronize()
+
+    def _exchange(self, user, n_peers, peers, off, d_send, d_recv, side):
+        try:
+            peers_l = [peers[k] for k in range(n_peers)]
+            total = off[n_peers]
+            counts = [off[k + 1] - off[k] for k in range(n_peers)]
+            nb = 8 * total
+            stream = torch.cuda.ExternalStream(side, device=self.device) if side else \
+                torch.cuda.default_stream(self.device)
+            send, recv = self._bufs("x", total, stream)
+            _lib.check(self.lib.sem_copy_async(send.data_ptr(), d_send, nb, side))
+            if self.on_device:
+                with torch.cuda.stream(stream):
+                    torch_p2p_exchange(send, peers_l, counts, self.group, recv)
+                    _lib.check(self.lib.sem_copy_async(d_recv, recv.data_ptr(), nb, side))
+            else:
+                self._sync(stream)
+                torch_p2p_exchange(send, peers_l, counts, self.group, recv)
+                _lib.check(self.lib.sem_copy_async(d_recv, recv.data_ptr(), nb, side))
+                self._sync(stream)  # the host buffer is reused by the next call
+            return 0
+        except Exception as e:  # reported through the library's return code
+            self.error = e
+            return 1
+
+    def _allreduce(self, user, d_buf, count, st):
+        try:
+            nb = 8 * count
+            # NULL (None here) is the legacy default stream
+            stream = torch.cuda.ExternalStream(st, device=self.device) if st else \
+                torch.cuda.default_stream(self.device)
+            t, _ = self._bufs("r%d" % (st or 0), count, stream)
+            if self.on_device:
+                with torch.cuda.stream(stream):
+                    _lib.check(self.lib.sem_copy_async(t.data_ptr(), d_buf, nb, st))
+                    dist.all_reduce(t, group=self.group)
+                    _lib.check(self.lib.sem_copy_async(d_buf, t.data_ptr(), nb, st))
+            else:
+                _lib.check(self.lib.sem_copy_async(t.data_ptr(), d_buf, nb, st))
+                self._sync(stream)
+                dist.all_reduce(t, group=self.group)
+                _lib.check(self.lib.sem_copy_async(d_buf, t.data_ptr(), nb, st))
+                self._sync(stream)
+            return 0
+        except Exception as e:
+            self.error = e
+            return 1
+
+    def install(self, dd, world, rank):
+        _lib.check(self.lib.sem_dd_set_transport(dd, C.cast(self._xfn, C.c_void_p),
+                                                 C.cast(self._rfn, C.c_void_p), None, world,
+                                                 rank))
+
+
+def init_rccl(dd, world, rank, group=None):
+    """Native transport: one RCCL communicator over all ranks (collective:
+    every rank calls it).  Rank 0 draws the id, torch.distributed carries it."""
+    lib = _lib.load()
+    buf = C.create_string_buffer(_lib.RCCL_ID_BYTES)
+    if rank == 0:
+        _lib.check(lib.sem_rccl_unique_id(buf, _lib.RCCL_ID_BYTES))
+    obj = [buf.raw if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    buf = C.create_string_buffer(obj[0], _lib.RCCL_ID_BYTES)
+    _lib.check(lib.sem_dd_init_rccl(dd, buf, world, rank))
+
+
 class OverlappedOperator(object):
-    """Rank-local operator whose interface sum overlaps the interior
-    elements: interface elements are applied first, an
-    event releases the RCCL exchange on a side stream, and the interior
-    elements run meanwhile on the caller's stream.  Interface nodes are
-    touched only by interface elements, so the exchange's scatter-add never
-    races the interior kernel."""
+    """One rank's part of the global operator.
+
+    Single rank (``world`` 1): one ``SEMOperator``.  Several ranks: a native
+    ``sem_dd`` (csrc/sem_dd.hip) holding two operators -- the interface
+    elements over a compact numbering of their nodes, applied on a side
+    stream and summed with the neighbours, and the interior elements applied
+    meanwhile on the caller's stream -- so one ``step`` is one C call.
+
+    transport: "rccl" (native RCCL send/recv + all-reduce), "torch"
+    (torch.distributed point-to-point, see TorchTransport), or "auto"
+    (RCCL when the process group is NCCL and the communicator comes up,
+    torch otherwise)."""
 
     def __init__(self, p, nodes, e2n, neighbors, dofs_per_node=1, device=None, group=None,
-                 geometry="auto", kind=0, kernel="auto"):
+                 geometry="auto", kind=0, kernel="auto", owned=None, transport="auto",
+                 world=None, rank=None):
         from .operators import SEMOperator
         self.dpn = dofs_per_node
         self.kind = kind
         self.device = torch.device(device) if device is not None else torch.device("cuda")
+        self._lib = _lib.load()
         e2n = np.asarray(e2n)
-        n_node = np.asarray(nodes).shape[1]
-        ie, be, st_i, st_b = split_interface_elements(e2n, neighbors)
-        if st_i.size < n_node:  # nodes beyond the last referenced one
-            pad = n_node - st_i.size
-            st_i = np.concatenate([st_i, np.zeros(pad, np.uint8)])
-            st_b = np.concatenate([st_b, np.full(pad, _lib.NODE_OTHER, np.uint8)])
-        self.n_iface_elem, self.n_interior_elem = ie.size, be.size
-        if ie.size == 0 or be.size == 0:  # nothing to overlap
-            self.ops = [SEMOperator(p, e2n, nodes, dofs_per_node, device=self.device,
-                                    geometry=geometry, kernel=kernel)]
+        nodes = np.asarray(nodes)
+        n_node = nodes.shape[1]
+        self.world = world if world is not None else (
+            dist.get_world_size(group) if dist.is_initialized() else 1)
+        self.rank = rank if rank is not None else (dist.get_rank(group) if dist.is_initialized()
+                                                   else 0)
+        self.n_elem = e2n.shape[0]
+        self.ndof = dofs_per_node * n_node
+        self.dd = None
+        self.transport = "none"
+        self.exchange_bytes = 0
+        kw = dict(dofs_per_node=dofs_per_node, device=self.device, geometry=geometry,
+                  kernel=kernel)
+        if self.world == 1:
+            self.ops = [SEMOperator(p, e2n, nodes, **kw)]
+            self.n_iface_elem, self.n_interior_elem = 0, self.n_elem
+            self.plan = None
         else:
-            self.ops = [SEMOperator(p, e2n[ie], nodes, dofs_per_node, device=self.device,
-                                    geometry=geometry, node_state=st_i, kernel=kernel),
-                        SEMOperator(p, e2n[be], nodes, dofs_per_node, device=self.device,
-                                    geometry=geometry, node_state=st_b, kernel=kernel)]
+            self.plan = pl = DDPlan(e2n, n_node, neighbors, dofs_per_node, owned)
+            self.n_iface_elem, self.n_interior_elem = pl.iface_elems.size, pl.interior_elems.size
+            self.iface = SEMOperator(p, pl.e2n_iface, nodes[:, pl.iface_nodes], **kw) \
+                if pl.iface_elems.size else None
+            self.interior = SEMOperator(p, e2n[pl.interior_elems], nodes, **kw) \
+                if pl.interior_elems.size else None
+            self.ops = [o for o in (self.iface, self.interior) if o is not None]
+            dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(self.device)  # noqa: E731
+            cidx = dev(pl.iface_dofs.view(np.int32))
+            pidx = dev(pl.peer_dofs.view(np.int32))
+            notown = dev(pl.not_owned) if pl.not_owned is not None else None
+            peers = (C.c_int * max(1, len(pl.peers)))(*pl.peers)
+            counts = (C.c_int64 * max(1, len(pl.peers)))(*pl.peer_counts.tolist())
+            dd = C.c_void_p()
+            _lib.check(self._lib.sem_dd_create(
+                C.byref(dd), self.iface._ctx if self.iface else None,
+                self.interior._ctx if self.interior else None, self.ndof, _lib.tptr(cidx),
+                int(pl.iface_dofs.size), len(pl.peers), peers, counts, _lib.tptr(pidx),
+                _lib.tptr(notown), self.device.index))
+            self.dd = dd
+            self.exchange_bytes = 8 * pl.exchanged_per_direction
+            self._install_transport(transport, group)
         for op in self.ops:
             op.compute_geometry(kind)
-        self.ndof = self.ops[0].ndof
-        self.n_elem = e2n.shape[0]
-        self.xchg = InterfaceExchange(neighbors, dofs_per_node, self.device, group) \
-            if neighbors else None
-        self.side = torch.cuda.Stream(device=self.device)
-        self.ready = torch.cuda.Event()
-        self._lib = _lib.load()
+
+    def _install_transport(self, transport, group):
+        backend = str(dist.get_backend(group)).lower()
+        if transport not in ("auto", "rccl", "torch"):
+            raise ValueError("transport must be auto, rccl or torch")
+        if transport == "rccl" or (transport == "auto" and "nccl" in backend):
+            try:
+                init_rccl(self.dd, self.world, self.rank, group)
+                self.transport = "rccl"
+                return
+            except Exception as e:
+                if transport == "rccl":
+                    raise
+                import sys
+                print("[sem] native RCCL transport unavailable (%s); using torch.distributed" % e,
+                      file=sys.stderr, flush=True)
+        self._torch = TorchTransport(self.device, group)
+        self._torch.install(self.dd, self.world, self.rank)
+        self.transport = "torch-" + ("device" if self._torch.on_device else "host")
+
+    def close(self):
+        if self.dd:
+            self._lib.sem_dd_destroy(self.dd)
+            self.dd = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc and getattr(self, "_torch", None) is not None and self._torch.error is not None:
+            err, self._torch.error = self._torch.error, None
+            raise RuntimeError("interface transport failed: %r" % (err,))
+        _lib.check(rc)
 
     def plan_info(self):
-        return self.ops[-1].plan_info()
+        return (self.interior or self.iface).plan_info() if self.dd else self.ops[0].plan_info()
 
     def step(self, u, y, events=None):
-        """y = K u on this rank's nodes, interface sum included.  ``events``
-        (start, end) bracket the element kernels on the caller's stream."""
+        """y = K u on this rank's DOFs, shared DOFs summed over all ranks.
+        ``events`` (start, end) bracket the step on the caller's stream."""
         main = torch.cuda.current_stream(self.device)
         sp = _lib.stream_ptr(main)
-        up, yp = _lib.tptr(u), _lib.tptr(y)
-        last = len(self.ops) - 1
-        for i, op in enumerate(self.ops):
-            _lib.check(self._lib.sem_zero_shared(op._ctx, yp, sp))
-            if events is not None and i == 0:
-                events[0].record(main)
-            _lib.check(self._lib.sem_apply(op._ctx, self.kind, up, yp, _lib.APPLY_SKIP_ZERO, sp))
-            if i == 0 and self.xchg is not None:
-                self.ready.record(main)
-            if events is not None and i == last:
-                events[1].record(main)
-        if self.xchg is not None:
-            with torch.cuda.stream(self.side):
-                self.side.wait_event(self.ready)
-                self.xchg.exchange(y)
-            main.wait_stream(self.side)
+        if events is not None:
+            events[0].record(main)
+        if self.dd:
+            self._check(self._lib.sem_dd_apply(self.dd, self.kind, _lib.tptr(u), _lib.tptr(y),
+                                               sp))
+        else:
+            _lib.check(self._lib.sem_apply(self.ops[0]._ctx, self.kind, _lib.tptr(u),
+                                           _lib.tptr(y), 0, sp))
+        if events is not None:
+            events[1].record(main)
         return y
 
     def apply(self, u, out=None):
         if out is None:
             out = torch.empty_like(u)
         return self.step(u, out)
+
+    def diag(self):
+        d = torch.empty(self.ndof, dtype=torch.float64, device=self.device)
+        sp = _lib.stream_ptr(torch.cuda.current_stream(self.device))
+        if self.dd:
+            self._check(self._lib.sem_dd_diag(self.dd, self.kind, _lib.tptr(d), sp))
+        else:
+            _lib.check(self._lib.sem_diag(self.ops[0]._ctx, self.kind, _lib.tptr(d), sp))
+        return d
+
+    def pcg_solve(self, rhs, x, dirichlet, rtol=1e-13, max_iter=20000,
+                  check_every=_lib.PCG_CHECK_EVERY):
+        """Jacobi-PCG for K x = rhs on this rank's DOFs (dirichlet: bool mask;
+        x holds the Dirichlet values and the initial guess, updated in place).
+        Returns (x, iterations executed, final relative residual)."""
+        mask = torch.as_tensor(dirichlet, dtype=torch.bool).to(self.device).to(torch.uint8)
+        its, rel = C.c_int(0), C.c_double(0.0)
+        sp = _lib.stream_ptr(torch.cuda.current_stream(self.device))
+        if self.dd:
+            self._check(self._lib.sem_dd_pcg_solve(
+                self.dd, self.kind, _lib.tptr(rhs), _lib.tptr(x), _lib.tptr(mask), float(rtol),
+                int(max_iter), int(check_every), C.byref(its), C.byref(rel), sp))
+        else:
+            _lib.check(self._lib.sem_pcg_solve(self.ops[0]._ctx, self.kind, _lib.tptr(rhs),
+                                               _lib.tptr(x), _lib.tptr(mask), float(rtol),
+                                               int(max_iter), C.byref(its), C.byref(rel), sp))
+        return x, its.value, rel.value
+
+
+DomainOperator = OverlappedOperator

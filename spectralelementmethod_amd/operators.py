@@ -95,9 +95,9 @@ class SEMOperator(object):
         sem_set_geom_mode.
     kernel : {"auto", "column", "mfma"}
         Kernel family of the Poisson action: the LDS column kernel or the
-        fp64 matrix-core element kernel (p <= 15, stored factors); "auto"
-        (default) resolves to the library's measured choice (mfma for
-        12 <= p <= 15 with stored geometry).  See include/sem_hip.h
+        fp64 matrix-core element kernel (p <= 15); "auto" (default) resolves
+        to the library's measured choice (mfma for 13 <= p <= 15 unless nodal
+        geometry is requested).  See include/sem_hip.h
         sem_set_kernel.
     node_state : array-like uint8 [n_node], optional
         For operators that share the output vector with others applied
@@ -282,6 +282,8 @@ class SEMOperator(object):
                   and out.numel() == self.ndof):
             raise TypeError("out must be a contiguous float64 tensor of %d entries on %s"
                             % (self.ndof, self.device))
+        if out.data_ptr() == u.data_ptr():
+            raise ValueError("apply: out must not alias u (the kernels read u while writing out)")
         with torch.cuda.device(self.device):
             flags = (_lib.APPLY_ACCUMULATE if accumulate else 0) | \
                 (_lib.APPLY_LINEARIZE if linearize else 0)
@@ -289,6 +291,25 @@ class SEMOperator(object):
                                            self._stream(stream)))
         if is_np:
             return out.cpu().numpy()
+        return out
+
+    def assemble(self, elem_vals, out=None, accumulate=False, stream=None):
+        """Sum element-local nodal values [E, n, n] through the element map
+        into a global vector (sem_assemble): the reference's RHS assembly
+        grhs[inds] += lrhs (examples/poisson.py:219-243), e.g. the f = 1 load
+        vector from geometry_fields()["detJxW"]."""
+        if self.dpn != 1:
+            raise NotImplementedError("assemble: dofs_per_node == 1")
+        v = torch.as_tensor(elem_vals, dtype=torch.float64).to(self.device).contiguous()
+        if tuple(v.shape) != (self.n_elem, self.n, self.n):
+            raise ValueError("element values must have shape [%d, %d, %d]" % (self.n_elem, self.n,
+                                                                               self.n))
+        if out is None:
+            out = torch.empty(self.ndof, dtype=torch.float64, device=self.device)
+            accumulate = False
+        with torch.cuda.device(self.device):
+            _lib.check(self._lib.sem_assemble(self._ctx, _lib.tptr(v), _lib.tptr(out),
+                                              1 if accumulate else 0, self._stream(stream)))
         return out
 
     def diag(self, kind=POISSON, stream=None):
@@ -303,8 +324,11 @@ class SEMOperator(object):
     def pcg_solve(self, rhs, x, dirichlet, rtol=1e-13, max_iter=20000, kind=POISSON,
                   stream=None):
         """Solve K x = rhs on the free DOFs (``dirichlet`` True => x fixed)
-        with Jacobi-preconditioned CG on the device.  ``x`` (device tensor) is
-        updated in place and returned with (iterations, relative residual)."""
+        with Jacobi-preconditioned CG on the device (sem_pcg_solve: every
+        scalar stays on the device, convergence read every 16 iterations;
+        rtol = 0 runs exactly max_iter iterations).  ``x`` (device tensor) is
+        updated in place and returned with (iterations executed, relative
+        residual).  Raises ValueError when not converged."""
         kind = op_kind(kind)
         if _geom_key(kind) not in self._geom_ready:
             self.compute_geometry(kind, stream=stream)

@@ -114,6 +114,108 @@ def test_strip_partition_bookkeeping():
         StripPartition(3, 4, 2, 4, 0)
 
 
+def _dd_worker(rank, world, port, mode, q):
+    """The overlapped multi-GPU step's protocol (DDPlan + the sequence
+    sem_dd_apply enqueues, dd_step_reference) with oracle stand-ins for the
+    two device operators, under gloo."""
+    import sys
+    for pth in (ROOT, os.path.join(ROOT, "oracle")):
+        if pth not in sys.path:
+            sys.path.insert(0, pth)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sem_oracle
+        from spectralelementmethod_amd import meshgen
+        from spectralelementmethod_amd.distributed import (DDPlan, GenericPartition,
+                                                           StripPartition, dd_step_reference,
+                                                           torch_p2p_exchange)
+        gll = np.load(os.path.join(ROOT, "tests", "golden", "gll.npz"))
+        p, nex, ney = 3, 9, 4
+        half = gll["half_%d" % p]
+        gnodes, ge2n = meshgen.structured_square(nex, ney, p, warp=0.05)
+        u_glob = np.random.default_rng(5).standard_normal(gnodes.shape[1])
+        y_glob = sem_oracle.PoissonProblem(gnodes, ge2n, half).apply(u_glob)
+        if mode == "strip":
+            part = StripPartition(nex, ney, p, world, rank)
+            nodes, e2n = part.local_mesh(0.05)
+        else:
+            rng = np.random.default_rng(8)
+            elem_rank = rng.integers(0, world, size=ge2n.shape[0])
+            part = GenericPartition(ge2n, elem_rank, world, rank)
+            e2n, nodes = part.e2n_local, gnodes[:, part.l2g]
+        plan = DDPlan(e2n, nodes.shape[1], part.neighbors, 1, part.owned)
+        # interface elements over the compact node numbering, interior over the local one
+        op_i = sem_oracle.PoissonProblem(nodes[:, plan.iface_nodes], plan.e2n_iface, half) \
+            if plan.iface_elems.size else None
+        op_b = sem_oracle.PoissonProblem(nodes, e2n[plan.interior_elems], half) \
+            if plan.interior_elems.size else None
+        l2g = part.local_to_global()
+        u = torch.from_numpy(u_glob[l2g].copy())
+        y = dd_step_reference(
+            plan, u, lambda uc: torch.from_numpy(op_i.apply(uc.numpy())),
+            lambda ul: torch.from_numpy(op_b.apply(ul.numpy())),
+            lambda send, peers, counts: torch_p2p_exchange(send, peers, counts))
+        err = np.abs(y.numpy() - y_glob[l2g]).max() / np.abs(y_glob).max()
+        own = torch.from_numpy(np.asarray(plan.not_owned == 0))
+        d = torch.sum(u[own] * y[own]).reshape(1)
+        dist.all_reduce(d)
+        q.put((rank, err, d.item(), float(np.dot(u_glob, y_glob)),
+               plan.exchanged_per_direction, len(plan.peers)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,mode", [(2, "strip"), (3, "strip"), (2, "generic"),
+                                        (4, "generic")])
+def test_overlapped_protocol_gloo(world, mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dd_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    for rank, err, d, d_ref, nx, npeer in res:
+        assert err < 1e-14, (rank, err)
+        assert abs(d - d_ref) <= 1e-12 * abs(d_ref)
+        assert nx > 0 and npeer >= 1
+
+
+def test_ddplan_bookkeeping():
+    """DDPlan (host side of sem_dd): compact interface numbering, peer lists
+    in compact DOFs that map back to the partition's shared nodes, owned DOFs,
+    and dpn = 2 interleaving."""
+    from spectralelementmethod_amd.distributed import DDPlan, StripPartition
+    for dpn in (1, 2):
+        for rank in range(3):
+            part = StripPartition(12, 4, 3, 3, rank, dofs_per_node=dpn)
+            nodes, e2n = part.local_mesh(0.05)
+            pl = DDPlan(e2n, part.n_nodes, part.neighbors, dpn, part.owned)
+            assert pl.iface_elems.size == len(part.neighbors) * part.ney
+            assert np.union1d(pl.iface_elems, pl.interior_elems).size == e2n.shape[0]
+            # compact map reproduces the local map of the interface elements
+            assert np.array_equal(pl.iface_nodes[pl.e2n_iface], e2n[pl.iface_elems])
+            assert pl.iface_dofs.size == dpn * pl.iface_nodes.size
+            off = np.concatenate([[0], np.cumsum(pl.peer_counts)])
+            for k, r in enumerate(pl.peers):
+                cd = pl.peer_dofs[off[k]:off[k + 1]].astype(np.int64)
+                ld = pl.iface_dofs[cd].astype(np.int64)
+                nodes_back = ld[::dpn] // dpn
+                assert np.array_equal(nodes_back, part.neighbors[r])
+                assert np.array_equal(ld % dpn, np.tile(np.arange(dpn), part.Ny))
+            # shared nodes are touched by interface elements only
+            iface = np.concatenate(list(part.neighbors.values()))
+            assert not np.isin(iface, e2n[pl.interior_elems]).any()
+            assert pl.not_owned.sum() == (dpn * part.Ny if rank > 0 else 0)
+    with pytest.raises(ValueError):  # a shared node no element of the rank references
+        DDPlan(e2n, part.n_nodes + 1, {0: np.array([0, part.n_nodes])}, 1)
+
+
 def test_split_interface_elements():
     """Interface / interior element split and node states of the overlapped
     multi-GPU operator (host logic)."""
