@@ -143,7 +143,9 @@ def test_single_rank_overlapped_is_plain_operator(gpu):
     full = SEMOperator(5, e2n, nodes, device=gpu)
     u = torch.randn(full.ndof, dtype=torch.float64, device=gpu,
                     generator=torch.Generator(device=gpu).manual_seed(3))
-    assert torch.equal(op.apply(u), full.apply(u))
+    # (this small mesh has atomic-fallback groups: equal up to summation order)
+    a, b = op.apply(u), full.apply(u)
+    assert (a - b).norm().item() <= 1e-14 * b.norm().item()
     assert op.dd is None and op.transport == "none"
 
 
