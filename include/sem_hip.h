@@ -273,6 +273,35 @@ int sem_pcg_solve(sem_ctx* ctx, int op_kind, const double* d_b, double* d_x,
                   int* iters, double* final_relres, void* stream);
 
 /* ------------------------------------------------------------------ */
+/* Static condensation (DOFManagerSC, sem/discrete.py:283-528)         */
+/* ------------------------------------------------------------------ */
+/* Element Schur complements of local systems in hierarchical order
+ * (exterior DOFs first; DOFManagerSC.reorder_local_system_hier), all
+ * elements in one launch: compute_local_sc_system (sem/discrete.py:428-466)
+ *   S_e = A_ee - A_ei A_ii^-1 A_ie,  s_e = b_e - A_ei A_ii^-1 b_i.
+ * d_mat [n_elem][nl][nl], d_rhs [n_elem][nl] -> d_sc_mat [n_elem][ne][ne],
+ * d_sc_rhs [n_elem][ne]; d_work [n_elem][nl-ne][nl+1] keeps
+ * A_ii^-1 [A_ie | b_i] for sem_schur_backsolve.  Gauss-Jordan with partial
+ * pivoting, one workgroup per element (nl - ne <= 512).  SEM_E_INVALID
+ * (count in *n_singular) when an interior block is singular. */
+int sem_schur_batched(int64_t n_elem, int nl, int ne, const double* d_mat, const double* d_rhs,
+                      double* d_work, double* d_sc_mat, double* d_sc_rhs, int64_t* n_singular,
+                      void* stream);
+/* Interior DOFs from the exterior ones, x_i = A_ii^-1 (b_i - A_ie x_e)
+ * (_solve_interior_dofs, sem/discrete.py:512-524): d_xe [n_elem][ne] ->
+ * d_xi [n_elem][nl-ne], from the d_work of sem_schur_batched. */
+int sem_schur_backsolve(int64_t n_elem, int nl, int ne, const double* d_work, const double* d_xe,
+                        double* d_xi, void* stream);
+/* Jacobi-PCG (as sem_pcg_solve) on an assembled symmetric positive definite
+ * CSR matrix (device int64 row pointers, int32 columns, float64 values):
+ * the condensed exterior system of _solve_boundary_dofs
+ * (sem/discrete.py:502-510, a scipy spsolve in the reference). */
+int sem_csr_pcg_solve(int64_t n, const int64_t* d_rowptr, const int32_t* d_colind,
+                      const double* d_val, const double* d_b, double* d_x,
+                      const uint8_t* d_dirichlet, double rtol, int max_iter, int* iters,
+                      double* final_relres, int device, void* stream);
+
+/* ------------------------------------------------------------------ */
 /* Domain decomposition across GPUs (one process per GPU)              */
 /* ------------------------------------------------------------------ */
 /* The reference's element loop (sem/discrete.py:189-209) is serial; its

@@ -7,7 +7,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_NAME = "libsem_hip.so"
 LIB_PATH = os.environ.get("SEM_LIB_PATH", os.path.join(PKG_DIR, LIB_NAME))
-SOURCES = ["sem_device.hip", "sem_dd.hip", "sem_basis.cpp"]
+SOURCES = ["sem_device.hip", "sem_dd.hip", "sem_sc.hip", "sem_basis.cpp"]
 DEPS = SOURCES + ["sem_internal.h", "sem_kernels.h", "gll_table.h"]
 ARCH = os.environ.get("SEM_OFFLOAD_ARCH", "gfx950")
 

@@ -74,6 +74,11 @@ SIGNATURES = {
     "sem_scatter_add": (C.c_int, [_vp, _vp, _i64, _vp, _vp]),
     "sem_pcg_solve": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, C.c_double, C.c_int,
                                 C.POINTER(C.c_int), C.POINTER(C.c_double), _vp]),
+    "sem_schur_batched": (C.c_int, [_i64, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp,
+                                    C.POINTER(_i64), _vp]),
+    "sem_schur_backsolve": (C.c_int, [_i64, C.c_int, C.c_int, _vp, _vp, _vp, _vp]),
+    "sem_csr_pcg_solve": (C.c_int, [_i64, _vp, _vp, _vp, _vp, _vp, _vp, C.c_double, C.c_int,
+                                    C.POINTER(C.c_int), C.POINTER(C.c_double), C.c_int, _vp]),
     "sem_rccl_unique_id": (C.c_int, [_vp, C.c_int]),
     "sem_copy_async": (C.c_int, [_vp, _vp, _i64, _vp]),
     "sem_dd_create": (C.c_int, [C.POINTER(_vp), _vp, _vp, _i64, _vp, _i64, C.c_int,

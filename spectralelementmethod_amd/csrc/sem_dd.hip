@@ -203,6 +203,28 @@ __global__ void k_cg_record(const double* __restrict__ rr, double* __restrict__ 
   if (threadIdx.x == 0) *hist = *rr;
 }
 
+// y = A x for a CSR matrix (one thread per row; the condensed exterior
+// systems of static condensation have a few tens of entries per row)
+__global__ void k_csr_spmv(int64_t n, const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                           const double* __restrict__ v, const double* __restrict__ x,
+                           double* __restrict__ y) {
+  for (int64_t r = blockIdx.x * (int64_t)BLK + threadIdx.x; r < n; r += (int64_t)gridDim.x * BLK) {
+    double acc = 0.0;
+    for (int64_t k = rp[r]; k < rp[r + 1]; ++k) acc = fma(v[k], x[ci[k]], acc);
+    y[r] = acc;
+  }
+}
+
+__global__ void k_csr_diag(int64_t n, const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                           const double* __restrict__ v, double* __restrict__ d) {
+  for (int64_t r = blockIdx.x * (int64_t)BLK + threadIdx.x; r < n; r += (int64_t)gridDim.x * BLK) {
+    double acc = 0.0;
+    for (int64_t k = rp[r]; k < rp[r + 1]; ++k)
+      if (ci[k] == r) acc += v[k];
+    d[r] = acc;
+  }
+}
+
 __global__ void k_scatter_add_peer(double* __restrict__ dst, const uint32_t* __restrict__ idx,
                                    int64_t n, const double* __restrict__ src) {
   for (int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x; t < n; t += (int64_t)gridDim.x * BLK)
@@ -329,9 +351,17 @@ int dd_allreduce(sem_dd* d, double* buf, int count, hipStream_t st) {
 struct PcgOp {
   sem_ctx* ctx = nullptr;  // single GPU
   sem_dd* dd = nullptr;    // or a rank of a decomposition
+  const int64_t* rp = nullptr;  // or an assembled CSR matrix
+  const int32_t* ci = nullptr;
+  const double* v = nullptr;
   int64_t n = 0;
   int device = 0;
   int apply(int kind, const double* p, double* q, hipStream_t st) const {
+    if (rp) {
+      hipLaunchKernelGGL(k_csr_spmv, dim3(grid_for(n)), dim3(BLK), 0, st, n, rp, ci, v, p, q);
+      HIP_TRY(hipGetLastError());
+      return SEM_OK;
+    }
     if (dd) {
       SEM_TRY(dd_begin(dd, kind, false, p, q, st));
       SEM_TRY(dd_exchange(dd));
@@ -340,6 +370,11 @@ struct PcgOp {
     return sem_apply(ctx, kind, p, q, 0, st);
   }
   int diag(int kind, double* out, hipStream_t st) const {
+    if (rp) {
+      hipLaunchKernelGGL(k_csr_diag, dim3(grid_for(n)), dim3(BLK), 0, st, n, rp, ci, v, out);
+      HIP_TRY(hipGetLastError());
+      return SEM_OK;
+    }
     if (dd) {
       SEM_TRY(dd_begin(dd, kind, true, nullptr, out, st));
       SEM_TRY(dd_exchange(dd));
@@ -370,7 +405,7 @@ int pcg_run(const PcgOp& op, int kind, const double* b, double* x, const uint8_t
             const uint8_t* notown, double rtol, int max_iter, int check, int* iters,
             double* relres, hipStream_t st) {
   if (!b || !x || !dir) return fail(SEM_E_INVALID, "null argument");
-  if (kind != SEM_OP_POISSON) return fail(SEM_E_NOTIMPL, "PCG: Poisson only");
+  if (kind != SEM_OP_POISSON && !op.rp) return fail(SEM_E_NOTIMPL, "PCG: Poisson only");
   // rtol = 0: run exactly max_iter iterations (benchmarking)
   if (max_iter < 0 || !(rtol >= 0.0)) return fail(SEM_E_INVALID, "need rtol >= 0, max_iter >= 0");
   if (check < 1) check = 1;
@@ -455,6 +490,22 @@ int sem_pcg_solve(sem_ctx* c, int op_kind, const double* b, double* x, const uin
   op.device = sem::ctx_device(c);
   return pcg_run(op, op_kind, b, x, mask, nullptr, rtol, max_iter, SEM_PCG_CHECK_EVERY, iters,
                  relres, S(stream));
+}
+
+int sem_csr_pcg_solve(int64_t n, const int64_t* d_rowptr, const int32_t* d_colind,
+                      const double* d_val, const double* d_b, double* d_x,
+                      const uint8_t* d_dirichlet, double rtol, int max_iter, int* iters,
+                      double* final_relres, int device, void* stream) {
+  if (n < 1 || !d_rowptr || !d_colind || !d_val)
+    return fail(SEM_E_INVALID, "sem_csr_pcg_solve: bad matrix");
+  PcgOp op;
+  op.rp = d_rowptr;
+  op.ci = d_colind;
+  op.v = d_val;
+  op.n = n;
+  op.device = device;
+  return pcg_run(op, SEM_OP_POISSON, d_b, d_x, d_dirichlet, nullptr, rtol, max_iter,
+                 SEM_PCG_CHECK_EVERY, iters, final_relres, S(stream));
 }
 
 int sem_copy_async(void* dst, const void* src, int64_t nbytes, void* stream) {

@@ -376,6 +376,13 @@ void launch_geom_n(sem_ctx* c, const double* nodes, int op_kind, double* GP, dou
                      J, iJ, dJ, dJW, XG, XG ? c->d_owner : nullptr, XGin, c->d_bad);
 }
 
+#ifdef SEM_ONLY_N  // diagnostic variant builds: one order only (fast compiles)
+#define SEM_DISPATCH_N(n, FN, ...)                   \
+  switch (n) {                                       \
+    case SEM_ONLY_N: FN<SEM_ONLY_N>(__VA_ARGS__); break; \
+    default: break;                                  \
+  }
+#else
 #define SEM_DISPATCH_N(n, FN, ...)       \
   switch (n) {                           \
     case 2: FN<2>(__VA_ARGS__); break;   \
@@ -396,6 +403,7 @@ void launch_geom_n(sem_ctx* c, const double* nodes, int op_kind, double* GP, dou
     case 17: FN<17>(__VA_ARGS__); break; \
     default: break;                      \
   }
+#endif
 
 int check_op(sem_ctx* c, int op_kind) {
   if (op_kind == SEM_OP_POISSON) {

@@ -13,9 +13,13 @@ them one element at a time.  Here the element loop is one GPU launch:
 * ``finite_elements()`` still yields per-element ``FiniteElement`` objects
   with the reference's properties, but their geometry (x_phys, J, invJ,
   detJ, detJxW) comes from one batched device computation;
-* ``DOFManagerSC.solve_poisson`` solves the assembled Poisson system with
-  matrix-free Jacobi-PCG on the GPU; the reference's static-condensation
-  solve (:404-528) gives the same solution (tests/test_gpu_parity.py).
+* ``DOFManagerSC`` keeps the reference's static-condensation API
+  (init_global_linear_system, reorder_local_system_hier,
+  compute_local_sc_system, assemble_global_sc_system, solve; :404-528) with
+  the element Schur complements and interior back-solves as batched device
+  launches and the condensed system solved by device PCG;
+  ``DOFManagerSC.solve_poisson`` solves the same assembled Poisson system
+  matrix-free (Jacobi-PCG on the GPU, no element matrices at all).
 
 Node reorderings (RCM, static-condensation ordering) are host-side setup and
 reproduce the reference's permutations exactly.
@@ -509,6 +513,134 @@ class DOFManagerSC(DOFManager):
         perm[n_ext:] = np.arange(n_ext, mesh.n_nodes)
         mesh._permute_nodes(perm)
 
+    # -------------------------------------------------- static condensation
+    # The reference's API (sem/discrete.py:404-528), same names, arguments and
+    # results; the per-element dense linear algebra runs as one batched device
+    # launch (csrc/sem_sc.hip) instead of a Python loop of scipy.linalg.solve.
+    def _cell_dofs_hier(self):
+        """Global DOFs of every cell in hierarchical order (exterior first):
+        FiniteElement.global_dof_ind_hier for all cells, [E, n_nodes * dpn]."""
+        mesh = self._mesh
+        geo = mesh._geometries[mesh._geom_ids[0]]
+        e2n = mesh.element_map()
+        h = geo.hierarchical_node_order
+        nodes = e2n.reshape(e2n.shape[0], -1)[:, h].astype(np.int64)
+        dpn = self._dpn
+        return (nodes[:, :, None] * dpn + np.arange(dpn)[None, None, :]).reshape(
+            nodes.shape[0], -1), geo.n_exterior_nodes * dpn
+
+    def init_global_linear_system(self):
+        """Zero COO matrix over the element-exterior DOFs and a zero RHS
+        (sem/discrete.py:404-426)."""
+        _, ne = self._cell_dofs_hier()
+        n_mat_entries = self._mesh.n_cells * ne ** 2
+        row_col = np.zeros((2, n_mat_entries), dtype=np.uint32)
+        entries = np.zeros(n_mat_entries, dtype=np.float64)
+        ndof_ext = self.ndof_exterior
+        return Static_COO_Matrix(entries, row_col, (ndof_ext, ndof_ext)), \
+            np.zeros(ndof_ext, dtype=np.float64)
+
+    @staticmethod
+    def reorder_local_system_hier(fe, local_system):
+        """Lexicographic local system -> hierarchical DOF order, exterior
+        first (sem/discrete.py:428-436)."""
+        lmat, lrhs = local_system
+        hier = fe.loc_dof_ind_hier
+        return lmat[np.ix_(hier, hier)], lrhs[hier]
+
+    @staticmethod
+    def compute_local_sc_system(fe, local_system):
+        """Schur complement system of one element's hierarchical local system
+        (sem/discrete.py:438-472), on the device."""
+        S, s, _ = _schur_batched([local_system], fe.ndof_exterior)
+        return S[0].cpu().numpy(), s[0].cpu().numpy()
+
+    def assemble_global_sc_system(self, global_sc_system, local_systems):
+        """Element Schur complements of all local systems (one batched
+        device launch) assembled into the COO system from
+        init_global_linear_system (sem/discrete.py:474-500)."""
+        gmat, grhs = global_sc_system
+        dofs, ne = self._cell_dofs_hier()
+        local_systems = list(local_systems) if not isinstance(local_systems, list) \
+            else local_systems
+        S, s, work = _schur_batched(local_systems, ne, self._device)
+        ext = dofs[:, :ne]
+        E = ext.shape[0]
+        gmat.row[:] = np.repeat(ext, ne, axis=1).ravel()
+        gmat.col[:] = np.tile(ext, (1, ne)).ravel()
+        gmat.data[:] = S.reshape(E, -1).cpu().numpy().ravel()
+        grhs += np.bincount(ext.ravel(), weights=s.cpu().numpy().ravel(), minlength=grhs.size)
+        self._sc_state = (local_systems, local_systems[0] if local_systems else None, work, ne)
+
+    def _solve_boundary_dofs(self, global_sc_system, dof_vec, on_ebc, rtol=1e-13):
+        """Solve the condensed exterior system with the essential BCs
+        (sem/discrete.py:502-510).  Symmetric systems (Poisson): Jacobi-PCG on
+        the device over the assembled CSR matrix; otherwise the reference's
+        own sparse direct solve."""
+        import torch
+        from . import _lib
+        sc_mat, sc_rhs = global_sc_system
+        is_unk = ~np.asarray(on_ebc, dtype=bool)
+        n = self.ndof_exterior
+        ext_dofs = dof_vec[:n]
+        A = sparse.coo_matrix((sc_mat.data, (sc_mat.row, sc_mat.col)), shape=(n, n)).tocsr()
+        A.sum_duplicates()
+        asym = abs(A - A.T)
+        if asym.nnz == 0 or asym.max() <= 1e-12 * abs(A).max():
+            dev = self.operator().device
+            lib = _lib.load()
+            rp = torch.from_numpy(A.indptr.astype(np.int64)).to(dev)
+            ci = torch.from_numpy(A.indices.astype(np.int32)).to(dev)
+            va = torch.from_numpy(A.data.astype(np.float64)).to(dev)
+            b = torch.from_numpy(np.asarray(sc_rhs, dtype=np.float64)).to(dev)
+            x = torch.from_numpy(np.where(is_unk, 0.0, ext_dofs)).to(dev)
+            mask = torch.from_numpy((~is_unk).astype(np.uint8)).to(dev)
+            import ctypes as C
+            its, rel = C.c_int(0), C.c_double(0.0)
+            with torch.cuda.device(dev):
+                _lib.check(lib.sem_csr_pcg_solve(n, _lib.tptr(rp), _lib.tptr(ci), _lib.tptr(va),
+                                                 _lib.tptr(b), _lib.tptr(x), _lib.tptr(mask),
+                                                 float(rtol), 100000, C.byref(its), C.byref(rel),
+                                                 dev.index, _lib.stream_ptr()))
+            ext_dofs[is_unk] = x.cpu().numpy()[is_unk]
+            return its.value, rel.value
+        from scipy.sparse import linalg as spla
+        A1 = A[is_unk]
+        rhs1 = sc_rhs[is_unk] - A1[:, ~is_unk].dot(ext_dofs[~is_unk])
+        ext_dofs[is_unk] = spla.spsolve(A1[:, is_unk].tocsc(), rhs1)
+        return None, None
+
+    def _solve_interior_dofs(self, local_systems, dof_vec):
+        """Interior DOFs of every element from its exterior DOFs
+        (sem/discrete.py:512-524), one batched device launch reusing the
+        eliminations of assemble_global_sc_system."""
+        import torch
+        from . import _lib
+        dofs, ne = self._cell_dofs_hier()
+        st = getattr(self, "_sc_state", None)
+        if st is None or st[0] is not local_systems or \
+                (local_systems and st[1] is not local_systems[0]):
+            _, _, work = _schur_batched(list(local_systems), ne, self._device)
+        else:
+            work = st[2]
+        E, nl = dofs.shape
+        if nl == ne:
+            return
+        xe = torch.from_numpy(np.ascontiguousarray(dof_vec[dofs[:, :ne]])).to(work.device)
+        xi = torch.empty(E, nl - ne, dtype=torch.float64, device=work.device)
+        lib = _lib.load()
+        with torch.cuda.device(work.device):
+            _lib.check(lib.sem_schur_backsolve(E, nl, ne, _lib.tptr(work), _lib.tptr(xe),
+                                               _lib.tptr(xi), _lib.stream_ptr()))
+        dof_vec[dofs[:, ne:]] = xi.cpu().numpy()
+
+    def solve(self, global_sc_system, local_systems, dof_vec, on_ebc):
+        """Static-condensation solve (sem/discrete.py:526-528): exterior DOFs
+        from the condensed system, then the element interiors; dof_vec
+        holds the essential BC values on entry and the solution on exit."""
+        self._solve_boundary_dofs(global_sc_system, dof_vec, on_ebc)
+        self._solve_interior_dofs(local_systems, dof_vec)
+
     def solve_poisson(self, rhs, dof_vec, on_ebc, rtol=1e-13, max_iter=20000):
         """Assembled Poisson solve K u = rhs with essential BCs: the result of
         DOFManagerSC.solve (sem/discrete.py:502-528) computed matrix-free with
@@ -527,6 +659,36 @@ class DOFManagerSC(DOFManager):
         x, its, rel = op.pcg_solve(b, x, mask, rtol=rtol, max_iter=max_iter)
         dof_vec[...] = x.cpu().numpy()
         return dof_vec, its, rel
+
+
+def _schur_batched(local_systems, ne, device=None):
+    """Device Schur complements of hierarchical local systems (list of
+    (lmat [nl, nl], lrhs [nl])): returns S [E, ne, ne], s [E, ne] and the
+    elimination workspace (A_ii^-1 [A_ie | b_i]) as device tensors."""
+    import ctypes as C
+    import torch
+    from . import _lib
+    from .operators import _device_index
+    dev = torch.device("cuda", _device_index(device))
+    mats = torch.from_numpy(np.ascontiguousarray(
+        np.stack([np.asarray(m, dtype=np.float64) for m, _ in local_systems]))).to(dev)
+    rhs = torch.from_numpy(np.ascontiguousarray(
+        np.stack([np.asarray(r, dtype=np.float64) for _, r in local_systems]))).to(dev)
+    E, nl = rhs.shape
+    if mats.shape != (E, nl, nl) or not (0 <= ne <= nl):
+        raise ValueError("local systems must be [nl, nl] matrices and [nl] vectors")
+    S = torch.empty(E, ne, ne, dtype=torch.float64, device=dev)
+    s = torch.empty(E, ne, dtype=torch.float64, device=dev)
+    work = torch.empty(E, max(nl - ne, 1), nl + 1, dtype=torch.float64, device=dev)
+    bad = C.c_int64(0)
+    lib = _lib.load()
+    with torch.cuda.device(dev):
+        rc = lib.sem_schur_batched(E, nl, ne, _lib.tptr(mats), _lib.tptr(rhs), _lib.tptr(work),
+                                   _lib.tptr(S), _lib.tptr(s), C.byref(bad), _lib.stream_ptr())
+    if rc == _lib.SEM_E_INVALID and bad.value:
+        raise np.linalg.LinAlgError("Singular matrix (%d elements)" % bad.value)
+    _lib.check(rc)
+    return S, s, work
 
 
 class FiniteElement(object):
