@@ -69,6 +69,14 @@ constexpr uint32_t W_CARRY = 8;   // add the value handed over by the previous g
 #ifndef SEM_RMW_PREFETCH
 #define SEM_RMW_PREFETCH 1  // Poisson: read read-modify-write targets before the last passes
 #endif
+// The prefetch holds n operands per lane through the last contractions:
+// measured on MI355X at ~1e7 DOF it pays up to n = 13 (p = 12: 0.142 vs
+// 0.163 ms) and costs at n = 17 (p = 16: 0.197 vs 0.176 ms; 246 vs 159
+// VGPRs, profiles/r02/variants).
+template <int N>
+struct RmwPrefetch {
+  static constexpr int value = N <= 16 ? SEM_RMW_PREFETCH : 0;
+};
 
 // D1 in even-odd form.  D is centro-antisymmetric (D[N-1-i][N-1-j] =
 // -D[i][j] on the symmetric GLL nodes), so with e_r = x_r + x_{N-1-r},
@@ -487,13 +495,9 @@ __device__ __forceinline__ void poisson_group_stored(const MapRef& mref,
       w0[m] = fma(g00, d0[m], g01 * d1);
       L[m * RS + j] = fma(g01, d0[m], g11 * d1);  // w1, same lane's slot
     }
-#if SEM_RMW_PREFETCH == 1
-    rmw_prefetch<N>(y, raw, accumulate, prev);
-#endif
+    if constexpr (RmwPrefetch<N>::value == 1) rmw_prefetch<N>(y, raw, accumulate, prev);
     deo_apply_t<N>(D, w0, v);
-#if SEM_RMW_PREFETCH == 2
-    rmw_prefetch<N>(y, raw, accumulate, prev);
-#endif
+    if constexpr (RmwPrefetch<N>::value == 2) rmw_prefetch<N>(y, raw, accumulate, prev);
   }
   wave_sync();
   // row i = j: yb[i][q] = sum_n D[n][q] w1[i][n]
@@ -635,13 +639,9 @@ __device__ __forceinline__ void nodal_laplacian(const double (&uc)[N], int j, do
       w0[m] = fma(g00[m], d0[m], g01[m] * d1);
       A[m * RS + j] = fma(g01[m], d0[m], B[m * RS + j] * d1);
     }
-#if SEM_RMW_PREFETCH == 1
-    rmw_prefetch<N>(y, raw, accumulate, prev);
-#endif
+    if constexpr (RmwPrefetch<N>::value == 1) rmw_prefetch<N>(y, raw, accumulate, prev);
     deo_apply_t<N>(D, w0, v);
-#if SEM_RMW_PREFETCH == 2
-    rmw_prefetch<N>(y, raw, accumulate, prev);
-#endif
+    if constexpr (RmwPrefetch<N>::value == 2) rmw_prefetch<N>(y, raw, accumulate, prev);
   }
   wave_sync();
   row_pass<N, RS, true, false>(A, j, D);
@@ -797,7 +797,8 @@ __global__ void __launch_bounds__(CHAIN_BLOCK, (PoissonMinWaves<N, NODAL>::value
 #ifdef SEM_DIAG_NO_STORE
     if (in_wave && v[0][0] == 1234.5678) y[0] = v[0][1];  // timing-only
 #else
-    chain_emit<N, 1, (SEM_RMW_PREFETCH > 0)>(y, raw, v, lane, wave, rd, in_wave, carry, accumulate, prev);
+    chain_emit<N, 1, (RmwPrefetch<N>::value > 0)>(y, raw, v, lane, wave, rd, in_wave, carry,
+                                                  accumulate, prev);
 #endif
   }
 }
