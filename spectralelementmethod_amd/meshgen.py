@@ -119,3 +119,103 @@ def write_square_msh(path, nex, ney, p, warp=0.0):
     names = [(1, 1, "ebc"), (1, 2, "nbc"), (2, 3, "interior")]
     write_msh(path, nodes, e2n, np.full(e2n.shape[0], 3), names, lines)
     return nodes, e2n
+
+
+# ---------------------------------------------------------------------------
+# Unstructured quad meshes (planner / partitioner coverage)
+# ---------------------------------------------------------------------------
+def _order_p_quads(corners, p):
+    """Order-p lexicographic element nodes of straight-sided quads with CCW
+    corners [E, 4, 2] (c0 -> c1 along xi0, c0 -> c3 along xi1), equispaced
+    (Gmsh high-order placement); shared nodes merged by position.
+    Returns nodes [2, n_nodes], e2n uint32 [E, p+1, p+1]."""
+    corners = np.asarray(corners, dtype=np.float64)
+    E = corners.shape[0]
+    t = np.linspace(0.0, 1.0, p + 1)
+    s0 = t[:, None]   # xi0 (row index i)
+    s1 = t[None, :]   # xi1 (column index j)
+    c0, c1, c2, c3 = (corners[:, k, :][:, None, None, :] for k in range(4))
+    X = ((1 - s0) * (1 - s1))[None, :, :, None] * c0 + (s0 * (1 - s1))[None, :, :, None] * c1 \
+        + (s0 * s1)[None, :, :, None] * c2 + ((1 - s0) * s1)[None, :, :, None] * c3
+    pts = X.reshape(-1, 2)
+    scale = max(1.0, float(np.abs(pts).max()))
+    key = np.round(pts / scale * 1e9).astype(np.int64)
+    _, first, inv = np.unique(key, axis=0, return_index=True, return_inverse=True)
+    # number nodes in order of first appearance (element-major: locality)
+    order = np.argsort(first)
+    rank = np.empty_like(order)
+    rank[order] = np.arange(order.size)
+    ids = rank[inv.ravel()]
+    nodes = pts[first[order]].T.copy()
+    return nodes, ids.reshape(E, p + 1, p + 1).astype(np.uint32)
+
+
+def quads_from_triangles(nx, ny, p, jitter=0.2, seed=0):
+    """Irregular-valence quad mesh of [-1,1]^2: a jittered nx x ny grid is
+    split into triangles (alternating diagonals), and every triangle into
+    three quads through its centroid and edge midpoints -- interior vertices
+    of valence 3 (centroids), 4 (edge midpoints) and 6 or more (grid points),
+    unlike any structured mesh.  Elements are numbered triangle by triangle
+    (a locality-preserving but non-lexicographic order)."""
+    rng = np.random.default_rng(seed)
+    x = np.linspace(-1, 1, nx + 1)
+    y = np.linspace(-1, 1, ny + 1)
+    X, Y = np.meshgrid(x, y, indexing="ij")
+    h = min(2.0 / nx, 2.0 / ny)
+    inner = np.zeros_like(X, dtype=bool)
+    inner[1:-1, 1:-1] = True
+    X = X + np.where(inner, rng.uniform(-jitter, jitter, X.shape) * h, 0.0)
+    Y = Y + np.where(inner, rng.uniform(-jitter, jitter, Y.shape) * h, 0.0)
+    P = np.stack([X, Y], axis=-1)
+    tris = []
+    for i in range(nx):
+        for j in range(ny):
+            a, b, c, d = P[i, j], P[i + 1, j], P[i + 1, j + 1], P[i, j + 1]
+            if (i + j) % 2 == 0:
+                tris += [(a, b, c), (a, c, d)]
+            else:
+                tris += [(a, b, d), (b, c, d)]
+    quads = []
+    for (a, b, c) in tris:  # CCW triangles -> 3 CCW quads
+        g = (a + b + c) / 3.0
+        mab, mbc, mca = (a + b) / 2, (b + c) / 2, (c + a) / 2
+        quads += [(a, mab, g, mca), (b, mbc, g, mab), (c, mca, g, mbc)]
+    return _order_p_quads(np.array(quads), p)
+
+
+def shuffle_elements(e2n, seed=0):
+    """The same mesh with its elements in random order (destroys the
+    locality the chain planner exploits)."""
+    perm = np.random.default_rng(seed).permutation(np.asarray(e2n).shape[0])
+    return np.ascontiguousarray(np.asarray(e2n)[perm])
+
+
+def shuffle_nodes(nodes, e2n, seed=0):
+    """The same mesh with its nodes renumbered at random (rows of a group then
+    span far more than the 4096 ids of the 16-bit packed map)."""
+    n = nodes.shape[1]
+    perm = np.random.default_rng(seed).permutation(n)  # new id of old node
+    new_nodes = np.empty_like(nodes)
+    new_nodes[:, perm] = nodes
+    return new_nodes, perm[np.asarray(e2n).astype(np.int64)].astype(np.uint32)
+
+
+def rcm_renumber(nodes, e2n):
+    """Reverse Cuthill-McKee renumbering of the nodes (what DOFManager does by
+    default, sem/discrete.py:169-178), then elements sorted by their smallest
+    node: restores locality after shuffling."""
+    from scipy import sparse
+    from scipy.sparse import csgraph
+    e2n = np.asarray(e2n).astype(np.int64)
+    E = e2n.shape[0]
+    n = nodes.shape[1]
+    flat = e2n.reshape(E, -1)
+    rows = np.repeat(flat, flat.shape[1], axis=1).ravel()
+    cols = np.tile(flat, (1, flat.shape[1])).ravel()
+    g = sparse.csr_matrix((np.ones(rows.size, np.int8), (rows, cols)), shape=(n, n))
+    order = csgraph.reverse_cuthill_mckee(g, symmetric_mode=True)
+    new_id = np.empty(n, dtype=np.int64)
+    new_id[order] = np.arange(n)
+    e_new = new_id[flat]
+    e_order = np.argsort(e_new.min(axis=1), kind="stable")
+    return nodes[:, order].copy(), e_new[e_order].reshape(e2n.shape).astype(np.uint32)

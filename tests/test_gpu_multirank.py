@@ -64,10 +64,18 @@ def _rank_worker(rank, world, port, mode, p, nex, ney, q):
         from spectralelementmethod_amd.operators import SEMOperator
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
-        gnodes, ge2n = meshgen.structured_square(nex, ney, p, warp=0.05)
+        if mode == "sfc":  # irregular-valence mesh, Morton-curve partition
+            from spectralelementmethod_amd.distributed import partition_elements
+            gnodes, ge2n = meshgen.quads_from_triangles(nex, ney, p, seed=4)
+        else:
+            gnodes, ge2n = meshgen.structured_square(nex, ney, p, warp=0.05)
         if mode == "strip":
             part = StripPartition(nex, ney, p, world, rank)
             nodes, e2n = part.local_mesh(0.05)
+        elif mode == "sfc":
+            part = GenericPartition(ge2n, partition_elements(ge2n, gnodes, world, "sfc"), world,
+                                    rank)
+            e2n, nodes = part.e2n_local, gnodes[:, part.l2g]
         else:
             elem_rank = np.random.default_rng(8).integers(0, world, size=ge2n.shape[0])
             part = GenericPartition(ge2n, elem_rank, world, rank)
@@ -106,7 +114,8 @@ def _rank_worker(rank, world, port, mode, p, nex, ney, q):
 
 
 @pytest.mark.parametrize("world,mode,p,nex,ney", [(2, "strip", 8, 12, 6), (3, "strip", 4, 10, 5),
-                                                  (3, "generic", 3, 7, 6)])
+                                                  (3, "generic", 3, 7, 6),
+                                                  (4, "sfc", 4, 6, 5)])
 def test_overlapped_operator_ranks_on_one_gpu(gpu, world, mode, p, nex, ney):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
