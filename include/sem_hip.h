@@ -128,7 +128,12 @@ int sem_set_map_shared(sem_ctx* ctx, const uint32_t* d_e2n, const uint8_t* d_nod
  * kernel streams (2: 16-bit row offsets, used when every group row spans
  * < 4096 node ids; 4 otherwise; SEM_MAP16=0 in the environment forces 4).
  * [19] the Poisson geometry mode the action uses (SEM_GEOM_NODAL or
- * SEM_GEOM_STORED, AUTO resolved).  Writes min(n_info, 20) values. */
+ * SEM_GEOM_STORED, AUTO resolved; nodal only once x_phys per node exists).
+ * [20] scatter plan: 0 chains of consecutive elements (carry / merge codes),
+ * 1 element-coloured chains (chosen when the element order defeats the chain
+ * patterns: more than 1/16 of the groups would need atomics; SEM_PLAN=1 / 0
+ * in the environment forces / forbids it), 2 one element per wavefront
+ * (MFMA kernel).  Writes min(n_info, 21) values. */
 int sem_plan_info(sem_ctx* ctx, int64_t* info, int n_info);
 
 /* How the Poisson action obtains its geometric factors.

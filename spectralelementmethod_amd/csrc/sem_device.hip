@@ -28,9 +28,9 @@ namespace {
 
 inline int epw_of(int n) { return WAVE / n; }
 
-// user-supplied factors [E][ncomp][n][n] -> packed (group order via gpos)
+// user-supplied factors [E][ncomp][n][n] -> packed (element positions epos)
 __global__ void k_pack_geom(const double* __restrict__ G, int64_t n_elem, int n, int ncomp,
-                            int epw, const int* __restrict__ gpos, double* __restrict__ GP) {
+                            int epw, const int* __restrict__ epos, double* __restrict__ GP) {
   const int64_t nn = (int64_t)n * n;
   const int64_t total = n_elem * ncomp * nn;
   const int lw = epw * n;
@@ -41,9 +41,9 @@ __global__ void k_pack_geom(const double* __restrict__ G, int64_t n_elem, int n,
     const int c = (int)(rem / nn);
     const int node = (int)(rem - c * nn);
     const int r = node / n, jj = node - r * n;
-    const int64_t grp = e / epw;
-    const int kk = (int)(e - grp * epw);
-    const int64_t gg = gpos[grp];
+    const int64_t pos = epos[e];  // packed position slot * epw + lane element
+    const int64_t gg = pos / epw;
+    const int kk = (int)(pos - gg * epw);
     GP[((gg * ncomp + c) * n + r) * lw + kk * n + jj] = G[t];
   }
 }
@@ -60,7 +60,7 @@ __global__ void k_zero_list(double* __restrict__ y, const uint32_t* __restrict__
 // diag of the Poisson element operator, summed through the map:
 // K_e[pq,pq] = sum_m D[m][p]^2 G00[m][q] + sum_n D[n][q]^2 G11[p][n] + 2 D[p][p] D[q][q] G01[p][q]
 __global__ void k_poisson_diag(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
-                               const int* __restrict__ gpos, const double* __restrict__ gD, int n,
+                               const int* __restrict__ epos, const double* __restrict__ gD, int n,
                                int epw, int64_t n_elem, double* __restrict__ diag) {
   __shared__ double sD[MAXN * MAXN];
   for (int i = threadIdx.x; i < n * n; i += blockDim.x) sD[i] = gD[i];
@@ -72,9 +72,9 @@ __global__ void k_poisson_diag(const uint32_t* __restrict__ mapP, const double* 
     const int64_t e = t / (n * n);
     const int node = (int)(t - e * n * n);
     const int p = node / n, q = node - p * n;
-    const int64_t grp = e / epw;
-    const int kk = (int)(e - grp * epw);
-    const int64_t gg = gpos[grp];
+    const int64_t pos = epos[e];  // packed position slot * epw + lane element
+    const int64_t gg = pos / epw;
+    const int kk = (int)(pos - gg * epw);
     const double* G = GP + gg * (int64_t)(3 * n * lw) + kk * n;
     double s = 0.0;
     for (int m = 0; m < n; ++m) s += sD[m * n + p] * sD[m * n + p] * G[(0 * n + m) * lw + q];
@@ -190,7 +190,7 @@ struct sem_ctx {
   uint16_t* d_map16 = nullptr;  // the same map as 16-bit row offsets (column kernel)
   uint32_t* d_mbase = nullptr;  // their per-(slot, row) 32-bit bases
   bool map16 = false;
-  int* d_gpos = nullptr;         // natural group -> packed slot
+  int* d_epos = nullptr;         // element -> packed position slot * epw + k
   const uint32_t* d_e2n = nullptr;
   uint32_t* d_zero = nullptr;    // y entries no kernel stores first (unreferenced / first-atomic)
   int64_t n_zero = 0;
@@ -210,6 +210,7 @@ struct sem_ctx {
   // need different plans and packed layouts)
   int kernel = SEM_KERNEL_AUTO;
   bool mfma = false;
+  bool ecol = false;  // column kernel on the element-coloured plan
   double2* d_XG = nullptr;
   uint32_t* d_owner = nullptr;
   bool xg_valid = false;
@@ -371,7 +372,7 @@ void launch_geom_n(sem_ctx* c, const double* nodes, int op_kind, double* GP, dou
   using Sh = GeomShape<N>;
   const int grid = (int)((c->n_elem + Sh::EPB - 1) / Sh::EPB);
   hipLaunchKernelGGL((k_geometry<N>), dim3(grid), dim3(Sh::THREADS), 0, st, nodes, c->n_node,
-                     c->d_e2n, c->n_elem, c->d_Vinv, c->d_D, c->d_w, op_kind, c->epw, c->d_gpos, GP,
+                     c->d_e2n, c->n_elem, c->d_Vinv, c->d_D, c->d_w, op_kind, c->epw, c->d_epos, GP,
                      xph,
                      J, iJ, dJ, dJW, XG, XG ? c->d_owner : nullptr, XGin, c->d_bad);
 }
@@ -446,7 +447,7 @@ int ensure_gp(sem_ctx* c, int op_kind, hipStream_t st) {
 //   2. greedy colouring of chains: chains of one colour share no node
 //      (per-node colour bitmask; chains needing > MAX_COLOURS colours, and
 //      every chain of a non-conforming mesh, go to a final all-atomic class);
-//   3. launch order = colour-major; gpos[g] = packed slot of group g;
+//   3. launch order = colour-major; epos[e] = packed position of element e;
 //   4. inside a chain the 4 groups of a round run concurrently, rounds run in
 //      order.  A node may be shared inside a round only by (a) the elements on
 //      two neighbouring lanes of one group (row r, lanes L, L+1: MERGE on L,
@@ -460,7 +461,8 @@ int ensure_gp(sem_ctx* c, int op_kind, hipStream_t st) {
 struct Plan {
   std::vector<uint32_t> owner;  // first element referencing each node
   std::vector<uint32_t> mapP;
-  std::vector<int> gpos;
+  std::vector<int> epos;             // element -> packed position slot * epw + k
+  std::vector<uint8_t> slot_fill;    // real elements in each slot (first lanes)
   std::vector<int64_t> colour_start;  // in chains
   std::vector<uint32_t> zero;
   int64_t n_atomic_groups = 0;
@@ -550,11 +552,16 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
     for (int64_t ch = 0; ch < n_chains; ++ch) order[fill[colour[ch]]++] = ch;
   }
   P.n_slots = n_chains * CH;
-  P.gpos.assign(n_groups, 0);
+  P.epos.assign(n_elem, 0);
+  P.slot_fill.assign(P.n_slots, 0);
   for (int64_t q = 0; q < n_chains; ++q)
     for (int i = 0; i < CH; ++i) {
       const int64_t g = order[q] * CH + i;
-      if (g < n_groups) P.gpos[g] = (int)(q * CH + i);
+      if (g >= n_groups) continue;
+      const int64_t slot = q * CH + i;
+      const int fill = (int)std::min<int64_t>(epw, n_elem - g * epw);
+      P.slot_fill[slot] = (uint8_t)fill;
+      for (int k = 0; k < fill; ++k) P.epos[g * epw + k] = (int)(slot * epw + k);
     }
   // 4./5. validation and write codes, chain by chain in launch order
   P.mapP.assign((size_t)P.n_slots * n * lw, W_SKIP << CODE_SHIFT);
@@ -654,15 +661,12 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
 static bool build_map16(const Plan& P, int64_t n_elem, int n, int epw, int64_t n_groups,
                         std::vector<uint16_t>& m16, std::vector<uint32_t>& base) {
   const int lw = epw * n;
-  std::vector<int64_t> slot_group(P.n_slots, -1);
-  for (int64_t g = 0; g < n_groups; ++g) slot_group[P.gpos[g]] = g;
   m16.assign((size_t)P.n_slots * n * lw, (uint16_t)(W_SKIP << M16_CODE_SHIFT));
   base.assign((size_t)P.n_slots * n, 0u);
   int64_t wide = 0;
   for (int64_t sl = 0; sl < P.n_slots; ++sl) {
-    const int64_t g = slot_group[sl];
-    if (g < 0) continue;
-    const int lanes = (int)std::min<int64_t>(epw, n_elem - g * epw) * n;
+    if (!P.slot_fill[sl]) continue;
+    const int lanes = P.slot_fill[sl] * n;
     bool fits = true;
     for (int r = 0; r < n && fits; ++r) {
       const uint32_t* row = &P.mapP[((size_t)sl * n + r) * lw];
@@ -687,7 +691,10 @@ static bool build_map16(const Plan& P, int64_t n_elem, int n, int epw, int64_t n
         out[l] = (uint16_t)(((row[l] & GID_MASK) - lo) | ((row[l] >> CODE_SHIFT) << M16_CODE_SHIFT));
     }
   }
-  return wide * 16 <= n_groups;
+  int64_t filled = 0;
+  for (uint8_t f : P.slot_fill) filled += f ? 1 : 0;
+  (void)n_groups;
+  return wide * 16 <= filled;
 }
 
 // ---------------------------------------------------------------------------
@@ -721,11 +728,50 @@ int build_plan_elem(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_
         }
   P.conforming = conforming;
   auto shared_local = [&](int r, int jj) { return !conforming || is_bnd(r, jj); };
+  // breadth-first element order over shared nodes: greedy colouring along it
+  // needs far fewer colours than along a random element order (split
+  // triangles, shuffled: 8 instead of 11), and packing classes in it keeps
+  // neighbouring elements in neighbouring groups
+  std::vector<int64_t> bfs;
+  bfs.reserve(n_elem);
+  {
+    std::vector<int64_t> start(n_node + 1, 0);
+    for (int64_t e = 0; e < n_elem; ++e)
+      for (int r = 0; r < n; ++r)
+        for (int jj = 0; jj < n; ++jj)
+          if (shared_local(r, jj)) start[e2n[e * nn + r * n + jj] + 1]++;
+    for (int64_t i = 0; i < n_node; ++i) start[i + 1] += start[i];
+    std::vector<int64_t> inc(start[n_node]), fill(start.begin(), start.end() - 1);
+    for (int64_t e = 0; e < n_elem; ++e)
+      for (int r = 0; r < n; ++r)
+        for (int jj = 0; jj < n; ++jj)
+          if (shared_local(r, jj)) inc[fill[e2n[e * nn + r * n + jj]]++] = e;
+    std::vector<uint8_t> seen(n_elem, 0);
+    for (int64_t s0 = 0; s0 < n_elem; ++s0) {
+      if (seen[s0]) continue;
+      seen[s0] = 1;
+      size_t head = bfs.size();
+      bfs.push_back(s0);
+      while (head < bfs.size()) {
+        const int64_t e = bfs[head++];
+        for (int r = 0; r < n; ++r)
+          for (int jj = 0; jj < n; ++jj) {
+            if (!shared_local(r, jj)) continue;
+            const uint32_t gid = e2n[e * nn + r * n + jj];
+            for (int64_t t = start[gid]; t < start[gid + 1]; ++t)
+              if (!seen[inc[t]]) {
+                seen[inc[t]] = 1;
+                bfs.push_back(inc[t]);
+              }
+          }
+      }
+    }
+  }
   std::vector<uint8_t> cmask(n_node, 0);
   std::vector<int64_t> stamp(n_node, -1);
   std::vector<int> colour(n_elem);
   std::vector<uint32_t> cn;
-  for (int64_t e = 0; e < n_elem; ++e) {
+  for (const int64_t e : bfs) {
     cn.clear();
     uint32_t forb = 0;
     bool dup = false;
@@ -766,8 +812,9 @@ int build_plan_elem(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_
     for (int64_t e = 0; e < n_elem; ++e) order[fill[colour[e]]++] = e;
   }
   P.n_slots = n_elem;
-  P.gpos.assign(n_elem, 0);
-  for (int64_t q = 0; q < n_elem; ++q) P.gpos[order[q]] = (int)q;
+  P.epos.assign(n_elem, 0);
+  for (int64_t q = 0; q < n_elem; ++q) P.epos[order[q]] = (int)q;
+  P.slot_fill.assign(n_elem, 1);
   P.mapP.assign((size_t)n_elem * nn, W_SKIP << CODE_SHIFT);
   std::vector<uint8_t> written(n_node, 0);
   if (!node_state.empty())
@@ -791,6 +838,163 @@ int build_plan_elem(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_
         written[gid] = 1;
         out[r * n + jj] = gid | (code << CODE_SHIFT);
       }
+  }
+  for (int64_t i = 0; i < n_node; ++i)
+    if (cnt[i] == 0 && (node_state.empty() || !node_state[i])) P.zero.push_back((uint32_t)i);
+  std::sort(P.zero.begin(), P.zero.end());
+  return SEM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Element-coloured plan for the column kernel (meshes whose element order
+// defeats the chain patterns: irregular valence, random element order).
+// Elements are greedily coloured, in breadth-first order over shared nodes,
+// so that elements of one colour share no node, then packed colour class by
+// colour class, in that order inside a class, into groups of EPW elements and
+// chains of CHAIN_WAVES * rounds groups (a class's last group / chain may
+// be partly empty).  Nothing inside a launch shares a node, so the codes
+// are plain STORE (first writer in launch order) / RMW with no merge or
+// carry; elements needing more than MAX_COLOURS colours go to a final
+// all-atomic class.  Chosen by sem_set_map when the chain plan would send
+// more than 1/16 of its groups to the atomic fallback and this plan sends
+// fewer.
+// ---------------------------------------------------------------------------
+int build_plan_ecol(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node, int n,
+                    int rounds, const std::vector<uint8_t>& node_state, Plan& P) {
+  const int epw = WAVE / n, lw = epw * n, nn = n * n;
+  const int CH = CHAIN_WAVES * rounds;
+  auto is_bnd = [n](int r, int jj) { return r == 0 || r == n - 1 || jj == 0 || jj == n - 1; };
+  std::vector<uint32_t> cnt(n_node, 0);
+  P.owner.assign(n_node, 0xFFFFFFFFu);
+  for (int64_t t = 0; t < n_elem * nn; ++t) {
+    if (e2n[t] >= n_node) return fail(SEM_E_INVALID, "element map references node >= n_node");
+    if (!cnt[e2n[t]]++) P.owner[e2n[t]] = (uint32_t)(t / nn);
+  }
+  bool conforming = true;
+  for (int64_t e = 0; e < n_elem && conforming; ++e)
+    for (int r = 1; r < n - 1 && conforming; ++r)
+      for (int jj = 1; jj < n - 1; ++jj)
+        if (cnt[e2n[e * nn + r * n + jj]] != 1) {
+          conforming = false;
+          break;
+        }
+  P.conforming = conforming;
+  auto shared_local = [&](int r, int jj) { return !conforming || is_bnd(r, jj); };
+  // breadth-first element order over shared nodes: greedy colouring along it
+  // needs far fewer colours than along a random element order (split
+  // triangles, shuffled: 8 instead of 11), and packing classes in it keeps
+  // neighbouring elements in neighbouring groups
+  std::vector<int64_t> bfs;
+  bfs.reserve(n_elem);
+  {
+    std::vector<int64_t> start(n_node + 1, 0);
+    for (int64_t e = 0; e < n_elem; ++e)
+      for (int r = 0; r < n; ++r)
+        for (int jj = 0; jj < n; ++jj)
+          if (shared_local(r, jj)) start[e2n[e * nn + r * n + jj] + 1]++;
+    for (int64_t i = 0; i < n_node; ++i) start[i + 1] += start[i];
+    std::vector<int64_t> inc(start[n_node]), fill(start.begin(), start.end() - 1);
+    for (int64_t e = 0; e < n_elem; ++e)
+      for (int r = 0; r < n; ++r)
+        for (int jj = 0; jj < n; ++jj)
+          if (shared_local(r, jj)) inc[fill[e2n[e * nn + r * n + jj]]++] = e;
+    std::vector<uint8_t> seen(n_elem, 0);
+    for (int64_t s0 = 0; s0 < n_elem; ++s0) {
+      if (seen[s0]) continue;
+      seen[s0] = 1;
+      size_t head = bfs.size();
+      bfs.push_back(s0);
+      while (head < bfs.size()) {
+        const int64_t e = bfs[head++];
+        for (int r = 0; r < n; ++r)
+          for (int jj = 0; jj < n; ++jj) {
+            if (!shared_local(r, jj)) continue;
+            const uint32_t gid = e2n[e * nn + r * n + jj];
+            for (int64_t t = start[gid]; t < start[gid + 1]; ++t)
+              if (!seen[inc[t]]) {
+                seen[inc[t]] = 1;
+                bfs.push_back(inc[t]);
+              }
+          }
+      }
+    }
+  }
+  std::vector<uint8_t> cmask(n_node, 0);
+  std::vector<int64_t> stamp(n_node, -1);
+  std::vector<int> colour(n_elem);
+  std::vector<uint32_t> cn;
+  for (const int64_t e : bfs) {
+    cn.clear();
+    uint32_t forb = 0;
+    bool dup = false;
+    for (int r = 0; r < n; ++r)
+      for (int jj = 0; jj < n; ++jj)
+        if (shared_local(r, jj)) {
+          const uint32_t gid = e2n[e * nn + r * n + jj];
+          if (stamp[gid] == e) {
+            dup = true;
+            continue;
+          }
+          stamp[gid] = e;
+          cn.push_back(gid);
+          forb |= cmask[gid];
+        }
+    int c = MAX_COLOURS;
+    if (!dup)
+      for (int q = 0; q < MAX_COLOURS; ++q)
+        if (!(forb & (1u << q))) {
+          c = q;
+          break;
+        }
+    if (c < MAX_COLOURS)
+      for (uint32_t gid : cn) cmask[gid] |= (uint8_t)(1u << c);
+    colour[e] = c;
+  }
+  std::vector<uint8_t>().swap(cmask);
+  // pack each class into groups and chains
+  std::vector<std::vector<int64_t>> cls(MAX_COLOURS + 1);
+  for (const int64_t e : bfs) cls[colour[e]].push_back(e);
+  P.colour_start.assign(MAX_COLOURS + 2, 0);
+  int64_t n_chains = 0;
+  for (int q = 0; q <= MAX_COLOURS; ++q) {
+    const int64_t groups = ((int64_t)cls[q].size() + epw - 1) / epw;
+    n_chains += (groups + CH - 1) / CH;
+    P.colour_start[q + 1] = n_chains;
+  }
+  P.n_slots = n_chains * CH;
+  P.epos.assign(n_elem, 0);
+  P.slot_fill.assign(P.n_slots, 0);
+  P.mapP.assign((size_t)P.n_slots * n * lw, W_SKIP << CODE_SHIFT);
+  std::vector<uint8_t> written(n_node, 0);
+  if (!node_state.empty())
+    for (int64_t i = 0; i < n_node; ++i) written[i] = (node_state[i] & SEM_NODE_PRIOR) ? 1 : 0;
+  P.n_atomic_groups = 0;
+  for (int q = 0; q <= MAX_COLOURS; ++q) {
+    const bool atomic = q == MAX_COLOURS;
+    const int64_t slot0 = P.colour_start[q] * CH;
+    const auto& L = cls[q];
+    for (size_t idx = 0; idx < L.size(); ++idx) {
+      const int64_t e = L[idx];
+      const int64_t slot = slot0 + (int64_t)(idx / epw);
+      const int k = (int)(idx % epw);
+      P.epos[e] = (int)(slot * epw + k);
+      P.slot_fill[slot] = (uint8_t)(k + 1);
+      uint32_t* out = P.mapP.data() + slot * (int64_t)n * lw;
+      for (int r = 0; r < n; ++r)
+        for (int jj = 0; jj < n; ++jj) {
+          const uint32_t gid = e2n[e * nn + r * n + jj];
+          uint32_t code;
+          if (atomic && shared_local(r, jj)) {
+            code = W_ATOMIC;
+            if (!written[gid]) P.zero.push_back(gid);
+          } else {
+            code = written[gid] ? W_RMW : W_STORE;
+          }
+          written[gid] = 1;
+          out[r * lw + k * n + jj] = gid | (code << CODE_SHIFT);
+        }
+    }
+    if (atomic) P.n_atomic_groups += ((int64_t)L.size() + epw - 1) / epw;
   }
   for (int64_t i = 0; i < n_node; ++i)
     if (cnt[i] == 0 && (node_state.empty() || !node_state[i])) P.zero.push_back((uint32_t)i);
@@ -853,7 +1057,7 @@ void sem_ctx_destroy(sem_ctx* c) {
   (void)hipFree(c->d_mapP);
   (void)hipFree(c->d_map16);
   (void)hipFree(c->d_mbase);
-  (void)hipFree(c->d_gpos);
+  (void)hipFree(c->d_epos);
   (void)hipFree(c->d_zero);
   for (double* g : c->d_GP) (void)hipFree(g);
   (void)hipFree(c->d_lin);
@@ -908,6 +1112,20 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
   int rc = mfma ? build_plan_elem(h, c->n_elem, c->n_node, n, state, P)
                 : build_plan(h, c->n_elem, c->n_node, n, rounds, state, P);
   if (rc) return rc;
+  // element-coloured fallback for orders that defeat the chain patterns
+  // (SEM_PLAN=1 forces it, SEM_PLAN=0 forbids it)
+  const char* penv = std::getenv("SEM_PLAN");
+  const int pmode = penv ? std::atoi(penv) : -1;
+  c->ecol = false;
+  const int64_t ng_col = (c->n_elem + epw_of(n) - 1) / epw_of(n);
+  if (!mfma && pmode != 0 && (pmode == 1 || P.n_atomic_groups * 16 > ng_col)) {
+    Plan Q;
+    if ((rc = build_plan_ecol(h, c->n_elem, c->n_node, n, rounds, state, Q))) return rc;
+    if (pmode == 1 || Q.n_atomic_groups < P.n_atomic_groups) {
+      P = std::move(Q);
+      c->ecol = true;
+    }
+  }
   c->mfma = mfma;
   c->epw = mfma ? 1 : epw_of(n);
   c->lw = c->epw * n;
@@ -917,10 +1135,10 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
   std::vector<uint32_t>().swap(h);
   c->d_e2n = d_e2n;
   (void)hipFree(c->d_mapP);
-  (void)hipFree(c->d_gpos);
+  (void)hipFree(c->d_epos);
   (void)hipFree(c->d_zero);
   c->d_mapP = nullptr;
-  c->d_gpos = nullptr;
+  c->d_epos = nullptr;
   c->d_zero = nullptr;
   HIP_TRY(hipMalloc(&c->d_mapP, P.mapP.size() * sizeof(uint32_t)));
   HIP_TRY(hipMemcpy(c->d_mapP, P.mapP.data(), P.mapP.size() * sizeof(uint32_t),
@@ -946,8 +1164,8 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
       c->map16 = true;
     }
   }
-  HIP_TRY(hipMalloc(&c->d_gpos, P.gpos.size() * sizeof(int)));
-  HIP_TRY(hipMemcpy(c->d_gpos, P.gpos.data(), P.gpos.size() * sizeof(int), hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&c->d_epos, P.epos.size() * sizeof(int)));
+  HIP_TRY(hipMemcpy(c->d_epos, P.epos.data(), P.epos.size() * sizeof(int), hipMemcpyHostToDevice));
   c->n_zero = (int64_t)P.zero.size();
   if (c->n_zero) {
     HIP_TRY(hipMalloc(&c->d_zero, P.zero.size() * sizeof(uint32_t)));
@@ -977,18 +1195,19 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
 int sem_plan_info(sem_ctx* c, int64_t* info, int n_info) {
   if (!c || !info || n_info < 1) return fail(SEM_E_INVALID, "bad arguments");
   const int64_t nc = c->colour_start.empty() ? 0 : (int64_t)c->colour_start.size() - 1;
-  constexpr int NV = 8 + MAX_COLOURS + 1 + 1 + 1 + 1;
+  constexpr int NV = 8 + MAX_COLOURS + 1 + 1 + 1 + 1 + 1;
   int64_t vals[NV] = {c->n_groups, c->n_zero, c->n_atomic_groups, c->conforming ? 1 : 0,
                       c->epw,      nc,        c->rounds,          c->n_slots};
   for (int64_t q = 0; q < nc && q <= MAX_COLOURS; ++q)
     vals[8 + q] = c->colour_start[q + 1] - c->colour_start[q];
-  vals[NV - 3] = c->mfma ? SEM_KERNEL_MFMA : SEM_KERNEL_COLUMN;
-  vals[NV - 2] = c->map16 ? 2 : 4;  // bytes per packed map entry
+  vals[NV - 4] = c->mfma ? SEM_KERNEL_MFMA : SEM_KERNEL_COLUMN;
+  vals[NV - 3] = c->map16 ? 2 : 4;  // bytes per packed map entry
   // the geometry the Poisson action actually uses: nodal only once x_phys
   // per node exists (sem_set_geom installs stored factors); before any
   // geometry, the mode sem_geom_from_nodes will resolve to
   const bool eff_nodal = c->xg_valid ? true : (c->d_GP[0] ? false : nodal_mode(c));
-  vals[NV - 1] = eff_nodal ? SEM_GEOM_NODAL : SEM_GEOM_STORED;
+  vals[NV - 2] = eff_nodal ? SEM_GEOM_NODAL : SEM_GEOM_STORED;
+  vals[NV - 1] = c->mfma ? 2 : (c->ecol ? 1 : 0);  // plan: chains, element-coloured, element
   for (int i = 0; i < n_info && i < NV; ++i) info[i] = vals[i];
   return SEM_OK;
 }
@@ -1078,7 +1297,7 @@ int sem_geom_fields(sem_ctx* c, const double* d_nodes, const double* h_Vinv, dou
 
 int sem_set_geom(sem_ctx* c, const double* d_G, int op_kind, void* stream) {
   if (!c || !d_G) return fail(SEM_E_INVALID, "null argument");
-  if (!c->d_gpos) return fail(SEM_E_STATE, "sem_set_map must precede sem_set_geom");
+  if (!c->d_epos) return fail(SEM_E_STATE, "sem_set_map must precede sem_set_geom");
   DeviceGuard g(c->device);
   int rc;
   if ((rc = check_op(c, op_kind))) return rc;
@@ -1086,7 +1305,7 @@ int sem_set_geom(sem_ctx* c, const double* d_G, int op_kind, void* stream) {
   const int ncomp = sem_op_ncomp(op_kind);
   if (op_kind == SEM_OP_POISSON) c->xg_valid = false;  // caller's factors take over
   hipLaunchKernelGGL(k_pack_geom, dim3(grid_for(c->n_elem * ncomp * c->n * c->n)), dim3(BLOCK), 0,
-                     S(stream), d_G, c->n_elem, c->n, ncomp, c->epw, c->d_gpos,
+                     S(stream), d_G, c->n_elem, c->n, ncomp, c->epw, c->d_epos,
                      c->d_GP[gp_slot(op_kind)]);
   HIP_TRY(hipGetLastError());
   return SEM_OK;
@@ -1161,7 +1380,7 @@ int sem_diag(sem_ctx* c, int op_kind, double* d_diag, void* stream) {
   }
   HIP_TRY(hipMemsetAsync(d_diag, 0, c->n_node * sizeof(double), st));
   hipLaunchKernelGGL(k_poisson_diag, dim3(grid_for(c->n_elem * c->n * c->n)), dim3(BLOCK), 0, st,
-                     c->d_mapP, c->d_GP[0], c->d_gpos, c->d_D, c->n, c->epw, c->n_elem, d_diag);
+                     c->d_mapP, c->d_GP[0], c->d_epos, c->d_D, c->n, c->epw, c->n_elem, d_diag);
   HIP_TRY(hipGetLastError());
   return SEM_OK;
 }

@@ -1184,7 +1184,7 @@ template <int N>
 __global__ void __launch_bounds__(GeomShape<N>::THREADS)
     k_geometry(const double* __restrict__ nodes, int64_t n_node, const uint32_t* __restrict__ e2n,
                int64_t n_elem, const double* __restrict__ gVinv, const double* __restrict__ gD,
-               const double* __restrict__ gw, int op_kind, int epw, const int* __restrict__ gpos,
+               const double* __restrict__ gw, int op_kind, int epw, const int* __restrict__ epos,
                double* __restrict__ GP, double* __restrict__ xph, double* __restrict__ Jo,
                double* __restrict__ iJo, double* __restrict__ dJo, double* __restrict__ dJW,
                double2* __restrict__ XG, const uint32_t* __restrict__ owner,
@@ -1300,9 +1300,9 @@ __global__ void __launch_bounds__(GeomShape<N>::THREADS)
   if (dJo) dJo[base] = det;
   if (dJW) dJW[base] = W;
   if (GP) {
-    const int64_t grp = e / epw;
-    const int kk = (int)(e - grp * epw);
-    const int64_t gg = gpos[grp];
+    const int64_t pos = epos[e];  // packed position slot * epw + lane element
+    const int64_t gg = pos / epw;
+    const int kk = (int)(pos - gg * epw);
     const int ncomp = (op_kind == 0) ? 3 : (op_kind == 1 ? 7 : 9);
     double* o = GP + gg * (int64_t)(ncomp * N * LW) + m * LW + kk * N + nq;
     const double A00 = iJ00 * iJ00 + iJ01 * iJ01;

@@ -60,6 +60,11 @@ def test_unstructured_action_vs_oracle(gpu, gll, kind, p, geometry):
     assert rel_l2(y, ref) < TOL, (kind, p, geometry, plan)
     if kind == "shuffled_nodes" and p == 8:
         assert plan["map_entry_bytes"] == 4  # rows span far beyond the 16-bit window
+    if kind in ("split_tri", "split_tri_shuffled", "shuffled_elems"):
+        # the element order defeats the chain patterns: element-coloured chains
+        # (greedy colouring in breadth-first order fits these in 8 colours), no
+        # atomics on these conforming meshes
+        assert plan["plan"] == "element-coloured" and plan["atomic_groups"] == 0, plan
 
 
 @pytest.mark.parametrize("p", [4, 12])
@@ -73,4 +78,25 @@ def test_unstructured_mfma_vs_oracle(gpu, gll, kind, p):
     op = SEMOperator(p, e2n, nodes, device=gpu, kernel="mfma")
     y = op.apply(torch.from_numpy(u).to(gpu)).cpu().numpy()
     assert op.plan_info()["kernel"] == "mfma"
-    assert rel_l2(y, ref) < TOL, (kind, p)
+    # above p = 10 the reference's equispaced->GLL transform (cond(V_eq) ~1e3 at
+    # p = 12) limits the oracle itself to ~1e-11 on these small elements
+    # (DESIGN.md §6); the north-star bar 1e-10 applies
+    assert rel_l2(y, ref) < (TOL if p <= 10 else 1e-10), (kind, p)
+
+
+@pytest.mark.parametrize("plan_env", ["1", "0"])
+def test_forced_plan_structured(gpu, gll, monkeypatch, plan_env):
+    """SEM_PLAN=1 forces the element-coloured plan on a structured mesh,
+    SEM_PLAN=0 the chain plan with its atomic fallback on split triangles:
+    both give the oracle's action."""
+    import sem_oracle
+    from spectralelementmethod_amd.operators import SEMOperator
+    monkeypatch.setenv("SEM_PLAN", plan_env)
+    for kind in ("shuffled_elems", "split_tri"):
+        nodes, e2n = make_mesh(kind, 4)
+        u = np.random.default_rng(1).standard_normal(nodes.shape[1])
+        ref = sem_oracle.PoissonProblem(nodes, e2n, gll["half_4"]).apply(u)
+        op = SEMOperator(4, e2n, nodes, device=gpu)
+        assert op.plan_info()["plan"] == ("element-coloured" if plan_env == "1" else "chains")
+        y = op.apply(torch.from_numpy(u).to(gpu)).cpu().numpy()
+        assert rel_l2(y, ref) < TOL

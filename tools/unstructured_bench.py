@@ -56,7 +56,7 @@ for p in (4, 8):
         rec = dict(kind=kind, p=p, n_elem=int(e2n.shape[0]), ndof=op.ndof, ms_per_action=ms,
                    dof_per_s=op.ndof / ms * 1e3, setup_s=t_setup,
                    **{k: plan[k] for k in ("colours", "chains_per_colour", "atomic_groups",
-                                           "zero_list", "map_entry_bytes", "geometry", "kernel")})
+                                           "zero_list", "map_entry_bytes", "geometry", "kernel", "plan")})
         print(json.dumps(rec), flush=True)
         out.append(rec)
         del op
