@@ -272,11 +272,11 @@ void upload_deo(sem_ctx* c, hipError_t* err) {
   *err = hipMemcpy(c->d_deo, &d, sizeof(d), hipMemcpyHostToDevice);
 }
 
-// the Poisson action recomputes its factors from x_phys per node (NODAL)
-// unless the stored-factor mode was chosen or the caller supplied factors
 // AUTO geometry of the column kernel, per order from the MI355X sweep at
-// ~1e7 DOF (profiles/r01c/geosweep): nodal at p = 2, 4, 5, 8
-// (and p = 1, unmeasured), stored factors at p = 3, 6, 7 and above 8
+// ~1e7 DOF (profiles/r01c/geosweep): NODAL (factors
+// re-derived from x_phys per node) at p = 1, 2, 4, 5, 8, STORED at p = 3, 6,
+// 7 and above 8.  The p = 3, 5, 6 picks are within 2-3 % (one run each);
+// the clear wins are p = 2, 4, 8 (nodal) and p >= 9 (stored).
 bool auto_nodal_order(int n) { return n == 2 || n == 3 || n == 5 || n == 6 || n == 9; }
 
 bool nodal_mode(const sem_ctx* c) {

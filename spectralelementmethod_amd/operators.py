@@ -91,7 +91,8 @@ class SEMOperator(object):
         How the Poisson action gets its geometric factors: re-derived per
         quadrature node from x_phys per global node ("nodal", least HBM
         traffic) or streamed from precomputed per-element factors ("stored");
-        "auto" (default) picks per order (nodal at p = 1, 2, 4, 5, 8).  See include/sem_hip.h
+        "auto" (default) picks per order (nodal at p = 1, 2, 4, 5, 8: the
+        library's measured table).  See include/sem_hip.h
         sem_set_geom_mode.
     kernel : {"auto", "column", "mfma"}
         Kernel family of the Poisson action: the LDS column kernel or the
