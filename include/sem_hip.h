@@ -131,7 +131,7 @@ int sem_set_map_shared(sem_ctx* ctx, const uint32_t* d_e2n, const uint8_t* d_nod
  * SEM_GEOM_STORED, AUTO resolved; nodal only once x_phys per node exists).
  * [20] scatter plan: 0 chains of consecutive elements (carry / merge codes),
  * 1 element-coloured chains (chosen when the element order defeats the chain
- * patterns: more than 1/16 of the groups would need atomics; SEM_PLAN=1 / 0
+ * patterns: more than half of the groups would need atomics; SEM_PLAN=1 / 0
  * in the environment forces / forbids it), 2 one element per wavefront
  * (MFMA kernel).  Writes min(n_info, 21) values. */
 int sem_plan_info(sem_ctx* ctx, int64_t* info, int n_info);
