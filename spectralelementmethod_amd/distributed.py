@@ -469,11 +469,12 @@ class OverlappedOperator(object):
     transport: "rccl" (native RCCL send/recv + all-reduce), "torch"
     (torch.distributed point-to-point, see TorchTransport), or "auto"
     (RCCL when the process group is NCCL and the communicator comes up,
-    torch otherwise)."""
+    torch otherwise).  decompose (default: world > 1) forces the sem_dd path
+    (tests run it on one rank to exercise the native RCCL calls)."""
 
     def __init__(self, p, nodes, e2n, neighbors, dofs_per_node=1, device=None, group=None,
                  geometry="auto", kind=0, kernel="auto", owned=None, transport="auto",
-                 world=None, rank=None):
+                 world=None, rank=None, decompose=None):
         from .operators import SEMOperator
         self.dpn = dofs_per_node
         self.kind = kind
@@ -493,7 +494,9 @@ class OverlappedOperator(object):
         self.exchange_bytes = 0
         kw = dict(dofs_per_node=dofs_per_node, device=self.device, geometry=geometry,
                   kernel=kernel)
-        if self.world == 1:
+        if decompose is None:
+            decompose = self.world > 1
+        if not decompose:
             self.ops = [SEMOperator(p, e2n, nodes, **kw)]
             self.n_iface_elem, self.n_interior_elem = 0, self.n_elem
             self.plan = None

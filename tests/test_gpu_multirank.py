@@ -202,3 +202,59 @@ def test_pcg_fixed_iterations_and_errors(gpu):
         op.pcg_solve(b, x.clone(), on, rtol=1e-14, max_iter=5)
     x, its, rel = op.pcg_solve(b, x, on, rtol=1e-12)
     assert rel <= 1e-12 and ((x - xs).norm() / xs.norm()).item() < 1e-9
+
+
+def _native_rccl_worker(q):
+    """One rank through the bench's process-group setup and the native RCCL
+    transport of sem_dd (communicator init, ncclAllReduce in the PCG; no peer
+    to send to at world size 1)."""
+    import sys
+    for pth in (ROOT, os.path.join(ROOT, "oracle")):
+        if pth not in sys.path:
+            sys.path.insert(0, pth)
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0",
+                      WORLD_SIZE="1")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("cpu:gloo,cuda:nccl", device_id=dev)  # as bench.py
+    try:
+        from spectralelementmethod_amd import meshgen
+        from spectralelementmethod_amd.distributed import OverlappedOperator, StripPartition
+        from spectralelementmethod_amd.operators import SEMOperator
+        dist.barrier()
+        part = StripPartition(10, 6, 4, 1, 0)
+        nodes, e2n = part.local_mesh(0.05)
+        op = OverlappedOperator(4, nodes, e2n, {}, 1, dev, owned=part.owned, transport="rccl",
+                                world=1, rank=0, decompose=True)
+        full = SEMOperator(4, e2n, nodes, device=dev)
+        u = torch.randn(full.ndof, dtype=torch.float64, device=dev,
+                        generator=torch.Generator(device=dev).manual_seed(2))
+        err = ((op.apply(u) - full.apply(u)).norm() / full.apply(u).norm()).item()
+        xs, on = _manufactured(nodes, dev)
+        b = full.apply(xs)
+        x1, its1, _ = full.pcg_solve(b, torch.where(on, xs, torch.zeros_like(xs)), on, rtol=1e-12)
+        x2, its2, _ = op.pcg_solve(b, torch.where(on, xs, torch.zeros_like(xs)), on, rtol=1e-12)
+        t = torch.tensor([1.0], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)       # bench's timing reduction (gloo)
+        got = [None]
+        dist.all_gather_object(got, 3.5)
+        q.put((op.transport, err, ((x2 - x1).norm() / x1.norm()).item(), its1, its2, got[0]))
+        op.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_native_rccl_transport_single_rank(gpu):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pr = ctx.Process(target=_native_rccl_worker, args=(q,))
+    pr.start()
+    try:
+        tr, err, err_pcg, its1, its2, got = q.get(timeout=150)
+    finally:
+        pr.join(timeout=60)
+    assert pr.exitcode == 0
+    assert tr == "rccl"
+    assert err < 1e-14 and err_pcg < 1e-12 and its1 == its2 and got == 3.5
