@@ -383,9 +383,9 @@ def test_mfma_auto_selection_and_limits(sem, poisson_action):
                       (16, "column")):
         nodes, e2n = meshgen.structured_square(3, 2, p)
         assert sem.SEMOperator(p, e2n, nodes).plan_info()["kernel"] == expect, p
-    # AUTO geometry per order (the column kernel's measured table)
-    for p, expect in ((2, "nodal"), (3, "stored"), (4, "nodal"), (7, "stored"), (8, "nodal"),
-                      (12, "stored")):
+    # AUTO geometry per order: only the orders with a clear measured win are
+    # pinned (p = 3, 5, 6, 7 were within 2-3 % in the sweep)
+    for p, expect in ((2, "nodal"), (4, "nodal"), (8, "nodal"), (12, "stored")):
         nodes, e2n = meshgen.structured_square(3, 2, p)
         assert sem.SEMOperator(p, e2n, nodes).plan_info()["geometry"] == expect, p
     # nodal geometry requested explicitly keeps the column kernel under auto
@@ -516,3 +516,18 @@ def test_axisym_ns_properties():
     jd = op.apply(d, kind="axisym_ns_jvp")
     cd = 0.5 * (op.apply(s + d, kind="axisym_ns") - op.apply(s - d, kind="axisym_ns"))
     assert (jd - cd).norm().item() <= 1e-12 * jd.norm().item()
+
+
+def test_apply_rejects_aliased_output(sem, poisson_action):
+    """u and y must not alias: the kernels read u while other workgroups
+    write y (include/sem_hip.h sem_apply); both the facade and the C ABI
+    refuse it."""
+    from spectralelementmethod_amd import _lib
+    fx = poisson_action
+    op = sem.SEMOperator(4, fx["p4_4x4_e2n"], fx["p4_4x4_nodes"])
+    u = torch.from_numpy(fx["p4_4x4_u"]).cuda()
+    with pytest.raises(ValueError):
+        op.apply(u, out=u)
+    op.compute_geometry()
+    rc = _lib.load().sem_apply(op._ctx, 0, _lib.tptr(u), _lib.tptr(u), 0, _lib.stream_ptr())
+    assert rc == _lib.SEM_E_INVALID and "overlap" in _lib.last_error()
