@@ -258,3 +258,60 @@ def test_native_rccl_transport_single_rank(gpu):
     assert pr.exitcode == 0
     assert tr == "rccl"
     assert err < 1e-14 and err_pcg < 1e-12 and its1 == its2 and got == 3.5
+
+
+def _axisym_worker(rank, world, port, q):
+    """The decomposition with two DOFs per node (interleaved psi, omega):
+    the axisymmetric Stokes block over theta-strips of a curved annulus."""
+    import sys
+    for pth in (ROOT, os.path.join(ROOT, "oracle")):
+        if pth not in sys.path:
+            sys.path.insert(0, pth)
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from spectralelementmethod_amd import meshgen
+        from spectralelementmethod_amd.distributed import GenericPartition, OverlappedOperator
+        from spectralelementmethod_amd.operators import AXISYM_STOKES, SEMOperator
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        p, nth, nr = 6, 9, 5
+        gnodes, ge2n = meshgen.annulus(nth, nr, p)
+        elem_rank = (np.arange(ge2n.shape[0]) * world) // ge2n.shape[0]  # theta strips
+        part = GenericPartition(ge2n, elem_rank, world, rank, dofs_per_node=2)
+        nodes, e2n = gnodes[:, part.l2g], part.e2n_local
+        op = OverlappedOperator(p, nodes, e2n, part.neighbors, 2, dev, owned=part.owned,
+                                kind=AXISYM_STOKES, transport="torch", world=world, rank=rank)
+        full = SEMOperator(p, ge2n, gnodes, dofs_per_node=2, device=dev)
+        g = torch.Generator(device=dev).manual_seed(9)
+        s = torch.randn(full.ndof, dtype=torch.float64, device=dev, generator=g)
+        ref = full.apply(s, kind="axisym_stokes")
+        dof = torch.from_numpy((part.l2g[:, None] * 2 + np.arange(2)).ravel()).to(dev)
+        y = op.apply(s[dof].contiguous())
+        q.put((rank, ((y - ref[dof]).norm() / ref[dof].norm()).item(), op.exchange_bytes))
+        op.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_overlapped_axisym_two_dofs_per_node(gpu):
+    import torch.multiprocessing as mp
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_axisym_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    try:
+        res = [q.get(timeout=150) for _ in range(world)]
+    finally:
+        for pr in procs:
+            pr.join(timeout=60)
+    for pr in procs:
+        assert pr.exitcode == 0
+    for rank, err, nbytes in res:
+        assert err < 1e-13, (rank, err)
+        assert nbytes > 0
