@@ -334,30 +334,30 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
       const double* GP = nodal ? nullptr : c->d_GP[0];
       const double2* XG = nodal ? c->d_XG : nullptr;
       if (nodal && c->map16)
-        hipLaunchKernelGGL((k_poisson_apply<N, true, true>), dim3(grid), dim3(CHAIN_BLOCK), 0, st,
+        hipLaunchKernelGGL((k_poisson_apply<N, true, true>), dim3(grid), dim3(ChainWaves<N>::block), 0, st,
                            mr, GP, XG, u, y, c0, c1, c->rounds, acc, D, w);
       else if (nodal)
-        hipLaunchKernelGGL((k_poisson_apply<N, true, false>), dim3(grid), dim3(CHAIN_BLOCK), 0,
+        hipLaunchKernelGGL((k_poisson_apply<N, true, false>), dim3(grid), dim3(ChainWaves<N>::block), 0,
                            st, mr, GP, XG, u, y, c0, c1, c->rounds, acc, D, w);
       else if (c->map16)
-        hipLaunchKernelGGL((k_poisson_apply<N, false, true>), dim3(grid), dim3(CHAIN_BLOCK), 0,
+        hipLaunchKernelGGL((k_poisson_apply<N, false, true>), dim3(grid), dim3(ChainWaves<N>::block), 0,
                            st, mr, GP, XG, u, y, c0, c1, c->rounds, acc, D, w);
       else
-        hipLaunchKernelGGL((k_poisson_apply<N, false, false>), dim3(grid), dim3(CHAIN_BLOCK), 0,
+        hipLaunchKernelGGL((k_poisson_apply<N, false, false>), dim3(grid), dim3(ChainWaves<N>::block), 0,
                            st, mr, GP, XG, u, y, c0, c1, c->rounds, acc, D, w);
     }
     else if (op_kind == SEM_OP_AXISYM_STOKES)
-      hipLaunchKernelGGL((k_axisym_apply<N, 0>), dim3(grid), dim3(CHAIN_BLOCK), 0, st, c->d_mapP,
+      hipLaunchKernelGGL((k_axisym_apply<N, 0>), dim3(grid), dim3(ChainWaves<N>::block), 0, st, c->d_mapP,
                          c->d_GP[1], u, y, c0, c1, c->rounds, acc, D, w, AxiNS());
     else {
       AxiNS ns;
       ns.re = c->reynolds;
       ns.lin = (op_kind == SEM_OP_AXISYM_NS_JVP || lin) ? c->d_lin : nullptr;
       if (op_kind == SEM_OP_AXISYM_NS)
-        hipLaunchKernelGGL((k_axisym_apply<N, 1>), dim3(grid), dim3(CHAIN_BLOCK), 0, st,
+        hipLaunchKernelGGL((k_axisym_apply<N, 1>), dim3(grid), dim3(ChainWaves<N>::block), 0, st,
                            c->d_mapP, c->d_GP[2], u, y, c0, c1, c->rounds, acc, D, w, ns);
       else
-        hipLaunchKernelGGL((k_axisym_apply<N, 2>), dim3(grid), dim3(CHAIN_BLOCK), 0, st,
+        hipLaunchKernelGGL((k_axisym_apply<N, 2>), dim3(grid), dim3(ChainWaves<N>::block), 0, st,
                            c->d_mapP, c->d_GP[2], u, y, c0, c1, c->rounds, acc, D, w, ns);
     }
   }
@@ -477,7 +477,7 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
                int rounds, const std::vector<uint8_t>& node_state, Plan& P) {
   const int epw = WAVE / n, lw = epw * n, nn = n * n;
   const int64_t n_groups = (n_elem + epw - 1) / epw;
-  const int CW = CHAIN_WAVES;  // groups of a chain that run concurrently
+  const int CW = chain_waves_of(n);  // groups of a chain that run concurrently
   const int CH = CW * rounds;
   const int64_t n_chains = (n_groups + CH - 1) / CH;
   auto is_bnd = [n](int r, int jj) { return r == 0 || r == n - 1 || jj == 0 || jj == n - 1; };
@@ -851,7 +851,7 @@ int build_plan_elem(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_
 // Elements are greedily coloured, in breadth-first order over shared nodes,
 // so that elements of one colour share no node, then packed colour class by
 // colour class, in that order inside a class, into groups of EPW elements and
-// chains of CHAIN_WAVES * rounds groups (a class's last group / chain may
+// chains of chain_waves_of(n) * rounds groups (a class's last group / chain may
 // be partly empty).  Nothing inside a launch shares a node, so the codes
 // are plain STORE (first writer in launch order) / RMW with no merge or
 // carry; elements needing more than MAX_COLOURS colours go to a final
@@ -862,7 +862,7 @@ int build_plan_elem(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_
 int build_plan_ecol(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node, int n,
                     int rounds, const std::vector<uint8_t>& node_state, Plan& P) {
   const int epw = WAVE / n, lw = epw * n, nn = n * n;
-  const int CH = CHAIN_WAVES * rounds;
+  const int CH = chain_waves_of(n) * rounds;
   auto is_bnd = [n](int r, int jj) { return r == 0 || r == n - 1 || jj == 0 || jj == n - 1; };
   std::vector<uint32_t> cnt(n_node, 0);
   P.owner.assign(n_node, 0xFFFFFFFFu);

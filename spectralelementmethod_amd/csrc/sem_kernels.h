@@ -40,11 +40,21 @@ namespace semk {
 
 constexpr int WAVE = 64;
 constexpr int BLOCK = 256;
-#ifndef SEM_CHAIN_WAVES
-#define SEM_CHAIN_WAVES 4
+// Groups per chain round = wavefronts per workgroup, per order: 4, and 2 at
+// n = 17 where a colour launch of the 4-wave form leaves the chip
+// under-filled (p = 16 at 1e7 DOF: 0.165 against 0.173 ms,
+// profiles/r02/variants).  SEM_CHAIN_WAVES (diagnostic builds) forces one
+// value for every order.
+#ifdef SEM_CHAIN_WAVES
+constexpr int chain_waves_of(int) { return SEM_CHAIN_WAVES; }
+#else
+constexpr int chain_waves_of(int n) { return n >= 17 ? 2 : 4; }
 #endif
-constexpr int CHAIN_WAVES = SEM_CHAIN_WAVES;  // groups per round = wavefronts per workgroup
-constexpr int CHAIN_BLOCK = CHAIN_WAVES * WAVE;
+template <int N>
+struct ChainWaves {
+  static constexpr int value = chain_waves_of(N);
+  static constexpr int block = value * WAVE;
+};
 constexpr int MAXN = 17;
 
 // packed map entry = gid | code << CODE_SHIFT
@@ -365,9 +375,10 @@ struct Tile {
   static constexpr int LW = EPW * N;
   static constexpr int RS = (PAD && N % 2) ? N + 1 : N;  // PAD: 16-B aligned rows
   static constexpr int ES = N * RS;
-  static constexpr int TILE_SLOTS = CHAIN_WAVES * EPW + (LW < WAVE ? 1 : 0);
+  static constexpr int CW = ChainWaves<N>::value;
+  static constexpr int TILE_SLOTS = CW * EPW + (LW < WAVE ? 1 : 0);
   __device__ static int slot(int wave, int k, bool in_wave) {
-    return in_wave ? wave * EPW + k : CHAIN_WAVES * EPW;
+    return in_wave ? wave * EPW + k : CW * EPW;
   }
 };
 
@@ -680,10 +691,10 @@ __device__ __forceinline__ void poisson_group_nodal(const MapRef& mref,
 // Scatter of one group's column values through the coded map, with the
 // in-group merge (next lane) and the chain carry (previous group) applied.
 // ncomp values per node (1: Poisson, 2: axisymmetric block).
-template <int N, int NC, bool PRE = false>
+template <int N, int NC, bool PRE = false, int CW = ChainWaves<N>::value>
 __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_t (&raw)[N],
                                            double (&v)[NC][N], int lane, int wave, int rd,
-                                           bool in_wave, double (*carry)[CHAIN_WAVES][NC][N],
+                                           bool in_wave, double (*carry)[CW][NC][N],
                                            int accumulate, const double* prev = nullptr) {
   constexpr int LW = Tile<N>::LW;
 #pragma unroll
@@ -704,7 +715,7 @@ __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_
   __syncthreads();
   if (lane == 0) {
     const double* src = (wave > 0) ? &carry[rd & 1][wave - 1][0][0]
-                                   : &carry[(rd + 1) & 1][CHAIN_WAVES - 1][0][0];
+                                   : &carry[(rd + 1) & 1][CW - 1][0][0];
 #pragma unroll
     for (int p = 0; p < N; ++p)
       if ((raw[p] >> CODE_SHIFT) & W_CARRY) {
@@ -762,7 +773,7 @@ struct PoissonMinWaves {
 };
 
 template <int N, bool NODAL, bool M16>
-__global__ void __launch_bounds__(CHAIN_BLOCK, (PoissonMinWaves<N, NODAL>::value))
+__global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODAL>::value))
     k_poisson_apply(const MapRef mref, const double* __restrict__ GP,
                     const double2* __restrict__ XG, const double* __restrict__ u,
                     double* __restrict__ y, int64_t c0, int64_t c1, int rounds, int accumulate,
@@ -770,7 +781,8 @@ __global__ void __launch_bounds__(CHAIN_BLOCK, (PoissonMinWaves<N, NODAL>::value
   using T = Tile<N, NODAL ? SEM_TILE_PAD_NODAL : SEM_TILE_PAD_STORED>;
   constexpr int NT = NODAL ? 2 : 1;  // tiles per element slot
   __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * T::ES * NT];
-  __shared__ double carry[2][CHAIN_WAVES][1][N];
+  constexpr int CW = ChainWaves<N>::value;
+  __shared__ double carry[2][CW][1][N];
   const int64_t chain = c0 + xcd_block(blockIdx.x, gridDim.x);
   if (chain >= c1) return;  // uniform over the workgroup
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);  // provably uniform
@@ -785,7 +797,7 @@ __global__ void __launch_bounds__(CHAIN_BLOCK, (PoissonMinWaves<N, NODAL>::value
   double* LB = L + (NT - 1) * T::TILE_SLOTS * T::ES;
   const double wj = pick<N>(w, j);
   for (int rd = 0; rd < rounds; ++rd) {
-    const int64_t g = (chain * rounds + rd) * CHAIN_WAVES + wave;
+    const int64_t g = (chain * rounds + rd) * CW + wave;
     uint32_t raw[N];
     double v[1][N], prev[N];
     if constexpr (NODAL)
@@ -955,13 +967,14 @@ __device__ __forceinline__ void axisym_group(const uint32_t* __restrict__ mapP,
 }
 
 template <int N, int MODE>
-__global__ void __launch_bounds__(CHAIN_BLOCK)
+__global__ void __launch_bounds__(ChainWaves<N>::block)
     k_axisym_apply(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
                    const double* __restrict__ u, double* __restrict__ y, int64_t c0, int64_t c1,
                    int rounds, int accumulate, const DEO<N> D, const WVec<N> w, const AxiNS ns) {
   using T = Tile<N>;
   __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * 2 * T::ES];
-  __shared__ double carry[2][CHAIN_WAVES][2][N];
+  constexpr int CW = ChainWaves<N>::value;
+  __shared__ double carry[2][CW][2][N];
   const int64_t chain = c0 + blockIdx.x;
   if (chain >= c1) return;
   const int wave = threadIdx.x / WAVE;
@@ -973,7 +986,7 @@ __global__ void __launch_bounds__(CHAIN_BLOCK)
   double* LP = lds + T::slot(wave, k, in_wave) * T::ES;  // psi tile plane
   double* LO = LP + T::TILE_SLOTS * T::ES;                // omega tile plane
   for (int rd = 0; rd < rounds; ++rd) {
-    const int64_t g = (chain * rounds + rd) * CHAIN_WAVES + wave;
+    const int64_t g = (chain * rounds + rd) * CW + wave;
     uint32_t raw[N];
     double v[2][N];  // [0] omega row (y[2k]), [1] psi row (y[2k+1])
     axisym_group<N, MODE>(mapP, GP, u, g, lane, j, in_wave, LP, LO, D, w, wj, ns, raw, v[0],
