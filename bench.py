@@ -71,11 +71,13 @@ def streamed_bytes(kind, n_nodes, n_elem, p, geometry, map_bytes):
     map_bytes = 2: 16-bit packed map plus one uint32 base per group row."""
     n = p + 1
     n2 = n * n
-    if kind != "poisson":
-        return alg_bytes_s8d(kind, n_nodes, n_elem, p)
     m = map_bytes * n_elem * n2
     if map_bytes == 2:
         m += 4 * n * n_elem // (64 // n)
+    if kind != "poisson":
+        if geometry == "nodal":  # (psi, omega) read + written, x_phys read
+            return 48 * n_nodes + m
+        return alg_bytes_s8d(kind, n_nodes, n_elem, p)
     if geometry == "nodal":
         return 32 * n_nodes + m
     return 16 * n_nodes + 24 * n_elem * n2 + m
@@ -86,10 +88,12 @@ def alg_flops(kind, n_elem, p, geometry="stored"):
     plus pointwise work; nodal geometry adds the four derivatives of x_phys
     and the per-node det / inverse / detJxW (15 n^2 incl. one division)."""
     n = p + 1
+    extra = 8 * n ** 3 + 15 * n ** 2 if geometry == "nodal" else 0
     if kind == "poisson":
-        extra = 8 * n ** 3 + 15 * n ** 2 if geometry == "nodal" else 0
         return n_elem * (8 * n ** 3 + 7 * n ** 2 + extra)
-    return n_elem * (16 * n ** 3 + (30 if kind == "axisym_ns" else 22) * n ** 2)
+    if geometry == "nodal":  # + the seven factors from J and rho (two reciprocals)
+        extra += 16 * n ** 2
+    return n_elem * (16 * n ** 3 + (30 if kind == "axisym_ns" else 22) * n ** 2 + extra)
 
 
 # ---------------------------------------------------------------- CPU baseline
@@ -329,7 +333,7 @@ def main():
     t_mesh = time.time() - t0
     log("rank %d: mesh %d elements, %d nodes (%.1fs)" % (rank, e2n.shape[0], nodes.shape[1],
                                                           t_mesh))
-    geometry = args.geometry if kind == POISSON else "stored"
+    geometry = args.geometry if kind in (POISSON, AXISYM_STOKES) else "stored"
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     op = OverlappedOperator(p, nodes, e2n, part.neighbors if world > 1 else {}, dpn, dev,
@@ -341,7 +345,9 @@ def main():
         for o in op.ops:
             o.set_reynolds(args.re)
     plan = op.plan_info()
-    geometry = plan["geometry"] if kind == POISSON else "stored"  # as the library resolved it
+    # as the library resolved it
+    geometry = (plan["geometry"] if kind == POISSON else
+                plan["geometry_axisym"] if kind == AXISYM_STOKES else "stored")
     log("rank %d: plan %s; %d interface + %d interior elements; transport %s; setup %.2fs" % (
         rank, plan, op.n_iface_elem, op.n_interior_elem, op.transport, t_setup))
     n_elem_local = op.n_elem
@@ -395,8 +401,8 @@ def main():
             assert parity["rel_l2"] < parity["tolerance"], parity
 
     value = ndof_global * args.steps / elapsed
-    map_bytes = plan.get("map_entry_bytes", 4) if (plan["kernel"] == "column"
-                                                  and kind == POISSON) else 4
+    map_bytes = plan.get("map_entry_bytes", 4) if (
+        plan["kernel"] == "column" and (kind == POISSON or geometry == "nodal")) else 4
     B = alg_bytes_s8d(kname, n_nodes_local, n_elem_local, p)
     B_stream = streamed_bytes(kname, n_nodes_local, n_elem_local, p, geometry, map_bytes)
     F = alg_flops(kname, n_elem_local, p, geometry)
@@ -458,7 +464,8 @@ def main():
             "frac_streamed_min": B_stream / kern_avg_s / 1e9 / HBM_PEAK_GBS,
             "kernel": (("k_poisson_mfma<%d>" if plan["kernel"] == "mfma" else
                         "k_poisson_apply<%d>") % (p + 1) if kind == POISSON else
-                       "k_axisym_apply<%d>" % (p + 1)),
+                       ("k_axisym_nodal<%d>" if geometry == "nodal" else "k_axisym_apply<%d>")
+                       % (p + 1)),
             "launch": ("one sem_apply = %d colour launches" % plan["colours"]) if world == 1 else
             "one sem_dd_apply (interface + interior elements + exchange), per rank",
             "fp64_tflops": F / kern_avg_s / 1e12, "fp64_peak_tflops": FP64_PEAK_TFLOPS,

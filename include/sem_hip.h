@@ -133,7 +133,8 @@ int sem_set_map_shared(sem_ctx* ctx, const uint32_t* d_e2n, const uint8_t* d_nod
  * 1 element-coloured chains (chosen when the element order defeats the chain
  * patterns: more than half of the groups would need atomics; SEM_PLAN=1 / 0
  * in the environment forces / forbids it), 2 one element per wavefront
- * (MFMA kernel).  Writes min(n_info, 21) values. */
+ * (MFMA kernel).  [21] the axisymmetric Stokes geometry mode (as [19];
+ * 0 when dofs_per_node != 2).  Writes min(n_info, 22) values. */
 int sem_plan_info(sem_ctx* ctx, int64_t* info, int n_info);
 
 /* How the Poisson action obtains its geometric factors.
@@ -149,7 +150,12 @@ int sem_plan_info(sem_ctx* ctx, int64_t* info, int n_info);
  *  SEM_GEOM_STORED: the 3 factors per quadrature node are precomputed and
  *    streamed (24 B per element node).
  * Takes effect at the next sem_geom_from_nodes; sem_set_geom always installs
- * stored factors.  The axisymmetric block always uses stored factors. */
+ * stored factors.  The axisymmetric Stokes block (SEM_OP_AXISYM_STOKES) reads
+ * the same modes: NODAL re-derives its 7 factors per node from x_phys, with
+ * rho = x (16 B/node instead of 56 B per element node; AUTO: NODAL,
+ * DESIGN.md §4.2); the Navier-Stokes kinds always use stored factors.
+ * x_phys per node is one array per context: sem_geom_from_nodes of either
+ * kind recomputes it from the nodes it is given. */
 #define SEM_GEOM_STORED 0
 #define SEM_GEOM_NODAL 1
 #define SEM_GEOM_AUTO 2

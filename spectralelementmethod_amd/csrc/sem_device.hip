@@ -213,7 +213,8 @@ struct sem_ctx {
   bool ecol = false;  // column kernel on the element-coloured plan
   double2* d_XG = nullptr;
   uint32_t* d_owner = nullptr;
-  bool xg_valid = false;
+  bool xg_valid = false;  // the Poisson action reads d_XG
+  bool xg_axi = false;    // the axisymmetric Stokes action reads d_XG
   unsigned long long* d_bad = nullptr;
 };
 
@@ -302,8 +303,27 @@ bool want_mfma(const sem_ctx* c) {
   return c->n >= SEM_MFMA_MIN_N && c->geom_mode != SEM_GEOM_NODAL;
 }
 
+// axisymmetric Stokes block (dpn = 2, column kernel only): AUTO picks NODAL
+// where it measured faster at ~9.4e6 nodes (DESIGN.md §4.2,
+// profiles/r02/axisym): p = 2 / 4 / 6 0.226 / 0.192 / 0.214 ms against
+// 0.367 / 0.306 / 0.305 stored, p = 16 0.428 vs 0.481; STORED at p = 8..12
+// (0.275 vs 0.286 at p = 8, 0.286 vs 0.421 at p = 10: the nodal kernel's
+// register demand drops it to one wave per SIMD).  Unmeasured orders follow
+// their neighbours.
+bool auto_nodal_axi_order(int n) { return n <= 7 || n == 17; }
+
+bool nodal_mode_op(const sem_ctx* c, int op_kind) {
+  if (op_kind == SEM_OP_POISSON) return nodal_mode(c);
+  if (op_kind == SEM_OP_AXISYM_STOKES)
+    return c->geom_mode == SEM_GEOM_NODAL ||
+           (c->geom_mode == SEM_GEOM_AUTO && auto_nodal_axi_order(c->n));
+  return false;  // Navier-Stokes: stored factors
+}
+
 bool use_nodal(const sem_ctx* c, int op_kind) {
-  return op_kind == SEM_OP_POISSON && nodal_mode(c) && c->xg_valid;
+  if (op_kind == SEM_OP_POISSON) return nodal_mode(c) && c->xg_valid;
+  if (op_kind == SEM_OP_AXISYM_STOKES) return nodal_mode_op(c, op_kind) && c->xg_axi;
+  return false;
 }
 
 template <int N>
@@ -346,7 +366,15 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
         hipLaunchKernelGGL((k_poisson_apply<N, false, false>), dim3(grid), dim3(ChainWaves<N>::block), 0,
                            st, mr, GP, XG, u, y, c0, c1, c->rounds, acc, D, w);
     }
-    else if (op_kind == SEM_OP_AXISYM_STOKES)
+    else if (op_kind == SEM_OP_AXISYM_STOKES && nodal) {
+      const MapRef mr{c->d_mapP, c->d_map16, c->d_mbase};
+      if (c->map16)
+        hipLaunchKernelGGL((k_axisym_nodal<N, true>), dim3(grid), dim3(ChainWaves<N>::block), 0,
+                           st, mr, c->d_XG, u, y, c0, c1, c->rounds, acc, D, w);
+      else
+        hipLaunchKernelGGL((k_axisym_nodal<N, false>), dim3(grid), dim3(ChainWaves<N>::block), 0,
+                           st, mr, c->d_XG, u, y, c0, c1, c->rounds, acc, D, w);
+    } else if (op_kind == SEM_OP_AXISYM_STOKES)
       hipLaunchKernelGGL((k_axisym_apply<N, 0>), dim3(grid), dim3(ChainWaves<N>::block), 0, st, c->d_mapP,
                          c->d_GP[1], u, y, c0, c1, c->rounds, acc, D, w, AxiNS());
     else {
@@ -1193,25 +1221,30 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
   c->d_lin = nullptr;
   c->lin_valid = false;
   c->xg_valid = false;
+  c->xg_axi = false;
   return SEM_OK;
 }
 
 int sem_plan_info(sem_ctx* c, int64_t* info, int n_info) {
   if (!c || !info || n_info < 1) return fail(SEM_E_INVALID, "bad arguments");
   const int64_t nc = c->colour_start.empty() ? 0 : (int64_t)c->colour_start.size() - 1;
-  constexpr int NV = 8 + MAX_COLOURS + 1 + 1 + 1 + 1 + 1;
+  constexpr int NV = 8 + MAX_COLOURS + 1 + 1 + 1 + 1 + 1 + 1;
   int64_t vals[NV] = {c->n_groups, c->n_zero, c->n_atomic_groups, c->conforming ? 1 : 0,
                       c->epw,      nc,        c->rounds,          c->n_slots};
   for (int64_t q = 0; q < nc && q <= MAX_COLOURS; ++q)
     vals[8 + q] = c->colour_start[q + 1] - c->colour_start[q];
-  vals[NV - 4] = c->mfma ? SEM_KERNEL_MFMA : SEM_KERNEL_COLUMN;
-  vals[NV - 3] = c->map16 ? 2 : 4;  // bytes per packed map entry
+  vals[NV - 5] = c->mfma ? SEM_KERNEL_MFMA : SEM_KERNEL_COLUMN;
+  vals[NV - 4] = c->map16 ? 2 : 4;  // bytes per packed map entry
   // the geometry the Poisson action actually uses: nodal only once x_phys
   // per node exists (sem_set_geom installs stored factors); before any
   // geometry, the mode sem_geom_from_nodes will resolve to
   const bool eff_nodal = c->xg_valid ? true : (c->d_GP[0] ? false : nodal_mode(c));
-  vals[NV - 2] = eff_nodal ? SEM_GEOM_NODAL : SEM_GEOM_STORED;
-  vals[NV - 1] = c->mfma ? 2 : (c->ecol ? 1 : 0);  // plan: chains, element-coloured, element
+  vals[NV - 3] = eff_nodal ? SEM_GEOM_NODAL : SEM_GEOM_STORED;
+  vals[NV - 2] = c->mfma ? 2 : (c->ecol ? 1 : 0);  // plan: chains, element-coloured, element
+  // the same for the axisymmetric Stokes block (dofs_per_node = 2)
+  const bool axi_nodal =
+      c->xg_axi ? true : (c->d_GP[1] ? false : nodal_mode_op(c, SEM_OP_AXISYM_STOKES));
+  vals[NV - 1] = c->dpn == 2 ? (axi_nodal ? SEM_GEOM_NODAL : SEM_GEOM_STORED) : 0;
   for (int i = 0; i < n_info && i < NV; ++i) info[i] = vals[i];
   return SEM_OK;
 }
@@ -1257,13 +1290,13 @@ int sem_geom_from_nodes(sem_ctx* c, const double* d_nodes, const double* h_Vinv,
   int rc = geom_common(c, d_nodes, h_Vinv);
   if (rc) return rc;
   if ((rc = check_op(c, op_kind))) return rc;
-  const bool nodal = op_kind == SEM_OP_POISSON && nodal_mode(c);
+  const bool nodal = nodal_mode_op(c, op_kind);
   double* GP = nullptr;
   if (nodal) {
     if (!c->d_XG) HIP_TRY(hipMalloc(&c->d_XG, c->n_node * sizeof(double2)));
     // stale stored factors would otherwise survive for sem_diag
-    (void)hipFree(c->d_GP[0]);
-    c->d_GP[0] = nullptr;
+    (void)hipFree(c->d_GP[gp_slot(op_kind)]);
+    c->d_GP[gp_slot(op_kind)] = nullptr;
   } else {
     if ((rc = ensure_gp(c, op_kind, S(stream)))) return rc;
     GP = c->d_GP[gp_slot(op_kind)];
@@ -1279,7 +1312,10 @@ int sem_geom_from_nodes(sem_ctx* c, const double* d_nodes, const double* h_Vinv,
   HIP_TRY(hipStreamSynchronize(st));
   if (n_bad_nodes) *n_bad_nodes = (int64_t)bad;
   if (bad) return fail(SEM_E_DETJ, "detJ <= 0 at " + std::to_string(bad) + " quadrature nodes");
+  // x_phys per node is one array for the mesh: recomputed here, from these
+  // nodes, for every operator that reads it
   if (op_kind == SEM_OP_POISSON) c->xg_valid = nodal;
+  if (op_kind == SEM_OP_AXISYM_STOKES) c->xg_axi = nodal;
   if (gp_slot(op_kind) == 2) c->lin_valid = false;  // linearisation used the old factors
   return SEM_OK;
 }
@@ -1308,6 +1344,7 @@ int sem_set_geom(sem_ctx* c, const double* d_G, int op_kind, void* stream) {
   if ((rc = ensure_gp(c, op_kind, S(stream)))) return rc;
   const int ncomp = sem_op_ncomp(op_kind);
   if (op_kind == SEM_OP_POISSON) c->xg_valid = false;  // caller's factors take over
+  if (op_kind == SEM_OP_AXISYM_STOKES) c->xg_axi = false;
   hipLaunchKernelGGL(k_pack_geom, dim3(grid_for(c->n_elem * ncomp * c->n * c->n)), dim3(BLOCK), 0,
                      S(stream), d_G, c->n_elem, c->n, ncomp, c->epw, c->d_epos,
                      c->d_GP[gp_slot(op_kind)]);

@@ -966,6 +966,206 @@ __device__ __forceinline__ void axisym_group(const uint32_t* __restrict__ mapP,
   wave_sync();
 }
 
+// ---------------------------------------------------------------------------
+// Axisymmetric Stokes block with NODAL geometry: the seven factors of the
+// lane's column are re-derived per node from x_phys per global node, as in
+// the Poisson NODAL group (J along the column in registers, along the row
+// through the tiles, coordinates relative to the line's first node), with
+// rho = x (squirmer-axisymmetric.py:193-227).  With ww = w_m w_j:
+//   G..rho = rho (ww / det) (the Poisson combinations of J),
+//   b0 = 2 W iJ00 = 2 ww J11,   b1 = 2 W iJ10 = -2 ww J10,
+//   c = W / rho,   m = rho^2 W,   W = ww det.
+// 16 B of x_phys per node replace 56 B of factors per element node.
+// ---------------------------------------------------------------------------
+#ifndef SEM_AXI_MIN_WAVES
+#define SEM_AXI_MIN_WAVES 1
+#endif
+#ifndef SEM_AXI_EARLY_U
+#define SEM_AXI_EARLY_U 0
+#endif
+template <int N, bool M16>
+__device__ __forceinline__ void axisym_group_nodal(const MapRef& mref,
+                                                   const double2* __restrict__ XG,
+                                                   const double* __restrict__ u, int64_t g,
+                                                   int lane, int j, bool in_wave, double* LP,
+                                                   double* LO, const DEO<N>& D, const WVec<N>& w,
+                                                   double wj, uint32_t (&raw)[N], double (&vo)[N],
+                                                   double (&vp)[N]) {
+  constexpr int RS = Tile<N>::RS;
+  load_map<N, M16>(mref, g, lane, in_wave, raw);
+  double2 xc[N];
+  gather_x<N>(XG, raw, j, xc);
+  const double2* u2 = reinterpret_cast<const double2*>(u);
+  double ps[N], om[N];
+#if SEM_AXI_EARLY_U
+#pragma unroll
+  for (int r = 0; r < N; ++r) {
+    const double2 val = u2[raw[r] & GID_MASK];
+    ps[r] = val.x;
+    om[r] = val.y;
+  }
+#endif
+  // Jacobian: jr = d(x, y)/dr along the column, js = d(x, y)/ds along the row
+  double jr0[N], jr1[N], js0[N], js1[N], rho[N];
+  {
+    double ta[N], tb[N];
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      ta[r] = xc[r].x - xc[0].x;
+      tb[r] = xc[r].y - xc[0].y;
+      rho[r] = xc[r].x;
+    }
+    deo_apply<N>(D, ta, jr0);
+    deo_apply<N>(D, tb, jr1);
+  }
+#pragma unroll
+  for (int r = 0; r < N; ++r) {
+    LP[r * RS + j] = xc[r].x;
+    LO[r * RS + j] = xc[r].y;
+  }
+  wave_sync();
+  {
+    double xa[RS], xb[RS], ra[N], rb[N], ta[N], tb[N];
+    load_row<N, RS>(LP, j, xa);
+    load_row<N, RS>(LO, j, xb);
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+      ra[q] = xa[q] - xa[0];
+      rb[q] = xb[q] - xb[0];
+    }
+    deo_apply<N>(D, ra, ta);
+    deo_apply<N>(D, rb, tb);
+    wave_sync();
+    store_row<N, RS>(LP, j, ta);
+    store_row<N, RS>(LO, j, tb);
+  }
+  wave_sync();
+  // own column slots: read js, then the same lane rewrites them with psi/omega
+#pragma unroll
+  for (int m = 0; m < N; ++m) {
+    js0[m] = LP[m * RS + j];
+    js1[m] = LO[m * RS + j];
+  }
+#if !SEM_AXI_EARLY_U
+#pragma unroll
+  for (int r = 0; r < N; ++r) {
+    const double2 val = u2[raw[r] & GID_MASK];
+    ps[r] = val.x;
+    om[r] = val.y;
+  }
+#endif
+  double d0p[N], d0o[N];
+  deo_apply<N>(D, ps, d0p);
+  deo_apply<N>(D, om, d0o);
+#pragma unroll
+  for (int r = 0; r < N; ++r) {
+    LP[r * RS + j] = ps[r];
+    LO[r * RS + j] = om[r];
+  }
+  wave_sync();
+  {
+    double rp[RS], ro[RS], xp[N], xo[N], tp[N], to[N];
+    load_row<N, RS>(LP, j, rp);
+    load_row<N, RS>(LO, j, ro);
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+      xp[q] = rp[q];
+      xo[q] = ro[q];
+    }
+    deo_apply<N>(D, xp, tp);
+    deo_apply<N>(D, xo, to);
+    wave_sync();
+    store_row<N, RS>(LP, j, tp);
+    store_row<N, RS>(LO, j, to);
+  }
+  wave_sync();
+#pragma unroll
+  for (int m = 0; m < N; ++m) {
+    const double d1p = LP[m * RS + j];
+    const double d1o = LO[m * RS + j];
+    const double det = jr0[m] * js1[m] - js0[m] * jr1[m];
+    const double wm = w.v[m];
+    const double rs = rho[m] * (wm * (wj * fast_rcp(det)));
+    const double g00 = rs * fma(js1[m], js1[m], js0[m] * js0[m]);
+    const double g01 = -rs * fma(js1[m], jr1[m], js0[m] * jr0[m]);
+    const double g11 = rs * fma(jr1[m], jr1[m], jr0[m] * jr0[m]);
+    const double W = wm * (wj * det);
+    const double b0 = 2.0 * wm * (wj * js1[m]);
+    const double b1 = -2.0 * wm * (wj * jr1[m]);
+    const double c = W * fast_rcp(rho[m]);
+    const double mm = rho[m] * rho[m] * W;
+    // w1 -> own slot (read above); w0 and the pointwise terms stay in registers
+    LP[m * RS + j] = fma(g01, d0p[m], g11 * d1p);
+    LO[m * RS + j] = fma(g01, d0o[m], g11 * d1o);
+    vp[m] = fma(b0, d0p[m], fma(b1, d1p, -mm * om[m]));
+    vo[m] = c * om[m];
+    d0p[m] = fma(g00, d0p[m], g01 * d1p);
+    d0o[m] = fma(g00, d0o[m], g01 * d1o);
+  }
+  {
+    double tp[N], to[N];
+    deo_apply_t<N>(D, d0p, tp);
+    deo_apply_t<N>(D, d0o, to);
+#pragma unroll
+    for (int p = 0; p < N; ++p) {
+      vp[p] += tp[p];
+      vo[p] += to[p];
+    }
+  }
+  wave_sync();
+  {
+    double rp[RS], ro[RS], xp[N], xo[N], tp[N], to[N];
+    load_row<N, RS>(LP, j, rp);
+    load_row<N, RS>(LO, j, ro);
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+      xp[q] = rp[q];
+      xo[q] = ro[q];
+    }
+    deo_apply_t<N>(D, xp, tp);
+    deo_apply_t<N>(D, xo, to);
+    wave_sync();
+    store_row<N, RS>(LP, j, tp);
+    store_row<N, RS>(LO, j, to);
+  }
+  wave_sync();
+#pragma unroll
+  for (int p = 0; p < N; ++p) {
+    vo[p] += LO[p * RS + j];
+    vp[p] += LP[p * RS + j];
+  }
+  wave_sync();
+}
+
+template <int N, bool M16>
+__global__ void __launch_bounds__(ChainWaves<N>::block, SEM_AXI_MIN_WAVES)
+    k_axisym_nodal(const MapRef mref, const double2* __restrict__ XG, const double* __restrict__ u,
+                   double* __restrict__ y, int64_t c0, int64_t c1, int rounds, int accumulate,
+                   const DEO<N> D, const WVec<N> w) {
+  using T = Tile<N>;
+  __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * 2 * T::ES];
+  constexpr int CW = ChainWaves<N>::value;
+  __shared__ double carry[2][CW][2][N];
+  const int64_t chain = c0 + blockIdx.x;
+  if (chain >= c1) return;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
+  const int lane = threadIdx.x % WAVE;
+  const int k = lane / N;
+  const int j = lane - k * N;
+  const bool in_wave = lane < T::LW;
+  const double wj = pick<N>(w, j);
+  double* LP = lds + T::slot(wave, k, in_wave) * T::ES;
+  double* LO = LP + T::TILE_SLOTS * T::ES;
+  for (int rd = 0; rd < rounds; ++rd) {
+    const int64_t g = (chain * rounds + rd) * CW + wave;
+    uint32_t raw[N];
+    double v[2][N];  // [0] omega row (y[2k]), [1] psi row (y[2k+1])
+    axisym_group_nodal<N, M16>(mref, XG, u, g, lane, j, in_wave, LP, LO, D, w, wj, raw, v[0],
+                               v[1]);
+    chain_emit<N, 2>(y, raw, v, lane, wave, rd, in_wave, carry, accumulate);
+  }
+}
+
 template <int N, int MODE>
 __global__ void __launch_bounds__(ChainWaves<N>::block)
     k_axisym_apply(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,

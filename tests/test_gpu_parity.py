@@ -93,20 +93,23 @@ def test_geometry_fields_golden(sem, poisson_action, name):
         assert rel_l2(got, ref) < TOL_GEOM, key
 
 
+@pytest.mark.parametrize("geometry", GEOMETRY)
 @pytest.mark.parametrize("name", ["p6_4x8", "p4_3x2"])
-def test_axisym_block_golden(sem, axisym_action, name):
-    op = make_op(sem, axisym_action, name, dpn=2)
+def test_axisym_block_golden(sem, axisym_action, name, geometry):
+    op = make_op(sem, axisym_action, name, dpn=2, geometry=geometry)
     sol = torch.from_numpy(axisym_action[name + "_soln"]).cuda()
     y = op.apply(sol, kind="axisym_stokes").cpu().numpy()
+    assert op.plan_info()["geometry_axisym"] == geometry
     ref = axisym_action[name + "_block"]
     assert rel_l2(y[0::2], ref[0::2]) < TOL_AXISYM     # Lve . omega
     assert rel_l2(y[1::2], ref[1::2]) < TOL_AXISYM     # E2e . psi - Me . omega
 
 
-def test_axisym_components_golden(sem, axisym_action):
+@pytest.mark.parametrize("geometry", GEOMETRY)
+def test_axisym_components_golden(sem, axisym_action, geometry):
     """Separate E2e.psi, Lve.omega and Me.omega via zeroed inputs."""
     name = "p6_4x8"
-    op = make_op(sem, axisym_action, name, dpn=2)
+    op = make_op(sem, axisym_action, name, dpn=2, geometry=geometry)
     psi = axisym_action[name + "_psi"]
     om = axisym_action[name + "_omega"]
     z = np.zeros_like(psi)
@@ -388,6 +391,12 @@ def test_mfma_auto_selection_and_limits(sem, poisson_action):
     for p, expect in ((2, "nodal"), (4, "nodal"), (8, "nodal"), (12, "stored")):
         nodes, e2n = meshgen.structured_square(3, 2, p)
         assert sem.SEMOperator(p, e2n, nodes).plan_info()["geometry"] == expect, p
+    # axisymmetric Stokes block: NODAL at p <= 6 and p = 16, STORED at 8..12
+    for p, expect in ((2, "nodal"), (6, "nodal"), (10, "stored")):
+        nodes, e2n = meshgen.annulus(3, 2, p)
+        op = sem.SEMOperator(p, e2n, nodes, dofs_per_node=2)
+        op.apply(torch.zeros(op.ndof, dtype=torch.float64, device="cuda"), kind="axisym_stokes")
+        assert op.plan_info()["geometry_axisym"] == expect, p
     # nodal geometry requested explicitly keeps the column kernel under auto
     nodes, e2n = meshgen.structured_square(3, 2, 12)
     assert sem.SEMOperator(12, e2n, nodes, geometry="nodal").plan_info()["kernel"] == "column"

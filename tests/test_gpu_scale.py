@@ -13,7 +13,8 @@ relative L2.
   geometry (element-relative coordinates) is checked against the
   extended-precision oracle on the golden meshes instead
   (test_gpu_parity.py);
-* config 5: the axisymmetric Stokes block on a 128 x 128 curved annulus, p = 6.
+* config 5: the axisymmetric Stokes block on a 128 x 128 curved annulus, p = 6,
+  with the factors re-derived per node from x_phys (NODAL) and streamed.
 
 The meshes are warped (non-constant Jacobians) and u ~ N(0, 1)."""
 import numpy as np
@@ -81,7 +82,8 @@ def test_config4_high_order_action_vs_oracle(gpu, gll, p, nex, kernel):
     assert rel_l2(y, ref) < TOL, (p, kernel, rel_l2(y, ref))
 
 
-def test_config5_axisym_vs_oracle(gpu, gll):
+@pytest.mark.parametrize("geometry", ["nodal", "stored"])
+def test_config5_axisym_vs_oracle(gpu, gll, geometry):
     import sem_oracle
     from spectralelementmethod_amd import meshgen
     from spectralelementmethod_amd.operators import SEMOperator
@@ -95,7 +97,8 @@ def test_config5_axisym_vs_oracle(gpu, gll):
     F = sem_oracle.axisym_factors(xp, invJ, detJxW)
     sol = np.random.default_rng(6).standard_normal(2 * nodes.shape[1])
     ref = sem_oracle.axisym_apply(F, D, e2n64, sol, nodes.shape[1])
-    op = SEMOperator(p, e2n, nodes, dofs_per_node=2, device=gpu)
+    op = SEMOperator(p, e2n, nodes, dofs_per_node=2, device=gpu, geometry=geometry)
     y = op.apply(torch.from_numpy(sol).to(gpu), kind="axisym_stokes").cpu().numpy()
+    assert op.plan_info()["geometry_axisym"] == geometry
     assert rel_l2(y[0::2], ref[0::2]) < TOL
     assert rel_l2(y[1::2], ref[1::2]) < TOL
