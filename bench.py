@@ -451,8 +451,9 @@ def main():
             "gflops_kernel": F / kern_avg_s / 1e9,
             "kernel_family": plan["kernel"], "map_entry_bytes": map_bytes,
             "gpu_setup_sec": t_setup, "gpu_setup_sec_per_elem": t_setup / max(1, n_elem_local),
-            "scatter_plan": {k: plan[k] for k in ("colours", "chains_per_colour", "rounds",
-                                                  "zero_list", "atomic_groups")},
+            "scatter_plan": {k: plan[k] for k in ("plan", "colours", "chains_per_colour", "rounds",
+                                                  "zero_list", "atomic_groups", "dependencies",
+                                                  "lag", "wait_timeouts")},
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -466,7 +467,9 @@ def main():
                         "k_poisson_apply<%d>") % (p + 1) if kind == POISSON else
                        ("k_axisym_nodal<%d>" if geometry == "nodal" else "k_axisym_apply<%d>")
                        % (p + 1)),
-            "launch": ("one sem_apply = %d colour launches" % plan["colours"]) if world == 1 else
+            "launch": ("one sem_apply = one launch of %d chains (k_df_begin + the action)"
+                       % plan["chains_per_colour"][0] if plan["plan"] == "chains-one-launch" else
+                       "one sem_apply = %d colour launches" % plan["colours"]) if world == 1 else
             "one sem_dd_apply (interface + interior elements + exchange), per rank",
             "fp64_tflops": F / kern_avg_s / 1e12, "fp64_peak_tflops": FP64_PEAK_TFLOPS,
             "traffic_source": os.path.relpath(traffic_src, ROOT) if traffic is not None else None,

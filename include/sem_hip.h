@@ -133,8 +133,19 @@ int sem_set_map_shared(sem_ctx* ctx, const uint32_t* d_e2n, const uint8_t* d_nod
  * 1 element-coloured chains (chosen when the element order defeats the chain
  * patterns: more than half of the groups would need atomics; SEM_PLAN=1 / 0
  * in the environment forces / forbids it), 2 one element per wavefront
- * (MFMA kernel).  [21] the axisymmetric Stokes geometry mode (as [19];
- * 0 when dofs_per_node != 2).  Writes min(n_info, 22) values. */
+ * (MFMA kernel), 3 chains of consecutive elements in ONE launch (the
+ * Poisson column kernel's default when dofs_per_node == 1; SEM_DF=0 in the
+ * environment gives one launch per colour class instead): workgroups take
+ * chains from a ticket counter, and a chain starts once every chain that
+ * wrote one of its shared nodes earlier in ticket order has published
+ * (per-chain flags); [5] is then 1 and [8] the chain count.
+ * [21] the axisymmetric Stokes geometry mode (as [19]; 0 when
+ * dofs_per_node != 2).  [22] dependency edges of the one-launch plan, [23]
+ * its colour lag in chains (SEM_DF_LAG), [24] dependency waits that hit
+ * their spin limit since sem_set_map (never expected; read from the device,
+ * so a request for 25 values synchronises with it).  Writes min(n_info, 25)
+ * values.  A context's actions must not run concurrently with each other
+ * (one stream at a time): the one-launch plan's counters are per context. */
 int sem_plan_info(sem_ctx* ctx, int64_t* info, int n_info);
 
 /* How the Poisson action obtains its geometric factors.

@@ -173,6 +173,11 @@ inline int grid_for(int64_t n, int per_block = BLOCK, int cap = 8192) {
 // context
 // ---------------------------------------------------------------------------
 constexpr int MAX_COLOURS = 8;  // + one trailing all-atomic class
+// colour lag of the one-launch plan's ticket order, in chains (about two
+// generations of resident workgroups at p = 8: 4 per CU x 256 CUs)
+#ifndef SEM_DF_LAG_DEFAULT
+#define SEM_DF_LAG_DEFAULT 2048
+#endif
 
 struct sem_ctx {
   int p = 0, n = 0, dpn = 1, device = 0;
@@ -216,6 +221,14 @@ struct sem_ctx {
   bool xg_valid = false;  // the Poisson action reads d_XG
   bool xg_axi = false;    // the axisymmetric Stokes action reads d_XG
   unsigned long long* d_bad = nullptr;
+  // one-launch plan of the Poisson column kernel (DFPlan, sem_kernels.h)
+  bool df = false;
+  int64_t df_lag = 0;
+  int64_t n_deps = 0;
+  int* d_dep_start = nullptr;
+  int* d_dep_idx = nullptr;
+  uint32_t* d_df_flags = nullptr;
+  uint32_t* d_df_state = nullptr;
 };
 
 namespace sem {
@@ -353,18 +366,41 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
       const MapRef mr{c->d_mapP, c->d_map16, c->d_mbase};
       const double* GP = nodal ? nullptr : c->d_GP[0];
       const double2* XG = nodal ? c->d_XG : nullptr;
+      const dim3 b(ChainWaves<N>::block);
+      if (c->df) {  // one launch for every chain (DFPlan)
+        static const int ticketed = [] {
+          const char* e = std::getenv("SEM_DF_TICKET");
+          return e ? std::atoi(e) : 1;
+        }();
+        const DFPlan df{c->d_dep_start, c->d_dep_idx, c->d_df_flags, c->d_df_state, ticketed};
+        hipLaunchKernelGGL(k_df_begin, dim3(1), dim3(WAVE), 0, st, c->d_df_state);
+        if (nodal && c->map16)
+          hipLaunchKernelGGL((k_poisson_apply<N, true, true, true>), dim3(grid), b, 0, st, mr, GP,
+                             XG, u, y, c0, c1, c->rounds, acc, D, w, df);
+        else if (nodal)
+          hipLaunchKernelGGL((k_poisson_apply<N, true, false, true>), dim3(grid), b, 0, st, mr,
+                             GP, XG, u, y, c0, c1, c->rounds, acc, D, w, df);
+        else if (c->map16)
+          hipLaunchKernelGGL((k_poisson_apply<N, false, true, true>), dim3(grid), b, 0, st, mr,
+                             GP, XG, u, y, c0, c1, c->rounds, acc, D, w, df);
+        else
+          hipLaunchKernelGGL((k_poisson_apply<N, false, false, true>), dim3(grid), b, 0, st, mr,
+                             GP, XG, u, y, c0, c1, c->rounds, acc, D, w, df);
+        continue;
+      }
+      const DFPlan nodf{};
       if (nodal && c->map16)
-        hipLaunchKernelGGL((k_poisson_apply<N, true, true>), dim3(grid), dim3(ChainWaves<N>::block), 0, st,
-                           mr, GP, XG, u, y, c0, c1, c->rounds, acc, D, w);
+        hipLaunchKernelGGL((k_poisson_apply<N, true, true>), dim3(grid), b, 0, st, mr, GP, XG, u,
+                           y, c0, c1, c->rounds, acc, D, w, nodf);
       else if (nodal)
-        hipLaunchKernelGGL((k_poisson_apply<N, true, false>), dim3(grid), dim3(ChainWaves<N>::block), 0,
-                           st, mr, GP, XG, u, y, c0, c1, c->rounds, acc, D, w);
+        hipLaunchKernelGGL((k_poisson_apply<N, true, false>), dim3(grid), b, 0, st, mr, GP, XG,
+                           u, y, c0, c1, c->rounds, acc, D, w, nodf);
       else if (c->map16)
-        hipLaunchKernelGGL((k_poisson_apply<N, false, true>), dim3(grid), dim3(ChainWaves<N>::block), 0,
-                           st, mr, GP, XG, u, y, c0, c1, c->rounds, acc, D, w);
+        hipLaunchKernelGGL((k_poisson_apply<N, false, true>), dim3(grid), b, 0, st, mr, GP, XG,
+                           u, y, c0, c1, c->rounds, acc, D, w, nodf);
       else
-        hipLaunchKernelGGL((k_poisson_apply<N, false, false>), dim3(grid), dim3(ChainWaves<N>::block), 0,
-                           st, mr, GP, XG, u, y, c0, c1, c->rounds, acc, D, w);
+        hipLaunchKernelGGL((k_poisson_apply<N, false, false>), dim3(grid), b, 0, st, mr, GP, XG,
+                           u, y, c0, c1, c->rounds, acc, D, w, nodf);
     }
     else if (op_kind == SEM_OP_AXISYM_STOKES && nodal) {
       const MapRef mr{c->d_mapP, c->d_map16, c->d_mbase};
@@ -496,13 +532,18 @@ struct Plan {
   int64_t n_atomic_groups = 0;
   int64_t n_slots = 0;
   bool conforming = true;
+  // one-launch plan (df_lag > 0): chains in ticket order, and per chain the
+  // earlier chains that last wrote one of its shared nodes
+  bool df = false;
+  std::vector<int> dep_start, dep_idx;
 };
 
 // node_state (may be empty): SEM_NODE_PRIOR = y already holds a value when
 // this operator runs (first touches become read-modify-write, never zeroed);
 // SEM_NODE_OTHER = another operator writes it (not zeroed when unreferenced).
 int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node, int n,
-               int rounds, const std::vector<uint8_t>& node_state, Plan& P) {
+               int rounds, const std::vector<uint8_t>& node_state, Plan& P,
+               int64_t df_lag = 0) {
   const int epw = WAVE / n, lw = epw * n, nn = n * n;
   const int64_t n_groups = (n_elem + epw - 1) / epw;
   const int CW = chain_waves_of(n);  // groups of a chain that run concurrently
@@ -569,13 +610,21 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
     }
   }
   std::vector<uint8_t>().swap(cmask);
-  // 3. launch order
-  std::vector<int64_t> count(MAX_COLOURS + 2, 0);
-  for (int64_t ch = 0; ch < n_chains; ++ch) count[colour[ch] + 1]++;
-  P.colour_start.assign(MAX_COLOURS + 2, 0);
-  for (int q = 0; q <= MAX_COLOURS; ++q) P.colour_start[q + 1] = P.colour_start[q] + count[q + 1];
+  // 3. launch order: colour-major (one launch per colour), or for the
+  // one-launch plan the ticket order chain + colour * lag
   std::vector<int64_t> order(n_chains);
-  {
+  P.df = df_lag > 0 && conforming && n_chains > 1;
+  if (P.df) {
+    for (int64_t ch = 0; ch < n_chains; ++ch) order[ch] = ch;
+    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+      return a + colour[a] * df_lag < b + colour[b] * df_lag;
+    });
+    P.colour_start = {0, n_chains};
+  } else {
+    std::vector<int64_t> count(MAX_COLOURS + 2, 0);
+    for (int64_t ch = 0; ch < n_chains; ++ch) count[colour[ch] + 1]++;
+    P.colour_start.assign(MAX_COLOURS + 2, 0);
+    for (int q = 0; q <= MAX_COLOURS; ++q) P.colour_start[q + 1] = P.colour_start[q] + count[q + 1];
     std::vector<int64_t> fill(P.colour_start.begin(), P.colour_start.end() - 1);
     for (int64_t ch = 0; ch < n_chains; ++ch) order[fill[colour[ch]]++] = ch;
   }
@@ -600,6 +649,12 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
   std::vector<int> lastt(n_node, -1);      // (group in chain) * n * lw + pos of the last touch
   std::vector<uint8_t> act((size_t)CH * n * lw);  // per entry: 0 normal, 1 merge-skip, 2 carry-skip, 3 carry-in
   P.n_atomic_groups = 0;
+  std::vector<int> lastq;  // one-launch plan: ticket of the last chain writing each node
+  std::vector<int> deps;
+  if (P.df) {
+    lastq.assign(n_node, -1);
+    P.dep_start.assign(n_chains + 1, 0);
+  }
   for (int64_t q = 0; q < n_chains; ++q) {
     const int64_t ch = order[q];
     bool atomic_chain = colour[ch] >= MAX_COLOURS;
@@ -669,7 +724,18 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
             if (a == 3) code |= W_CARRY;
           }
           out[pos] = gid | (code << CODE_SHIFT);
+          if (P.df && shared_local(r, jj)) {
+            if (lastq[gid] >= 0 && lastq[gid] != q) deps.push_back(lastq[gid]);
+            lastq[gid] = (int)q;
+          }
         }
+    }
+    if (P.df) {
+      std::sort(deps.begin(), deps.end());
+      deps.erase(std::unique(deps.begin(), deps.end()), deps.end());
+      P.dep_idx.insert(P.dep_idx.end(), deps.begin(), deps.end());
+      P.dep_start[q + 1] = (int)P.dep_idx.size();
+      deps.clear();
     }
   }
   for (int64_t i = 0; i < n_node; ++i)
@@ -1092,6 +1158,10 @@ void sem_ctx_destroy(sem_ctx* c) {
   (void)hipFree(c->d_XG);
   (void)hipFree(c->d_owner);
   (void)hipFree(c->d_bad);
+  (void)hipFree(c->d_dep_start);
+  (void)hipFree(c->d_dep_idx);
+  (void)hipFree(c->d_df_flags);
+  (void)hipFree(c->d_df_state);
   delete c;
 }
 
@@ -1137,8 +1207,18 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
   int rounds = 1;
   if (const char* s = std::getenv("SEM_CHAIN_ROUNDS")) rounds = std::max(1, std::atoi(s));
   const bool mfma = want_mfma(c);
+  // one-launch plan for the Poisson column kernel (SEM_DF=0: one launch per
+  // colour); SEM_DF_LAG = colour lag of the ticket order, in chains
+  int64_t df_lag = 0;
+  if (!mfma && c->dpn == 1) {
+    const char* e = std::getenv("SEM_DF");
+    if (!e || std::atoi(e) != 0) {
+      const char* l = std::getenv("SEM_DF_LAG");
+      df_lag = l ? std::max<int64_t>(1, std::atoll(l)) : SEM_DF_LAG_DEFAULT;
+    }
+  }
   int rc = mfma ? build_plan_elem(h, c->n_elem, c->n_node, n, state, P)
-                : build_plan(h, c->n_elem, c->n_node, n, rounds, state, P);
+                : build_plan(h, c->n_elem, c->n_node, n, rounds, state, P, df_lag);
   if (rc) return rc;
   // element-coloured fallback for orders that defeat the chain patterns
   // (SEM_PLAN=1 forces it, SEM_PLAN=0 forbids it)
@@ -1205,6 +1285,33 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
                       hipMemcpyHostToDevice));
   }
   c->colour_start = P.colour_start;
+  c->df = P.df;
+  c->df_lag = P.df ? df_lag : 0;
+  c->n_deps = (int64_t)P.dep_idx.size();
+  (void)hipFree(c->d_dep_start);
+  (void)hipFree(c->d_dep_idx);
+  (void)hipFree(c->d_df_flags);
+  c->d_dep_start = nullptr;
+  c->d_dep_idx = nullptr;
+  c->d_df_flags = nullptr;
+  if (P.df) {
+    const int64_t nch = (int64_t)P.dep_start.size() - 1;
+    HIP_TRY(hipMalloc(&c->d_dep_start, P.dep_start.size() * sizeof(int)));
+    HIP_TRY(hipMemcpy(c->d_dep_start, P.dep_start.data(), P.dep_start.size() * sizeof(int),
+                      hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&c->d_dep_idx, std::max<size_t>(1, P.dep_idx.size()) * sizeof(int)));
+    if (!P.dep_idx.empty())
+      HIP_TRY(hipMemcpy(c->d_dep_idx, P.dep_idx.data(), P.dep_idx.size() * sizeof(int),
+                        hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&c->d_df_flags, nch * sizeof(uint32_t)));
+    HIP_TRY(hipMemset(c->d_df_flags, 0, nch * sizeof(uint32_t)));
+    if (!c->d_df_state) {
+      HIP_TRY(hipMalloc(&c->d_df_state, 128 * sizeof(uint32_t)));
+      HIP_TRY(hipMemset(c->d_df_state, 0, 128 * sizeof(uint32_t)));
+    }
+    // flags hold the epoch of their last action: restart both from 0
+    HIP_TRY(hipMemset(c->d_df_state, 0, 128 * sizeof(uint32_t)));
+  }
   c->n_atomic_groups = P.n_atomic_groups;
   c->conforming = P.conforming;
   (void)hipFree(c->d_owner);
@@ -1228,23 +1335,35 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
 int sem_plan_info(sem_ctx* c, int64_t* info, int n_info) {
   if (!c || !info || n_info < 1) return fail(SEM_E_INVALID, "bad arguments");
   const int64_t nc = c->colour_start.empty() ? 0 : (int64_t)c->colour_start.size() - 1;
-  constexpr int NV = 8 + MAX_COLOURS + 1 + 1 + 1 + 1 + 1 + 1;
+  constexpr int NV = 8 + MAX_COLOURS + 1 + 1 + 1 + 1 + 1 + 1 + 3;
   int64_t vals[NV] = {c->n_groups, c->n_zero, c->n_atomic_groups, c->conforming ? 1 : 0,
                       c->epw,      nc,        c->rounds,          c->n_slots};
   for (int64_t q = 0; q < nc && q <= MAX_COLOURS; ++q)
     vals[8 + q] = c->colour_start[q + 1] - c->colour_start[q];
-  vals[NV - 5] = c->mfma ? SEM_KERNEL_MFMA : SEM_KERNEL_COLUMN;
-  vals[NV - 4] = c->map16 ? 2 : 4;  // bytes per packed map entry
+  vals[NV - 8] = c->mfma ? SEM_KERNEL_MFMA : SEM_KERNEL_COLUMN;
+  vals[NV - 7] = c->map16 ? 2 : 4;  // bytes per packed map entry
   // the geometry the Poisson action actually uses: nodal only once x_phys
   // per node exists (sem_set_geom installs stored factors); before any
   // geometry, the mode sem_geom_from_nodes will resolve to
   const bool eff_nodal = c->xg_valid ? true : (c->d_GP[0] ? false : nodal_mode(c));
-  vals[NV - 3] = eff_nodal ? SEM_GEOM_NODAL : SEM_GEOM_STORED;
-  vals[NV - 2] = c->mfma ? 2 : (c->ecol ? 1 : 0);  // plan: chains, element-coloured, element
+  vals[NV - 6] = eff_nodal ? SEM_GEOM_NODAL : SEM_GEOM_STORED;
+  // plan: chains, element-coloured, element, chains in one launch
+  vals[NV - 5] = c->mfma ? 2 : (c->ecol ? 1 : (c->df ? 3 : 0));
   // the same for the axisymmetric Stokes block (dofs_per_node = 2)
   const bool axi_nodal =
       c->xg_axi ? true : (c->d_GP[1] ? false : nodal_mode_op(c, SEM_OP_AXISYM_STOKES));
-  vals[NV - 1] = c->dpn == 2 ? (axi_nodal ? SEM_GEOM_NODAL : SEM_GEOM_STORED) : 0;
+  vals[NV - 4] = c->dpn == 2 ? (axi_nodal ? SEM_GEOM_NODAL : SEM_GEOM_STORED) : 0;
+  // one-launch plan: dependency edges, colour lag, waits that timed out so
+  // far (read from the device: synchronises with the device)
+  vals[NV - 3] = c->n_deps;
+  vals[NV - 2] = c->df_lag;
+  vals[NV - 1] = 0;
+  if (c->df && n_info >= NV) {
+    DeviceGuard g(c->device);
+    uint32_t err = 0;
+    HIP_TRY(hipMemcpy(&err, c->d_df_state + DF_ERR, sizeof(err), hipMemcpyDeviceToHost));
+    vals[NV - 1] = err;
+  }
   for (int i = 0; i < n_info && i < NV; ++i) info[i] = vals[i];
   return SEM_OK;
 }

@@ -35,6 +35,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 namespace semk {
 
@@ -273,37 +274,146 @@ __device__ __forceinline__ void emit1(double* __restrict__ y, uint32_t raw, doub
 // stores.  Safe because a RMW target's earlier writers are an earlier launch
 // (colour), an earlier round of this chain (ended by a workgroup barrier) or
 // an earlier operator in stream order -- never a concurrent wave.
-template <int N>
+// buffer-instruction cache policies (gfx950): nt = 2, sc1 = 16
+constexpr int CPOL_NT = 2;
+constexpr int CPOL_SC1 = 16;
+
+// y as a buffer resource: node ids are < 2^28, so byte offsets stay below
+// the 2^31-byte range, and an offset of 2^31 reads 0 with no memory traffic
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t y_rsrc(const double* y) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(y), 0, 0x80000000, 0x00020000);
+}
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+// one-launch plan (DFPlan below): every y access that another workgroup may
+// follow is agent-coherent -- sc1 stores (written through, line dropped
+// from the XCD's L2) and sc1 loads (MI355X_MICROARCH.md, inter-workgroup
+// visibility, hand-off table row 1)
+__device__ __forceinline__ double y_load_sc1(const double* y, uint32_t gid) {
+  return __builtin_bit_cast(double,
+                            __builtin_amdgcn_raw_buffer_load_b64(y_rsrc(y), gid * 8u, 0, CPOL_SC1));
+}
+__device__ __forceinline__ void y_store_sc1(double* y, uint32_t gid, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), y_rsrc(y), gid * 8u, 0,
+                                        CPOL_SC1);
+}
+
+template <int N, int AUX = CPOL_NT>
 __device__ __forceinline__ void rmw_prefetch(const double* __restrict__ y,
                                              const uint32_t (&raw)[N], int accumulate,
                                              double (&prev)[N]) {
   // predicated without branches: a lane that needs no operand reads past the
-  // end of the buffer range (returns 0, no memory traffic).  Node ids are
-  // < 2^28, so byte offsets stay below the 2^31-byte range.
-  const __amdgpu_buffer_rsrc_t ry =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(y), 0, 0x80000000, 0x00020000);
+  // end of the buffer range (returns 0, no memory traffic)
+  const __amdgpu_buffer_rsrc_t ry = y_rsrc(y);
 #pragma unroll
   for (int p = 0; p < N; ++p) {
     const uint32_t a = (raw[p] >> CODE_SHIFT) & 3u;
     const bool need = a == W_RMW || (a == W_STORE && accumulate);
     const uint32_t off = need ? (raw[p] & GID_MASK) * 8u : 0x80000000u;
-    prev[p] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(ry, off, 0, 2 /*nt*/));
+    prev[p] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(ry, off, 0, AUX));
   }
 }
 
+template <bool DF = false>
 __device__ __forceinline__ void emit1p(double* __restrict__ y, uint32_t raw, double v, double prev) {
   const uint32_t a = (raw >> CODE_SHIFT) & 3u;
   double* dst = y + (raw & GID_MASK);
   if (a == W_STORE || a == W_RMW) {  // prev = 0 for a first writer in overwrite mode
+    if constexpr (DF)
+      y_store_sc1(y, raw & GID_MASK, prev + v);
+    else
 #if SEM_NT_STORE
-    __builtin_nontemporal_store(prev + v, dst);
+      __builtin_nontemporal_store(prev + v, dst);
 #else
-    *dst = prev + v;
+      *dst = prev + v;
 #endif
   } else if (a == W_ATOMIC) {
     atomic_add_f64(dst, v);
   }
 }
+
+// emit1 of the one-launch plan (no prefetch): sc1 operand loads and stores
+__device__ __forceinline__ void emit1_df(double* __restrict__ y, uint32_t raw, double v,
+                                         int accumulate) {
+  const uint32_t a = (raw >> CODE_SHIFT) & 3u;
+  const uint32_t gid = raw & GID_MASK;
+  if (a == W_STORE)
+    y_store_sc1(y, gid, accumulate ? y_load_sc1(y, gid) + v : v);
+  else if (a == W_RMW)
+    y_store_sc1(y, gid, y_load_sc1(y, gid) + v);
+  else if (a == W_ATOMIC)
+    atomic_add_f64(y + gid, v);
+}
+
+// ---------------------------------------------------------------------------
+// One-launch ("dataflow") plan of the Poisson column kernel.
+// All chains run in ONE launch instead of one launch per colour.  A
+// workgroup takes the next chain from a ticket counter (so a chain is only
+// ever waited on by chains with later tickets: the grid cannot deadlock
+// whatever the dispatch order), and before it starts it waits until every
+// chain that wrote one of its shared nodes earlier in ticket order has
+// published: per-chain flag = the action's epoch, written
+// by one lane after every wave's stores drained and a workgroup barrier.
+// The write codes are those of the ticket order, so each node still has
+// exactly one writer at a time and its writers run in a fixed order
+// (bitwise-deterministic results).  The ticket order interleaves colours
+// with a lag: chain key = chain index + colour * lag, so a chain's
+// lower-coloured neighbours were taken about `lag` tickets earlier
+// (finished, and their shared u / x_phys lines recently read).
+// state[0] = ticket counter, state[DF_EPOCH] = epoch (both advanced by
+// k_df_begin before every launch), state[DF_ERR] = waits that timed out.
+// ---------------------------------------------------------------------------
+constexpr int DF_EPOCH = 32;  // separate 128-B lines
+constexpr int DF_ERR = 64;
+#ifndef SEM_DF_SPIN_LIMIT
+#define SEM_DF_SPIN_LIMIT (1 << 22)
+#endif
+struct DFPlan {
+  const int* __restrict__ dep_start;  // [chain + 1]
+  const int* __restrict__ dep_idx;    // earlier-ticket chains this chain follows
+  uint32_t* flags;                    // [chain] = epoch once the chain's y writes are out
+  uint32_t* state;
+  int ticketed;                       // 0: chain = blockIdx (timing experiments only)
+};
+typedef __attribute__((address_space(1))) uint32_t g_u32;
+
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
+  return __hip_atomic_load((g_u32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// wave-level wait (each wave polls for itself, then issues its own sc1
+// loads of the handed-off y entries)
+__device__ __forceinline__ void df_wait(const DFPlan& df, int64_t chain, uint32_t epoch) {
+  const int d0 = df.dep_start[chain], d1 = df.dep_start[chain + 1];
+  const int lane = threadIdx.x % WAVE;
+  for (int b = d0; b < d1; b += WAVE) {
+    const int i = b + lane;
+    const bool mine = i < d1;
+    const uint32_t* f = df.flags + (mine ? df.dep_idx[i] : 0);
+    for (int s = 0;; ++s) {
+      const bool ok = !mine || ld_agent(f) == epoch;
+      if (__all(ok)) break;
+      if (s >= SEM_DF_SPIN_LIMIT) {  // never expected: count it, do not hang
+        if (lane == 0)
+          __hip_atomic_fetch_add(df.state + DF_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(4);
+    }
+  }
+}
+
+struct NoWait {
+  static constexpr int aux = CPOL_NT;
+  __device__ void operator()() const {}
+};
+// the one-launch plan waits in the kernel's prologue, with nothing live
+// (waiting just before the read-modify-writes instead kept the plan's
+// pointers live through the contractions: 30 VGPRs spilled at p = 8); its
+// read-modify-write operands are read sc1
+struct DFWait {
+  static constexpr int aux = CPOL_SC1;
+  __device__ void operator()() const {}
+};
 
 __device__ __forceinline__ void emit2(double* __restrict__ y, uint32_t raw, double v0, double v1,
                                       int accumulate) {
@@ -460,14 +570,15 @@ __device__ __forceinline__ void load_map(const MapRef& m, int64_t g, int lane, b
 // (p = 0..N-1) of the lane's column j in v[], and the raw coded map entries.
 //   mapP[g][r][k*N + j] = map[e][r][j] | code,  GP[g][c][r][k*N + j] = G_c(e; r, j)
 // ---------------------------------------------------------------------------
-template <int N, bool M16>
+template <int N, bool M16, class Pre = NoWait>
 __device__ __forceinline__ void poisson_group_stored(const MapRef& mref,
                                                      const double* __restrict__ GP,
                                                      const double* __restrict__ u, int64_t g,
                                                      int lane, int j, bool in_wave, double* L,
                                                      const DEO<N>& D, uint32_t (&raw)[N],
                                                      double (&v)[N], const double* __restrict__ y,
-                                                     int accumulate, double (&prev)[N]) {
+                                                     int accumulate, double (&prev)[N],
+                                                     const Pre& pre = Pre()) {
   using T = Tile<N, SEM_TILE_PAD_STORED>;
   constexpr int LW = T::LW;
   constexpr int RS = T::RS;
@@ -506,9 +617,10 @@ __device__ __forceinline__ void poisson_group_stored(const MapRef& mref,
       w0[m] = fma(g00, d0[m], g01 * d1);
       L[m * RS + j] = fma(g01, d0[m], g11 * d1);  // w1, same lane's slot
     }
-    if constexpr (RmwPrefetch<N>::value == 1) rmw_prefetch<N>(y, raw, accumulate, prev);
+    if constexpr (RmwPrefetch<N>::value) pre();
+    if constexpr (RmwPrefetch<N>::value == 1) rmw_prefetch<N, Pre::aux>(y, raw, accumulate, prev);
     deo_apply_t<N>(D, w0, v);
-    if constexpr (RmwPrefetch<N>::value == 2) rmw_prefetch<N>(y, raw, accumulate, prev);
+    if constexpr (RmwPrefetch<N>::value == 2) rmw_prefetch<N, Pre::aux>(y, raw, accumulate, prev);
   }
   wave_sync();
   // row i = j: yb[i][q] = sum_n D[n][q] w1[i][n]
@@ -628,13 +740,13 @@ __device__ __forceinline__ void nodal_geometry(const double2 (&xc)[N], int j, do
 }
 
 // the Laplacian of the group on tile A with G00/G01 in registers, G11 in B
-template <int N>
+template <int N, class Pre = NoWait>
 __device__ __forceinline__ void nodal_laplacian(const double (&uc)[N], int j, double* A,
                                                 const double* B, const DEO<N>& D,
                                                 const double (&g00)[N], const double (&g01)[N],
                                                 double (&v)[N], const double* __restrict__ y,
                                                 const uint32_t (&raw)[N], int accumulate,
-                                                double (&prev)[N]) {
+                                                double (&prev)[N], const Pre& pre = Pre()) {
   constexpr int RS = Tile<N, SEM_TILE_PAD_NODAL>::RS;
   double d0[N];
   deo_apply<N>(D, uc, d0);
@@ -650,9 +762,10 @@ __device__ __forceinline__ void nodal_laplacian(const double (&uc)[N], int j, do
       w0[m] = fma(g00[m], d0[m], g01[m] * d1);
       A[m * RS + j] = fma(g01[m], d0[m], B[m * RS + j] * d1);
     }
-    if constexpr (RmwPrefetch<N>::value == 1) rmw_prefetch<N>(y, raw, accumulate, prev);
+    if constexpr (RmwPrefetch<N>::value) pre();
+    if constexpr (RmwPrefetch<N>::value == 1) rmw_prefetch<N, Pre::aux>(y, raw, accumulate, prev);
     deo_apply_t<N>(D, w0, v);
-    if constexpr (RmwPrefetch<N>::value == 2) rmw_prefetch<N>(y, raw, accumulate, prev);
+    if constexpr (RmwPrefetch<N>::value == 2) rmw_prefetch<N, Pre::aux>(y, raw, accumulate, prev);
   }
   wave_sync();
   row_pass<N, RS, true, false>(A, j, D);
@@ -662,7 +775,7 @@ __device__ __forceinline__ void nodal_laplacian(const double (&uc)[N], int j, do
 }
 
 // One group of the Poisson action with NODAL geometry (no prefetch).
-template <int N, bool M16>
+template <int N, bool M16, class Pre = NoWait>
 __device__ __forceinline__ void poisson_group_nodal(const MapRef& mref,
                                                     const double2* __restrict__ XG,
                                                     const double* __restrict__ u, int64_t g,
@@ -671,7 +784,7 @@ __device__ __forceinline__ void poisson_group_nodal(const MapRef& mref,
                                                     const WVec<N>& w, double wj,
                                                     uint32_t (&raw)[N], double (&v)[N],
                                                     const double* __restrict__ y, int accumulate,
-                                                    double (&prev)[N]) {
+                                                    double (&prev)[N], const Pre& pre = Pre()) {
   double uc[N];
   double2 xc[N];
   load_map<N, M16>(mref, g, lane, in_wave, raw);
@@ -684,14 +797,14 @@ __device__ __forceinline__ void poisson_group_nodal(const MapRef& mref,
 #if !SEM_NODAL_EARLY_U
   gather_u<N>(u, raw, uc);
 #endif
-  nodal_laplacian<N>(uc, j, A, B, D, g00, g01, v, y, raw, accumulate, prev);
+  nodal_laplacian<N>(uc, j, A, B, D, g00, g01, v, y, raw, accumulate, prev, pre);
 }
 
 
 // Scatter of one group's column values through the coded map, with the
 // in-group merge (next lane) and the chain carry (previous group) applied.
 // ncomp values per node (1: Poisson, 2: axisymmetric block).
-template <int N, int NC, bool PRE = false, int CW = ChainWaves<N>::value>
+template <int N, int NC, bool PRE = false, int CW = ChainWaves<N>::value, bool DF = false>
 __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_t (&raw)[N],
                                            double (&v)[NC][N], int lane, int wave, int rd,
                                            bool in_wave, double (*carry)[CW][NC][N],
@@ -728,7 +841,9 @@ __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_
 #pragma unroll
     for (int p = 0; p < N; ++p) {
       if constexpr (PRE)
-        emit1p(y, raw[p], v[0][p], prev[p]);
+        emit1p<DF>(y, raw[p], v[0][p], prev[p]);
+      else if (DF && NC == 1)
+        emit1_df(y, raw[p], v[0][p], accumulate);
       else if (NC == 1)
         emit1(y, raw[p], v[0][p], accumulate);
       else
@@ -772,18 +887,35 @@ struct PoissonMinWaves {
                                                         : 1;
 };
 
-template <int N, bool NODAL, bool M16>
+template <int N, bool NODAL, bool M16, bool DF = false>
 __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODAL>::value))
     k_poisson_apply(const MapRef mref, const double* __restrict__ GP,
                     const double2* __restrict__ XG, const double* __restrict__ u,
                     double* __restrict__ y, int64_t c0, int64_t c1, int rounds, int accumulate,
-                    const DEO<N> D, const WVec<N> w) {
+                    const DEO<N> D, const WVec<N> w, const DFPlan df) {
   using T = Tile<N, NODAL ? SEM_TILE_PAD_NODAL : SEM_TILE_PAD_STORED>;
   constexpr int NT = NODAL ? 2 : 1;  // tiles per element slot
   __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * T::ES * NT];
   constexpr int CW = ChainWaves<N>::value;
   __shared__ double carry[2][CW][1][N];
-  const int64_t chain = c0 + xcd_block(blockIdx.x, gridDim.x);
+  __shared__ int s_ticket_df;
+  __shared__ uint32_t s_epoch_df;
+  int64_t chain;
+  uint32_t epoch = 0;
+  if constexpr (DF) {
+    if (threadIdx.x == 0) {
+      s_ticket_df = df.ticketed ? (int)__hip_atomic_fetch_add(df.state, 1u, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT)
+                             : (int)blockIdx.x;
+      s_epoch_df = ld_agent(df.state + DF_EPOCH);
+    }
+    __syncthreads();
+    chain = c0 + s_ticket_df;
+    epoch = s_epoch_df;
+    if (chain < c1) df_wait(df, chain, epoch);
+  } else {
+    chain = c0 + xcd_block(blockIdx.x, gridDim.x);
+  }
   if (chain >= c1) return;  // uniform over the workgroup
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);  // provably uniform
   const int lane = threadIdx.x % WAVE;
@@ -800,18 +932,41 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
     const int64_t g = (chain * rounds + rd) * CW + wave;
     uint32_t raw[N];
     double v[1][N], prev[N];
+    using Pre = typename std::conditional<DF, DFWait, NoWait>::type;
+    const Pre pre{};
     if constexpr (NODAL)
       poisson_group_nodal<N, M16>(mref, XG, u, g, lane, j, in_wave, L, LB, D, w, wj, raw, v[0],
-                                  y, accumulate, prev);
+                                  y, accumulate, prev, pre);
     else
       poisson_group_stored<N, M16>(mref, GP, u, g, lane, j, in_wave, L, D, raw, v[0], y,
-                                   accumulate, prev);
+                                   accumulate, prev, pre);
 #ifdef SEM_DIAG_NO_STORE
     if (in_wave && v[0][0] == 1234.5678) y[0] = v[0][1];  // timing-only
 #else
-    chain_emit<N, 1, (RmwPrefetch<N>::value > 0)>(y, raw, v, lane, wave, rd, in_wave, carry,
-                                                  accumulate, prev);
+    chain_emit<N, 1, (RmwPrefetch<N>::value > 0), CW, DF>(y, raw, v, lane, wave, rd, in_wave,
+                                                          carry, accumulate, prev);
 #endif
+  }
+  if constexpr (DF) {
+    // publish: every wave's y writes have left the CU, then one lane flags
+    // the chain (hand-off table row 1: sc1 stores, vmcnt(0) in every storing
+    // wave, workgroup barrier, one sc1 flag store)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {  // chain and epoch re-read from LDS: nothing kept live
+      volatile int* st = &s_ticket_df;
+      volatile uint32_t* se = &s_epoch_df;
+      __hip_atomic_store((g_u32*)(df.flags + c0 + *st), *se, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// before every one-launch action: ticket counter to 0, next epoch
+__global__ void k_df_begin(uint32_t* state) {
+  if (threadIdx.x == 0) {
+    __hip_atomic_exchange(state, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(state + DF_EPOCH, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 

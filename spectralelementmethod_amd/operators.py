@@ -189,8 +189,8 @@ class SEMOperator(object):
 
     def plan_info(self):
         """Setup plan of the scatter (see include/sem_hip.h sem_plan_info)."""
-        info = (C.c_int64 * 22)()
-        _lib.check(self._lib.sem_plan_info(self._ctx, info, 22))
+        info = (C.c_int64 * 25)()
+        _lib.check(self._lib.sem_plan_info(self._ctx, info, 25))
         v = list(info)
         counts = [x for x in v[8:8 + v[5]]]
         while counts and counts[-1] == 0:
@@ -201,9 +201,10 @@ class SEMOperator(object):
                     kernel="mfma" if v[17] == _lib.KERNEL_MFMA else "column",
                     map_entry_bytes=v[18],
                     geometry="nodal" if v[19] == _lib.GEOM_NODAL else "stored",
-                    plan=("chains", "element-coloured", "element")[v[20]],
+                    plan=("chains", "element-coloured", "element", "chains-one-launch")[v[20]],
                     geometry_axisym=(None if self.dpn != 2 else
-                                     "nodal" if v[21] == _lib.GEOM_NODAL else "stored"))
+                                     "nodal" if v[21] == _lib.GEOM_NODAL else "stored"),
+                    dependencies=v[22], lag=v[23], wait_timeouts=v[24])
 
     # ------------------------------------------------------------------
     def compute_geometry(self, kind=POISSON, stream=None):

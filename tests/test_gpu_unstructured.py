@@ -97,6 +97,7 @@ def test_forced_plan_structured(gpu, gll, monkeypatch, plan_env):
         u = np.random.default_rng(1).standard_normal(nodes.shape[1])
         ref = sem_oracle.PoissonProblem(nodes, e2n, gll["half_4"]).apply(u)
         op = SEMOperator(4, e2n, nodes, device=gpu)
-        assert op.plan_info()["plan"] == ("element-coloured" if plan_env == "1" else "chains")
+        plan = op.plan_info()["plan"]
+        assert plan == "element-coloured" if plan_env == "1" else plan.startswith("chains")
         y = op.apply(torch.from_numpy(u).to(gpu)).cpu().numpy()
         assert rel_l2(y, ref) < TOL
