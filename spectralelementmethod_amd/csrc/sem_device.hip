@@ -339,6 +339,52 @@ bool use_nodal(const sem_ctx* c, int op_kind) {
   return false;
 }
 
+// one chain-kernel launch, one-launch plan (DF) or a colour class
+template <int N, bool DF>
+void launch_chains(sem_ctx* c, int op_kind, bool nodal, const double* u, double* y, int acc,
+                   bool lin, int64_t c0, int64_t c1, const DEO<N>& D, const WVec<N>& w,
+                   const DFPlan& df, hipStream_t st) {
+  const dim3 g((unsigned)(c1 - c0)), b(ChainWaves<N>::block);
+  const MapRef mr{c->d_mapP, c->d_map16, c->d_mbase};
+  const int R = c->rounds;
+  if (op_kind == SEM_OP_POISSON) {
+    const double* GP = nodal ? nullptr : c->d_GP[0];
+    const double2* XG = nodal ? c->d_XG : nullptr;
+    if (nodal && c->map16)
+      hipLaunchKernelGGL((k_poisson_apply<N, true, true, DF>), g, b, 0, st, mr, GP, XG, u, y, c0,
+                         c1, R, acc, D, w, df);
+    else if (nodal)
+      hipLaunchKernelGGL((k_poisson_apply<N, true, false, DF>), g, b, 0, st, mr, GP, XG, u, y, c0,
+                         c1, R, acc, D, w, df);
+    else if (c->map16)
+      hipLaunchKernelGGL((k_poisson_apply<N, false, true, DF>), g, b, 0, st, mr, GP, XG, u, y, c0,
+                         c1, R, acc, D, w, df);
+    else
+      hipLaunchKernelGGL((k_poisson_apply<N, false, false, DF>), g, b, 0, st, mr, GP, XG, u, y,
+                         c0, c1, R, acc, D, w, df);
+  } else if (op_kind == SEM_OP_AXISYM_STOKES && nodal) {
+    if (c->map16)
+      hipLaunchKernelGGL((k_axisym_nodal<N, true, DF>), g, b, 0, st, mr, c->d_XG, u, y, c0, c1, R,
+                         acc, D, w, df);
+    else
+      hipLaunchKernelGGL((k_axisym_nodal<N, false, DF>), g, b, 0, st, mr, c->d_XG, u, y, c0, c1,
+                         R, acc, D, w, df);
+  } else if (op_kind == SEM_OP_AXISYM_STOKES) {
+    hipLaunchKernelGGL((k_axisym_apply<N, 0, DF>), g, b, 0, st, c->d_mapP, c->d_GP[1], u, y, c0,
+                       c1, R, acc, D, w, AxiNS(), df);
+  } else {
+    AxiNS ns;
+    ns.re = c->reynolds;
+    ns.lin = (op_kind == SEM_OP_AXISYM_NS_JVP || lin) ? c->d_lin : nullptr;
+    if (op_kind == SEM_OP_AXISYM_NS)
+      hipLaunchKernelGGL((k_axisym_apply<N, 1, DF>), g, b, 0, st, c->d_mapP, c->d_GP[2], u, y, c0,
+                         c1, R, acc, D, w, ns, df);
+    else
+      hipLaunchKernelGGL((k_axisym_apply<N, 2, DF>), g, b, 0, st, c->d_mapP, c->d_GP[2], u, y, c0,
+                         c1, R, acc, D, w, ns, df);
+  }
+}
+
 template <int N>
 int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc, bool lin,
                    hipStream_t st) {
@@ -346,15 +392,25 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
   WVec<N> w;
   std::memcpy(w.v, c->hw, sizeof(w.v));
   const bool nodal = use_nodal(c, op_kind);
+  if (c->df) {  // every chain in one launch (DFPlan, sem_kernels.h)
+    static const int ticketed = [] {
+      const char* e = std::getenv("SEM_DF_TICKET");
+      return e ? std::atoi(e) : 1;
+    }();
+    const DFPlan df{c->d_dep_start, c->d_dep_idx, c->d_df_flags, c->d_df_state, ticketed};
+    hipLaunchKernelGGL(k_df_begin, dim3(1), dim3(WAVE), 0, st, c->d_df_state);
+    launch_chains<N, true>(c, op_kind, nodal, u, y, acc, lin, c->colour_start.front(),
+                           c->colour_start.back(), D, w, df, st);
+    return SEM_OK;
+  }
   const size_t nc = c->colour_start.size() - 1;
   for (size_t k = 0; k < nc; ++k) {
     const int64_t c0 = c->colour_start[k], c1 = c->colour_start[k + 1];
     if (c1 <= c0) continue;
-    const int grid = (int)(c1 - c0);
     if (op_kind == SEM_OP_POISSON && c->mfma) {
       if constexpr (N <= 16) {
         constexpr int per_block = MFMA_EPB * (16 / N) * (16 / N);
-        const dim3 g((grid + per_block - 1) / per_block);
+        const dim3 g((unsigned)((c1 - c0 + per_block - 1) / per_block));
         if (nodal)
           hipLaunchKernelGGL((k_poisson_mfma<N, true>), g, dim3(BLOCK), 0, st, c->d_mapP, nullptr,
                              c->d_XG, u, y, c->d_D, w, c0, c1, acc);
@@ -362,67 +418,8 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
           hipLaunchKernelGGL((k_poisson_mfma<N, false>), g, dim3(BLOCK), 0, st, c->d_mapP,
                              c->d_GP[0], nullptr, u, y, c->d_D, w, c0, c1, acc);
       }
-    } else if (op_kind == SEM_OP_POISSON) {
-      const MapRef mr{c->d_mapP, c->d_map16, c->d_mbase};
-      const double* GP = nodal ? nullptr : c->d_GP[0];
-      const double2* XG = nodal ? c->d_XG : nullptr;
-      const dim3 b(ChainWaves<N>::block);
-      if (c->df) {  // one launch for every chain (DFPlan)
-        static const int ticketed = [] {
-          const char* e = std::getenv("SEM_DF_TICKET");
-          return e ? std::atoi(e) : 1;
-        }();
-        const DFPlan df{c->d_dep_start, c->d_dep_idx, c->d_df_flags, c->d_df_state, ticketed};
-        hipLaunchKernelGGL(k_df_begin, dim3(1), dim3(WAVE), 0, st, c->d_df_state);
-        if (nodal && c->map16)
-          hipLaunchKernelGGL((k_poisson_apply<N, true, true, true>), dim3(grid), b, 0, st, mr, GP,
-                             XG, u, y, c0, c1, c->rounds, acc, D, w, df);
-        else if (nodal)
-          hipLaunchKernelGGL((k_poisson_apply<N, true, false, true>), dim3(grid), b, 0, st, mr,
-                             GP, XG, u, y, c0, c1, c->rounds, acc, D, w, df);
-        else if (c->map16)
-          hipLaunchKernelGGL((k_poisson_apply<N, false, true, true>), dim3(grid), b, 0, st, mr,
-                             GP, XG, u, y, c0, c1, c->rounds, acc, D, w, df);
-        else
-          hipLaunchKernelGGL((k_poisson_apply<N, false, false, true>), dim3(grid), b, 0, st, mr,
-                             GP, XG, u, y, c0, c1, c->rounds, acc, D, w, df);
-        continue;
-      }
-      const DFPlan nodf{};
-      if (nodal && c->map16)
-        hipLaunchKernelGGL((k_poisson_apply<N, true, true>), dim3(grid), b, 0, st, mr, GP, XG, u,
-                           y, c0, c1, c->rounds, acc, D, w, nodf);
-      else if (nodal)
-        hipLaunchKernelGGL((k_poisson_apply<N, true, false>), dim3(grid), b, 0, st, mr, GP, XG,
-                           u, y, c0, c1, c->rounds, acc, D, w, nodf);
-      else if (c->map16)
-        hipLaunchKernelGGL((k_poisson_apply<N, false, true>), dim3(grid), b, 0, st, mr, GP, XG,
-                           u, y, c0, c1, c->rounds, acc, D, w, nodf);
-      else
-        hipLaunchKernelGGL((k_poisson_apply<N, false, false>), dim3(grid), b, 0, st, mr, GP, XG,
-                           u, y, c0, c1, c->rounds, acc, D, w, nodf);
-    }
-    else if (op_kind == SEM_OP_AXISYM_STOKES && nodal) {
-      const MapRef mr{c->d_mapP, c->d_map16, c->d_mbase};
-      if (c->map16)
-        hipLaunchKernelGGL((k_axisym_nodal<N, true>), dim3(grid), dim3(ChainWaves<N>::block), 0,
-                           st, mr, c->d_XG, u, y, c0, c1, c->rounds, acc, D, w);
-      else
-        hipLaunchKernelGGL((k_axisym_nodal<N, false>), dim3(grid), dim3(ChainWaves<N>::block), 0,
-                           st, mr, c->d_XG, u, y, c0, c1, c->rounds, acc, D, w);
-    } else if (op_kind == SEM_OP_AXISYM_STOKES)
-      hipLaunchKernelGGL((k_axisym_apply<N, 0>), dim3(grid), dim3(ChainWaves<N>::block), 0, st, c->d_mapP,
-                         c->d_GP[1], u, y, c0, c1, c->rounds, acc, D, w, AxiNS());
-    else {
-      AxiNS ns;
-      ns.re = c->reynolds;
-      ns.lin = (op_kind == SEM_OP_AXISYM_NS_JVP || lin) ? c->d_lin : nullptr;
-      if (op_kind == SEM_OP_AXISYM_NS)
-        hipLaunchKernelGGL((k_axisym_apply<N, 1>), dim3(grid), dim3(ChainWaves<N>::block), 0, st,
-                           c->d_mapP, c->d_GP[2], u, y, c0, c1, c->rounds, acc, D, w, ns);
-      else
-        hipLaunchKernelGGL((k_axisym_apply<N, 2>), dim3(grid), dim3(ChainWaves<N>::block), 0, st,
-                           c->d_mapP, c->d_GP[2], u, y, c0, c1, c->rounds, acc, D, w, ns);
+    } else {
+      launch_chains<N, false>(c, op_kind, nodal, u, y, acc, lin, c0, c1, D, w, DFPlan{}, st);
     }
   }
   return SEM_OK;
@@ -1210,7 +1207,7 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
   // one-launch plan for the Poisson column kernel (SEM_DF=0: one launch per
   // colour); SEM_DF_LAG = colour lag of the ticket order, in chains
   int64_t df_lag = 0;
-  if (!mfma && c->dpn == 1) {
+  if (!mfma) {
     const char* e = std::getenv("SEM_DF");
     if (!e || std::atoi(e) != 0) {
       const char* l = std::getenv("SEM_DF_LAG");

@@ -284,6 +284,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t y_rsrc(const double* y) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(y), 0, 0x80000000, 0x00020000);
 }
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // one-launch plan (DFPlan below): every y access that another workgroup may
 // follow is agent-coherent -- sc1 stores (written through, line dropped
 // from the XCD's L2) and sc1 loads (MI355X_MICROARCH.md, inter-workgroup
@@ -415,6 +416,38 @@ struct DFWait {
   __device__ void operator()() const {}
 };
 
+// prologue / epilogue of a one-launch chain kernel (s: the kernel's LDS)
+struct DFShared {
+  int ticket;
+  uint32_t epoch;
+};
+__device__ __forceinline__ int64_t df_take(const DFPlan& df, int64_t c0, int64_t c1,
+                                           DFShared& s) {
+  if (threadIdx.x == 0) {
+    s.ticket = df.ticketed ? (int)__hip_atomic_fetch_add(df.state, 1u, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)
+                           : (int)blockIdx.x;
+    s.epoch = ld_agent(df.state + DF_EPOCH);
+  }
+  __syncthreads();
+  const int64_t chain = c0 + s.ticket;
+  if (chain < c1) df_wait(df, chain, s.epoch);
+  return chain;
+}
+// publish: every wave's y writes have left the CU, then one lane flags the
+// chain (hand-off table row 1: sc1 stores, vmcnt(0) in every storing wave,
+// workgroup barrier, one sc1 flag store); chain and epoch re-read from LDS so
+// nothing stays live through the kernel body
+__device__ __forceinline__ void df_publish(const DFPlan& df, int64_t c0, DFShared& s) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const volatile DFShared* vs = &s;
+    __hip_atomic_store((g_u32*)(df.flags + c0 + vs->ticket), vs->epoch, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 __device__ __forceinline__ void emit2(double* __restrict__ y, uint32_t raw, double v0, double v1,
                                       int accumulate) {
   const uint32_t a = (raw >> CODE_SHIFT) & 3u;
@@ -424,6 +457,29 @@ __device__ __forceinline__ void emit2(double* __restrict__ y, uint32_t raw, doub
   } else if (a == W_STORE || a == W_RMW) {
     const double o0 = rmw_load(dst), o1 = rmw_load(dst + 1);
     *reinterpret_cast<double2*>(dst) = make_double2(o0 + v0, o1 + v1);
+  } else if (a == W_ATOMIC) {
+    atomic_add_f64(dst, v0);
+    atomic_add_f64(dst + 1, v1);
+  }
+}
+
+// emit2 of the one-launch plan: sc1 operand loads and 16-B sc1 stores
+__device__ __forceinline__ void emit2_df(double* __restrict__ y, uint32_t raw, double v0,
+                                         double v1, int accumulate) {
+  const uint32_t a = (raw >> CODE_SHIFT) & 3u;
+  const uint32_t gid = raw & GID_MASK;
+  double* dst = y + 2 * (int64_t)gid;
+  if (a == W_STORE || a == W_RMW) {
+    const __amdgpu_buffer_rsrc_t ry = y_rsrc(y);
+    const uint32_t off = gid * 16u;
+    if (a == W_RMW || accumulate) {
+      const u32x4 o = __builtin_amdgcn_raw_buffer_load_b128(ry, off, 0, CPOL_SC1);
+      const double2 od = __builtin_bit_cast(double2, o);
+      v0 += od.x;
+      v1 += od.y;
+    }
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(v0, v1)), ry,
+                                           off, 0, CPOL_SC1);
   } else if (a == W_ATOMIC) {
     atomic_add_f64(dst, v0);
     atomic_add_f64(dst + 1, v1);
@@ -846,6 +902,8 @@ __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_
         emit1_df(y, raw[p], v[0][p], accumulate);
       else if (NC == 1)
         emit1(y, raw[p], v[0][p], accumulate);
+      else if (DF)
+        emit2_df(y, raw[p], v[0][p], v[NC - 1][p], accumulate);
       else
         emit2(y, raw[p], v[0][p], v[NC - 1][p], accumulate);
     }
@@ -898,24 +956,8 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
   __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * T::ES * NT];
   constexpr int CW = ChainWaves<N>::value;
   __shared__ double carry[2][CW][1][N];
-  __shared__ int s_ticket_df;
-  __shared__ uint32_t s_epoch_df;
-  int64_t chain;
-  uint32_t epoch = 0;
-  if constexpr (DF) {
-    if (threadIdx.x == 0) {
-      s_ticket_df = df.ticketed ? (int)__hip_atomic_fetch_add(df.state, 1u, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT)
-                             : (int)blockIdx.x;
-      s_epoch_df = ld_agent(df.state + DF_EPOCH);
-    }
-    __syncthreads();
-    chain = c0 + s_ticket_df;
-    epoch = s_epoch_df;
-    if (chain < c1) df_wait(df, chain, epoch);
-  } else {
-    chain = c0 + xcd_block(blockIdx.x, gridDim.x);
-  }
+  __shared__ DFShared sdf;
+  const int64_t chain = DF ? df_take(df, c0, c1, sdf) : c0 + xcd_block(blockIdx.x, gridDim.x);
   if (chain >= c1) return;  // uniform over the workgroup
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);  // provably uniform
   const int lane = threadIdx.x % WAVE;
@@ -947,19 +989,7 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
                                                           carry, accumulate, prev);
 #endif
   }
-  if constexpr (DF) {
-    // publish: every wave's y writes have left the CU, then one lane flags
-    // the chain (hand-off table row 1: sc1 stores, vmcnt(0) in every storing
-    // wave, workgroup barrier, one sc1 flag store)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {  // chain and epoch re-read from LDS: nothing kept live
-      volatile int* st = &s_ticket_df;
-      volatile uint32_t* se = &s_epoch_df;
-      __hip_atomic_store((g_u32*)(df.flags + c0 + *st), *se, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  if constexpr (DF) df_publish(df, c0, sdf);
 }
 
 // before every one-launch action: ticket counter to 0, next epoch
@@ -1292,16 +1322,17 @@ __device__ __forceinline__ void axisym_group_nodal(const MapRef& mref,
   wave_sync();
 }
 
-template <int N, bool M16>
+template <int N, bool M16, bool DF = false>
 __global__ void __launch_bounds__(ChainWaves<N>::block, SEM_AXI_MIN_WAVES)
     k_axisym_nodal(const MapRef mref, const double2* __restrict__ XG, const double* __restrict__ u,
                    double* __restrict__ y, int64_t c0, int64_t c1, int rounds, int accumulate,
-                   const DEO<N> D, const WVec<N> w) {
+                   const DEO<N> D, const WVec<N> w, const DFPlan df) {
   using T = Tile<N>;
   __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * 2 * T::ES];
   constexpr int CW = ChainWaves<N>::value;
   __shared__ double carry[2][CW][2][N];
-  const int64_t chain = c0 + blockIdx.x;
+  __shared__ DFShared sdf;
+  const int64_t chain = DF ? df_take(df, c0, c1, sdf) : c0 + blockIdx.x;
   if (chain >= c1) return;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   const int lane = threadIdx.x % WAVE;
@@ -1317,20 +1348,23 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, SEM_AXI_MIN_WAVES)
     double v[2][N];  // [0] omega row (y[2k]), [1] psi row (y[2k+1])
     axisym_group_nodal<N, M16>(mref, XG, u, g, lane, j, in_wave, LP, LO, D, w, wj, raw, v[0],
                                v[1]);
-    chain_emit<N, 2>(y, raw, v, lane, wave, rd, in_wave, carry, accumulate);
+    chain_emit<N, 2, false, CW, DF>(y, raw, v, lane, wave, rd, in_wave, carry, accumulate);
   }
+  if constexpr (DF) df_publish(df, c0, sdf);
 }
 
-template <int N, int MODE>
+template <int N, int MODE, bool DF = false>
 __global__ void __launch_bounds__(ChainWaves<N>::block)
     k_axisym_apply(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
                    const double* __restrict__ u, double* __restrict__ y, int64_t c0, int64_t c1,
-                   int rounds, int accumulate, const DEO<N> D, const WVec<N> w, const AxiNS ns) {
+                   int rounds, int accumulate, const DEO<N> D, const WVec<N> w, const AxiNS ns,
+                   const DFPlan df) {
   using T = Tile<N>;
   __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * 2 * T::ES];
   constexpr int CW = ChainWaves<N>::value;
   __shared__ double carry[2][CW][2][N];
-  const int64_t chain = c0 + blockIdx.x;
+  __shared__ DFShared sdf;
+  const int64_t chain = DF ? df_take(df, c0, c1, sdf) : c0 + blockIdx.x;
   if (chain >= c1) return;
   const int wave = threadIdx.x / WAVE;
   const int lane = threadIdx.x % WAVE;
@@ -1346,8 +1380,9 @@ __global__ void __launch_bounds__(ChainWaves<N>::block)
     double v[2][N];  // [0] omega row (y[2k]), [1] psi row (y[2k+1])
     axisym_group<N, MODE>(mapP, GP, u, g, lane, j, in_wave, LP, LO, D, w, wj, ns, raw, v[0],
                           v[1]);
-    chain_emit<N, 2>(y, raw, v, lane, wave, rd, in_wave, carry, accumulate);
+    chain_emit<N, 2, false, CW, DF>(y, raw, v, lane, wave, rd, in_wave, carry, accumulate);
   }
+  if constexpr (DF) df_publish(df, c0, sdf);
 }
 
 // ---------------------------------------------------------------------------

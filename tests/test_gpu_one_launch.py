@@ -130,3 +130,41 @@ def test_one_launch_accumulate_and_graph_replay(gpu, gll):
         torch.cuda.synchronize()
         _check(ys.cpu().numpy() / (k + 1), ref, ext)
     assert op.plan_info()["wait_timeouts"] == 0
+
+
+@pytest.mark.parametrize("geometry", ["nodal", "stored"])
+def test_one_launch_axisymmetric(gpu, gll, monkeypatch, geometry):
+    """The axisymmetric Stokes block (two DOFs per node, 16-B read-modify-
+    writes) and the Navier-Stokes residual / Jacobian-vector product in one
+    launch: equal to the per-colour launches to 1e-13, the Stokes block to the
+    oracle at 1e-12."""
+    import sem_oracle
+    from spectralelementmethod_amd import meshgen
+    from spectralelementmethod_amd.operators import SEMOperator
+    p = 6
+    nodes, e2n = meshgen.annulus(40, 36, p)
+    rng = np.random.default_rng(8)
+    sol = torch.from_numpy(rng.standard_normal(2 * nodes.shape[1])).to(gpu)
+    dirn = torch.from_numpy(rng.standard_normal(2 * nodes.shape[1])).to(gpu)
+    monkeypatch.setenv("SEM_DF_LAG", "8")
+    out = {}
+    for df in ("1", "0"):
+        monkeypatch.setenv("SEM_DF", df)
+        op = SEMOperator(p, e2n, nodes, dofs_per_node=2, device=gpu, geometry=geometry)
+        assert op.plan_info()["plan"] == ("chains-one-launch" if df == "1" else "chains")
+        op.set_reynolds(5.0)
+        ys = op.apply(sol, kind="axisym_stokes")
+        yn = op.apply(sol, kind="axisym_ns", linearize=True)
+        yj = op.apply(dirn, kind="axisym_ns_jvp")
+        out[df] = [t.cpu().numpy() for t in (ys, yn, yj)]
+        assert op.plan_info()["wait_timeouts"] == 0
+    for a, b in zip(out["1"], out["0"]):
+        assert rel_l2(a, b) < 1e-13
+    nodes_1d, bary, quad = sem_oracle.gll_unfold(gll["half_%d" % p])
+    D = sem_oracle.diff_matrix(nodes_1d, bary)
+    _, lu = sem_oracle.interp_eq_lu(nodes_1d, bary)
+    e2n64 = e2n.astype(np.int64)
+    xp, _, invJ, _, detJxW = sem_oracle.geometry(nodes, e2n64, D, quad, lu, batched=True)
+    F = sem_oracle.axisym_factors(xp, invJ, detJxW)
+    ref = sem_oracle.axisym_apply(F, D, e2n64, sol.cpu().numpy(), nodes.shape[1])
+    assert rel_l2(out["1"][0], ref) < TOL
