@@ -133,9 +133,9 @@ int sem_set_map_shared(sem_ctx* ctx, const uint32_t* d_e2n, const uint8_t* d_nod
  * 1 element-coloured chains (chosen when the element order defeats the chain
  * patterns: more than half of the groups would need atomics; SEM_PLAN=1 / 0
  * in the environment forces / forbids it), 2 one element per wavefront
- * (MFMA kernel), 3 chains of consecutive elements in ONE launch (the
- * Poisson column kernel's default when dofs_per_node == 1; SEM_DF=0 in the
- * environment gives one launch per colour class instead): workgroups take
+ * (MFMA kernel), 3 chains of consecutive elements in ONE launch (SEM_DF=1
+ * in the environment; measured slower than the colour launches on MI355X,
+ * DESIGN.md §5, so not the default): workgroups take
  * chains from a ticket counter, and a chain starts once every chain that
  * wrote one of its shared nodes earlier in ticket order has published
  * (per-chain flags); [5] is then 1 and [8] the chain count.

@@ -223,6 +223,7 @@ struct sem_ctx {
   unsigned long long* d_bad = nullptr;
   // one-launch plan of the Poisson column kernel (DFPlan, sem_kernels.h)
   bool df = false;
+  int df_ticketed = 1;  // SEM_DF_TICKET=0: chain = blockIdx (timing experiments)
   int64_t df_lag = 0;
   int64_t n_deps = 0;
   int* d_dep_start = nullptr;
@@ -393,11 +394,7 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
   std::memcpy(w.v, c->hw, sizeof(w.v));
   const bool nodal = use_nodal(c, op_kind);
   if (c->df) {  // every chain in one launch (DFPlan, sem_kernels.h)
-    static const int ticketed = [] {
-      const char* e = std::getenv("SEM_DF_TICKET");
-      return e ? std::atoi(e) : 1;
-    }();
-    const DFPlan df{c->d_dep_start, c->d_dep_idx, c->d_df_flags, c->d_df_state, ticketed};
+    const DFPlan df{c->d_dep_start, c->d_dep_idx, c->d_df_flags, c->d_df_state, c->df_ticketed};
     hipLaunchKernelGGL(k_df_begin, dim3(1), dim3(WAVE), 0, st, c->d_df_state);
     launch_chains<N, true>(c, op_kind, nodal, u, y, acc, lin, c->colour_start.front(),
                            c->colour_start.back(), D, w, df, st);
@@ -1204,12 +1201,14 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
   int rounds = 1;
   if (const char* s = std::getenv("SEM_CHAIN_ROUNDS")) rounds = std::max(1, std::atoi(s));
   const bool mfma = want_mfma(c);
-  // one-launch plan for the Poisson column kernel (SEM_DF=0: one launch per
-  // colour); SEM_DF_LAG = colour lag of the ticket order, in chains
+  // one-launch plan of the chain kernels (SEM_DF=1; measured slower than one
+  // launch per colour on MI355X at every BASELINE configuration but p = 12,
+  // DESIGN.md §5, profiles/r02/one_launch); SEM_DF_LAG = colour lag of the
+  // ticket order, in chains
   int64_t df_lag = 0;
   if (!mfma) {
     const char* e = std::getenv("SEM_DF");
-    if (!e || std::atoi(e) != 0) {
+    if (e && std::atoi(e) == 1) {
       const char* l = std::getenv("SEM_DF_LAG");
       df_lag = l ? std::max<int64_t>(1, std::atoll(l)) : SEM_DF_LAG_DEFAULT;
     }
@@ -1284,6 +1283,10 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
   c->colour_start = P.colour_start;
   c->df = P.df;
   c->df_lag = P.df ? df_lag : 0;
+  {
+    const char* t = std::getenv("SEM_DF_TICKET");
+    c->df_ticketed = t ? std::atoi(t) : 1;
+  }
   c->n_deps = (int64_t)P.dep_idx.size();
   (void)hipFree(c->d_dep_start);
   (void)hipFree(c->d_dep_idx);

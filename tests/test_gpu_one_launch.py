@@ -1,5 +1,6 @@
-"""The one-launch scatter plan of the Poisson column kernel (DESIGN.md §5,
-DFPlan in csrc/sem_kernels.h): every chain in one launch, workgroups taking
+"""The one-launch scatter plan of the chain kernels (SEM_DF=1; DESIGN.md §5,
+DFPlan in csrc/sem_kernels.h; measured slower than one launch per colour,
+so not the default): every chain in one launch, workgroups taking
 chains from a ticket counter, a chain starting once the chains that wrote its
 shared nodes earlier in ticket order have published their flags.
 
@@ -53,6 +54,7 @@ def test_one_launch_vs_colour_launches(gpu, gll, monkeypatch, p, nex, ney):
     u = np.random.default_rng(p).standard_normal(nodes.shape[1])
     ut = torch.from_numpy(u).to(gpu)
     monkeypatch.setenv("SEM_PLAN", "0")
+    monkeypatch.setenv("SEM_DF", "1")
     monkeypatch.setenv("SEM_DF_LAG", "4")  # small mesh: a lag below the chain count
     op1 = SEMOperator(p, e2n, nodes, device=gpu, kernel="column")
     info = op1.plan_info()
@@ -81,6 +83,7 @@ def test_one_launch_lag_and_dispatch(gpu, gll, monkeypatch, lag, ticket, geometr
     p = 8
     nodes, e2n = _mesh(p, 128, 96)
     u = np.random.default_rng(11).standard_normal(nodes.shape[1])
+    monkeypatch.setenv("SEM_DF", "1")
     monkeypatch.setenv("SEM_DF_LAG", str(lag))
     monkeypatch.setenv("SEM_DF_TICKET", ticket)
     op = SEMOperator(p, e2n, nodes, device=gpu, geometry=geometry)
@@ -96,13 +99,14 @@ def test_one_launch_lag_and_dispatch(gpu, gll, monkeypatch, lag, ticket, geometr
     assert op.plan_info()["wait_timeouts"] == 0
 
 
-def test_one_launch_accumulate_and_graph_replay(gpu, gll):
+def test_one_launch_accumulate_and_graph_replay(gpu, gll, monkeypatch):
     """accumulate mode (first writers read y too), and the action captured in
     a HIP graph: the epoch lives on the device, so every replay waits for the
     flags of ITS OWN launch."""
     from spectralelementmethod_amd.operators import SEMOperator
     p = 6
     nodes, e2n = _mesh(p, 48, 40)
+    monkeypatch.setenv("SEM_DF", "1")
     op = SEMOperator(p, e2n, nodes, device=gpu)
     assert op.plan_info()["plan"] == "chains-one-launch"
     g = torch.Generator(device=gpu).manual_seed(4)

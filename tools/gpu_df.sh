@@ -28,5 +28,7 @@ for lag in 512 1024 4096; do
   run p8_1024_lag$lag "SEM_DF_LAG=$lag" || exit 1
 done
 run p8_1024_noticket "SEM_DF_TICKET=0" || exit 1
+run axi6_512_colours "SEM_DF=0" --op axisym_stokes --p 6 --nex 512 --ney 512 || exit 1
+run axi6_512_df "SEM_DF=1" --op axisym_stokes --p 6 --nex 512 --ney 512 || exit 1
 run p16_198_lag1024 "SEM_DF_LAG=1024" --p 16 --nex 198 --ney 198 || exit 1
 run p16_198_lag4096 "SEM_DF_LAG=4096" --p 16 --nex 198 --ney 198 || exit 1
