@@ -175,6 +175,9 @@ inline int grid_for(int64_t n, int per_block = BLOCK, int cap = 8192) {
 constexpr int MAX_COLOURS = 8;  // + one trailing all-atomic class
 // colour lag of the one-launch plan's ticket order, in chains (about two
 // generations of resident workgroups at p = 8: 4 per CU x 256 CUs)
+#ifndef SEM_SEAM_DEFAULT
+#define SEM_SEAM_DEFAULT 0
+#endif
 #ifndef SEM_DF_LAG_DEFAULT
 #define SEM_DF_LAG_DEFAULT 2048
 #endif
@@ -230,6 +233,14 @@ struct sem_ctx {
   int* d_dep_idx = nullptr;
   uint32_t* d_df_flags = nullptr;
   uint32_t* d_df_state = nullptr;
+  // seam plan of the Poisson column kernel (SeamPlan, sem_kernels.h)
+  bool seam = false;
+  int seam_ns = 0;
+  int64_t n_seam = 0;
+  uint8_t* d_ccol = nullptr;
+  uint32_t* d_seam_gid = nullptr;
+  uint16_t* d_seam_mask = nullptr;
+  double* d_seam_buf = nullptr;
 };
 
 namespace sem {
@@ -341,7 +352,7 @@ bool use_nodal(const sem_ctx* c, int op_kind) {
 }
 
 // one chain-kernel launch, one-launch plan (DF) or a colour class
-template <int N, bool DF>
+template <int N, bool DF, bool SEAM = false>
 void launch_chains(sem_ctx* c, int op_kind, bool nodal, const double* u, double* y, int acc,
                    bool lin, int64_t c0, int64_t c1, const DEO<N>& D, const WVec<N>& w,
                    const DFPlan& df, hipStream_t st) {
@@ -351,18 +362,21 @@ void launch_chains(sem_ctx* c, int op_kind, bool nodal, const double* u, double*
   if (op_kind == SEM_OP_POISSON) {
     const double* GP = nodal ? nullptr : c->d_GP[0];
     const double2* XG = nodal ? c->d_XG : nullptr;
+    const SeamPlan sp{c->d_ccol, c->d_seam_buf, c->n_node};
     if (nodal && c->map16)
-      hipLaunchKernelGGL((k_poisson_apply<N, true, true, DF>), g, b, 0, st, mr, GP, XG, u, y, c0,
-                         c1, R, acc, D, w, df);
+      hipLaunchKernelGGL((k_poisson_apply<N, true, true, DF, SEAM>), g, b, 0, st, mr, GP, XG, u,
+                         y, c0, c1, R, acc, D, w, df, sp);
     else if (nodal)
-      hipLaunchKernelGGL((k_poisson_apply<N, true, false, DF>), g, b, 0, st, mr, GP, XG, u, y, c0,
-                         c1, R, acc, D, w, df);
+      hipLaunchKernelGGL((k_poisson_apply<N, true, false, DF, SEAM>), g, b, 0, st, mr, GP, XG, u,
+                         y, c0, c1, R, acc, D, w, df, sp);
     else if (c->map16)
-      hipLaunchKernelGGL((k_poisson_apply<N, false, true, DF>), g, b, 0, st, mr, GP, XG, u, y, c0,
-                         c1, R, acc, D, w, df);
+      hipLaunchKernelGGL((k_poisson_apply<N, false, true, DF, SEAM>), g, b, 0, st, mr, GP, XG, u,
+                         y, c0, c1, R, acc, D, w, df, sp);
     else
-      hipLaunchKernelGGL((k_poisson_apply<N, false, false, DF>), g, b, 0, st, mr, GP, XG, u, y,
-                         c0, c1, R, acc, D, w, df);
+      hipLaunchKernelGGL((k_poisson_apply<N, false, false, DF, SEAM>), g, b, 0, st, mr, GP, XG,
+                         u, y, c0, c1, R, acc, D, w, df, sp);
+  } else if constexpr (SEAM) {
+    // Poisson only (the seam plan is built for dpn = 1 contexts)
   } else if (op_kind == SEM_OP_AXISYM_STOKES && nodal) {
     if (c->map16)
       hipLaunchKernelGGL((k_axisym_nodal<N, true, DF>), g, b, 0, st, mr, c->d_XG, u, y, c0, c1, R,
@@ -393,6 +407,15 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
   WVec<N> w;
   std::memcpy(w.v, c->hw, sizeof(w.v));
   const bool nodal = use_nodal(c, op_kind);
+  if (c->seam && op_kind == SEM_OP_POISSON) {  // one launch + the seam sums (SeamPlan)
+    launch_chains<N, false, true>(c, op_kind, nodal, u, y, acc, lin, c->colour_start.front(),
+                                  c->colour_start.back(), D, w, DFPlan{}, st);
+    if (c->n_seam)
+      hipLaunchKernelGGL(k_seam_sum, dim3(grid_for(c->n_seam)), dim3(BLOCK), 0, st, y,
+                         c->d_seam_gid, c->d_seam_mask, c->n_seam, c->d_seam_buf, c->n_node,
+                         c->seam_ns, acc);
+    return SEM_OK;
+  }
   if (c->df) {  // every chain in one launch (DFPlan, sem_kernels.h)
     const DFPlan df{c->d_dep_start, c->d_dep_idx, c->d_df_flags, c->d_df_state, c->df_ticketed};
     hipLaunchKernelGGL(k_df_begin, dim3(1), dim3(WAVE), 0, st, c->d_df_state);
@@ -530,6 +553,14 @@ struct Plan {
   // earlier chains that last wrote one of its shared nodes
   bool df = false;
   std::vector<int> dep_start, dep_idx;
+  // seam plan: chains in element order, one launch; nodes written by several
+  // chains go through per-colour slots summed by k_seam_sum
+  bool seam = false;
+  std::vector<uint8_t> chain_colour;  // [chain] in launch order
+  std::vector<uint32_t> seam_gid;
+  std::vector<uint16_t> seam_mask;  // colours | 0x100 prior
+  int seam_ns = 0;
+  bool seam_failed = false;
 };
 
 // node_state (may be empty): SEM_NODE_PRIOR = y already holds a value when
@@ -537,7 +568,7 @@ struct Plan {
 // SEM_NODE_OTHER = another operator writes it (not zeroed when unreferenced).
 int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node, int n,
                int rounds, const std::vector<uint8_t>& node_state, Plan& P,
-               int64_t df_lag = 0) {
+               int64_t df_lag = 0, bool seam = false) {
   const int epw = WAVE / n, lw = epw * n, nn = n * n;
   const int64_t n_groups = (n_elem + epw - 1) / epw;
   const int CW = chain_waves_of(n);  // groups of a chain that run concurrently
@@ -605,10 +636,42 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
   }
   std::vector<uint8_t>().swap(cmask);
   // 3. launch order: colour-major (one launch per colour), or for the
-  // one-launch plan the ticket order chain + colour * lag
+  // one-launch plan the ticket order chain + colour * lag, or for the seam
+  // plan element order in one launch
   std::vector<int64_t> order(n_chains);
-  P.df = df_lag > 0 && conforming && n_chains > 1;
-  if (P.df) {
+  P.seam = seam && conforming;
+  for (int64_t ch = 0; ch < n_chains && P.seam; ++ch)
+    if (colour[ch] >= MAX_COLOURS) P.seam = false;
+  P.df = !P.seam && df_lag > 0 && conforming && n_chains > 1;
+  std::vector<uint8_t> nw;      // seam plan: chains writing each node (saturating)
+  std::vector<uint16_t> smask;  // and their colours
+  if (P.seam) {
+    for (int64_t ch = 0; ch < n_chains; ++ch) order[ch] = ch;
+    P.colour_start = {0, n_chains};
+    nw.assign(n_node, 0);
+    smask.assign(n_node, 0);
+    std::vector<int32_t> lastc2(n_node, -1);
+    int maxc = 0;
+    for (int64_t ch = 0; ch < n_chains; ++ch) {
+      int64_t e0, e1;
+      chain_elems(ch, e0, e1);
+      maxc = std::max(maxc, colour[ch]);
+      for (int64_t e = e0; e < e1; ++e)
+        for (int r = 0; r < n; ++r)
+          for (int jj = 0; jj < n; ++jj)
+            if (is_bnd(r, jj)) {
+              const uint32_t gid = e2n[e * nn + r * n + jj];
+              if (lastc2[gid] != (int32_t)ch) {
+                lastc2[gid] = (int32_t)ch;
+                if (nw[gid] < 255) nw[gid]++;
+                smask[gid] |= (uint16_t)(1u << colour[ch]);
+              }
+            }
+    }
+    P.seam_ns = maxc + 1;
+    P.chain_colour.resize(n_chains);
+    for (int64_t ch = 0; ch < n_chains; ++ch) P.chain_colour[ch] = (uint8_t)colour[ch];
+  } else if (P.df) {
     for (int64_t ch = 0; ch < n_chains; ++ch) order[ch] = ch;
     std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
       return a + colour[a] * df_lag < b + colour[b] * df_lag;
@@ -712,6 +775,9 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
             out[pos - 1] |= W_MERGE << CODE_SHIFT;
           } else if (a == 2) {
             code = W_SKIP;
+          } else if (P.seam && nw[gid] >= 2) {
+            code = W_ATOMIC;  // seam slot of this chain's colour (k_seam_sum)
+            if (a == 3) code |= W_CARRY;
           } else {
             code = written[gid] ? W_RMW : W_STORE;
             written[gid] = 1;
@@ -735,6 +801,19 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
   for (int64_t i = 0; i < n_node; ++i)
     if (cnt[i] == 0 && (node_state.empty() || !node_state[i])) P.zero.push_back((uint32_t)i);
   std::sort(P.zero.begin(), P.zero.end());
+  if (P.seam) {
+    if (P.n_atomic_groups) {  // in-round sharing the chains cannot express: no seam plan
+      P.seam = false;
+      P.seam_failed = true;  // the caller plans again without seams
+      return SEM_OK;
+    }
+    for (int64_t i = 0; i < n_node; ++i)
+      if (nw[i] >= 2) {
+        P.seam_gid.push_back((uint32_t)i);
+        const bool prior = !node_state.empty() && (node_state[i] & SEM_NODE_PRIOR);
+        P.seam_mask.push_back((uint16_t)(smask[i] | (prior ? 0x100u : 0u)));
+      }
+  }
   return SEM_OK;
 }
 
@@ -1156,6 +1235,10 @@ void sem_ctx_destroy(sem_ctx* c) {
   (void)hipFree(c->d_dep_idx);
   (void)hipFree(c->d_df_flags);
   (void)hipFree(c->d_df_state);
+  (void)hipFree(c->d_ccol);
+  (void)hipFree(c->d_seam_gid);
+  (void)hipFree(c->d_seam_mask);
+  (void)hipFree(c->d_seam_buf);
   delete c;
 }
 
@@ -1213,8 +1296,18 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
       df_lag = l ? std::max<int64_t>(1, std::atoll(l)) : SEM_DF_LAG_DEFAULT;
     }
   }
+  // seam plan (SEM_SEAM=1; Poisson contexts): one launch + seam sums
+  bool seam = false;
+  if (!mfma && c->dpn == 1) {
+    const char* e = std::getenv("SEM_SEAM");
+    seam = e ? std::atoi(e) == 1 : SEM_SEAM_DEFAULT;
+  }
   int rc = mfma ? build_plan_elem(h, c->n_elem, c->n_node, n, state, P)
-                : build_plan(h, c->n_elem, c->n_node, n, rounds, state, P, df_lag);
+                : build_plan(h, c->n_elem, c->n_node, n, rounds, state, P, df_lag, seam);
+  if (!rc && P.seam_failed) {
+    P = Plan();
+    rc = build_plan(h, c->n_elem, c->n_node, n, rounds, state, P, df_lag, false);
+  }
   if (rc) return rc;
   // element-coloured fallback for orders that defeat the chain patterns
   // (SEM_PLAN=1 forces it, SEM_PLAN=0 forbids it)
@@ -1312,6 +1405,32 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
     // flags hold the epoch of their last action: restart both from 0
     HIP_TRY(hipMemset(c->d_df_state, 0, 128 * sizeof(uint32_t)));
   }
+  c->seam = P.seam;
+  c->seam_ns = P.seam_ns;
+  c->n_seam = (int64_t)P.seam_gid.size();
+  (void)hipFree(c->d_ccol);
+  (void)hipFree(c->d_seam_gid);
+  (void)hipFree(c->d_seam_mask);
+  (void)hipFree(c->d_seam_buf);
+  c->d_ccol = nullptr;
+  c->d_seam_gid = nullptr;
+  c->d_seam_mask = nullptr;
+  c->d_seam_buf = nullptr;
+  if (P.seam) {
+    HIP_TRY(hipMalloc(&c->d_ccol, P.chain_colour.size()));
+    HIP_TRY(hipMemcpy(c->d_ccol, P.chain_colour.data(), P.chain_colour.size(),
+                      hipMemcpyHostToDevice));
+    if (c->n_seam) {
+      HIP_TRY(hipMalloc(&c->d_seam_gid, c->n_seam * sizeof(uint32_t)));
+      HIP_TRY(hipMemcpy(c->d_seam_gid, P.seam_gid.data(), c->n_seam * sizeof(uint32_t),
+                        hipMemcpyHostToDevice));
+      HIP_TRY(hipMalloc(&c->d_seam_mask, c->n_seam * sizeof(uint16_t)));
+      HIP_TRY(hipMemcpy(c->d_seam_mask, P.seam_mask.data(), c->n_seam * sizeof(uint16_t),
+                        hipMemcpyHostToDevice));
+      // slots addressed by node id (only seam nodes' slots are touched)
+      HIP_TRY(hipMalloc(&c->d_seam_buf, (size_t)c->n_node * c->seam_ns * sizeof(double)));
+    }
+  }
   c->n_atomic_groups = P.n_atomic_groups;
   c->conforming = P.conforming;
   (void)hipFree(c->d_owner);
@@ -1348,14 +1467,14 @@ int sem_plan_info(sem_ctx* c, int64_t* info, int n_info) {
   const bool eff_nodal = c->xg_valid ? true : (c->d_GP[0] ? false : nodal_mode(c));
   vals[NV - 6] = eff_nodal ? SEM_GEOM_NODAL : SEM_GEOM_STORED;
   // plan: chains, element-coloured, element, chains in one launch
-  vals[NV - 5] = c->mfma ? 2 : (c->ecol ? 1 : (c->df ? 3 : 0));
+  vals[NV - 5] = c->mfma ? 2 : (c->ecol ? 1 : (c->df ? 3 : (c->seam ? 4 : 0)));
   // the same for the axisymmetric Stokes block (dofs_per_node = 2)
   const bool axi_nodal =
       c->xg_axi ? true : (c->d_GP[1] ? false : nodal_mode_op(c, SEM_OP_AXISYM_STOKES));
   vals[NV - 4] = c->dpn == 2 ? (axi_nodal ? SEM_GEOM_NODAL : SEM_GEOM_STORED) : 0;
   // one-launch plan: dependency edges, colour lag, waits that timed out so
   // far (read from the device: synchronises with the device)
-  vals[NV - 3] = c->n_deps;
+  vals[NV - 3] = c->seam ? c->n_seam : c->n_deps;
   vals[NV - 2] = c->df_lag;
   vals[NV - 1] = 0;
   if (c->df && n_info >= NV) {

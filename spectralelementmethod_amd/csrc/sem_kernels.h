@@ -84,9 +84,12 @@ constexpr uint32_t W_CARRY = 8;   // add the value handed over by the previous g
 // measured on MI355X at ~1e7 DOF it pays up to n = 13 (p = 12: 0.142 vs
 // 0.163 ms) and costs at n = 17 (p = 16: 0.197 vs 0.176 ms; 246 vs 159
 // VGPRs, profiles/r02/variants).
+#ifndef SEM_RMW_PREFETCH_17
+#define SEM_RMW_PREFETCH_17 0  // n = 17: 0 off, 1 / 2 as SEM_RMW_PREFETCH
+#endif
 template <int N>
 struct RmwPrefetch {
-  static constexpr int value = N <= 16 ? SEM_RMW_PREFETCH : 0;
+  static constexpr int value = N <= 16 ? SEM_RMW_PREFETCH : SEM_RMW_PREFETCH_17;
 };
 
 // D1 in even-odd form.  D is centro-antisymmetric (D[N-1-i][N-1-j] =
@@ -332,6 +335,29 @@ __device__ __forceinline__ void emit1p(double* __restrict__ y, uint32_t raw, dou
   }
 }
 
+// Seam plan: a node written by several chains is not
+// read-modified-written in colour order; each chain stores its partial sum
+// in the node's slot for the chain's colour, buf[colour * n_node + gid], and
+// a second launch (k_seam_sum) adds the slots into y in colour order.  All
+// chains then run in one launch with no ordering and no read-modify-writes
+// between chains.  The code action 3 (W_ATOMIC) means "seam slot" in this
+// plan (the plan has no atomic chains).
+struct SeamOut {
+  double* base = nullptr;  // buf + colour * n_node of the chain
+};
+__device__ __forceinline__ void emit1_seam(double* __restrict__ y, uint32_t raw, double v,
+                                           int accumulate, const SeamOut& so) {
+  const uint32_t a = (raw >> CODE_SHIFT) & 3u;
+  const uint32_t gid = raw & GID_MASK;
+  double* dst = y + gid;
+  if (a == W_STORE)
+    __builtin_nontemporal_store(accumulate ? rmw_load(dst) + v : v, dst);
+  else if (a == W_RMW)  // first touch of a SEM_NODE_PRIOR node
+    __builtin_nontemporal_store(rmw_load(dst) + v, dst);
+  else if (a == W_ATOMIC)
+    __builtin_nontemporal_store(v, so.base + gid);
+}
+
 // emit1 of the one-launch plan (no prefetch): sc1 operand loads and stores
 __device__ __forceinline__ void emit1_df(double* __restrict__ y, uint32_t raw, double v,
                                          int accumulate) {
@@ -405,6 +431,13 @@ __device__ __forceinline__ void df_wait(const DFPlan& df, int64_t chain, uint32_
 
 struct NoWait {
   static constexpr int aux = CPOL_NT;
+  static constexpr bool prefetch = true;
+  __device__ void operator()() const {}
+};
+// seam plan: nothing to prefetch (no read-modify-writes between chains)
+struct NoPrefetch {
+  static constexpr int aux = CPOL_NT;
+  static constexpr bool prefetch = false;
   __device__ void operator()() const {}
 };
 // the one-launch plan waits in the kernel's prologue, with nothing live
@@ -413,6 +446,7 @@ struct NoWait {
 // read-modify-write operands are read sc1
 struct DFWait {
   static constexpr int aux = CPOL_SC1;
+  static constexpr bool prefetch = true;
   __device__ void operator()() const {}
 };
 
@@ -673,10 +707,11 @@ __device__ __forceinline__ void poisson_group_stored(const MapRef& mref,
       w0[m] = fma(g00, d0[m], g01 * d1);
       L[m * RS + j] = fma(g01, d0[m], g11 * d1);  // w1, same lane's slot
     }
-    if constexpr (RmwPrefetch<N>::value) pre();
-    if constexpr (RmwPrefetch<N>::value == 1) rmw_prefetch<N, Pre::aux>(y, raw, accumulate, prev);
+    constexpr int PF = Pre::prefetch ? RmwPrefetch<N>::value : 0;
+    if constexpr (PF) pre();
+    if constexpr (PF == 1) rmw_prefetch<N, Pre::aux>(y, raw, accumulate, prev);
     deo_apply_t<N>(D, w0, v);
-    if constexpr (RmwPrefetch<N>::value == 2) rmw_prefetch<N, Pre::aux>(y, raw, accumulate, prev);
+    if constexpr (PF == 2) rmw_prefetch<N, Pre::aux>(y, raw, accumulate, prev);
   }
   wave_sync();
   // row i = j: yb[i][q] = sum_n D[n][q] w1[i][n]
@@ -818,10 +853,11 @@ __device__ __forceinline__ void nodal_laplacian(const double (&uc)[N], int j, do
       w0[m] = fma(g00[m], d0[m], g01[m] * d1);
       A[m * RS + j] = fma(g01[m], d0[m], B[m * RS + j] * d1);
     }
-    if constexpr (RmwPrefetch<N>::value) pre();
-    if constexpr (RmwPrefetch<N>::value == 1) rmw_prefetch<N, Pre::aux>(y, raw, accumulate, prev);
+    constexpr int PF = Pre::prefetch ? RmwPrefetch<N>::value : 0;
+    if constexpr (PF) pre();
+    if constexpr (PF == 1) rmw_prefetch<N, Pre::aux>(y, raw, accumulate, prev);
     deo_apply_t<N>(D, w0, v);
-    if constexpr (RmwPrefetch<N>::value == 2) rmw_prefetch<N, Pre::aux>(y, raw, accumulate, prev);
+    if constexpr (PF == 2) rmw_prefetch<N, Pre::aux>(y, raw, accumulate, prev);
   }
   wave_sync();
   row_pass<N, RS, true, false>(A, j, D);
@@ -860,11 +896,13 @@ __device__ __forceinline__ void poisson_group_nodal(const MapRef& mref,
 // Scatter of one group's column values through the coded map, with the
 // in-group merge (next lane) and the chain carry (previous group) applied.
 // ncomp values per node (1: Poisson, 2: axisymmetric block).
-template <int N, int NC, bool PRE = false, int CW = ChainWaves<N>::value, bool DF = false>
+template <int N, int NC, bool PRE = false, int CW = ChainWaves<N>::value, bool DF = false,
+          bool SEAM = false>
 __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_t (&raw)[N],
                                            double (&v)[NC][N], int lane, int wave, int rd,
                                            bool in_wave, double (*carry)[CW][NC][N],
-                                           int accumulate, const double* prev = nullptr) {
+                                           int accumulate, const double* prev = nullptr,
+                                           const SeamOut& so = SeamOut()) {
   constexpr int LW = Tile<N>::LW;
 #pragma unroll
   for (int c = 0; c < NC; ++c)
@@ -896,7 +934,9 @@ __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_
   if (in_wave) {
 #pragma unroll
     for (int p = 0; p < N; ++p) {
-      if constexpr (PRE)
+      if constexpr (SEAM && NC == 1)
+        emit1_seam(y, raw[p], v[0][p], accumulate, so);
+      else if constexpr (PRE)
         emit1p<DF>(y, raw[p], v[0][p], prev[p]);
       else if (DF && NC == 1)
         emit1_df(y, raw[p], v[0][p], accumulate);
@@ -945,12 +985,18 @@ struct PoissonMinWaves {
                                                         : 1;
 };
 
-template <int N, bool NODAL, bool M16, bool DF = false>
+struct SeamPlan {
+  const uint8_t* __restrict__ colour;  // [chain]
+  double* buf;                         // [colour][node]
+  int64_t n_node;
+};
+
+template <int N, bool NODAL, bool M16, bool DF = false, bool SEAM = false>
 __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODAL>::value))
     k_poisson_apply(const MapRef mref, const double* __restrict__ GP,
                     const double2* __restrict__ XG, const double* __restrict__ u,
                     double* __restrict__ y, int64_t c0, int64_t c1, int rounds, int accumulate,
-                    const DEO<N> D, const WVec<N> w, const DFPlan df) {
+                    const DEO<N> D, const WVec<N> w, const DFPlan df, const SeamPlan sp) {
   using T = Tile<N, NODAL ? SEM_TILE_PAD_NODAL : SEM_TILE_PAD_STORED>;
   constexpr int NT = NODAL ? 2 : 1;  // tiles per element slot
   __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * T::ES * NT];
@@ -974,8 +1020,10 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
     const int64_t g = (chain * rounds + rd) * CW + wave;
     uint32_t raw[N];
     double v[1][N], prev[N];
-    using Pre = typename std::conditional<DF, DFWait, NoWait>::type;
+    using Pre = typename std::conditional<DF, DFWait,
+                                          typename std::conditional<SEAM, NoPrefetch, NoWait>::type>::type;
     const Pre pre{};
+    constexpr bool PRE = RmwPrefetch<N>::value > 0 && Pre::prefetch;
     if constexpr (NODAL)
       poisson_group_nodal<N, M16>(mref, XG, u, g, lane, j, in_wave, L, LB, D, w, wj, raw, v[0],
                                   y, accumulate, prev, pre);
@@ -985,11 +1033,37 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
 #ifdef SEM_DIAG_NO_STORE
     if (in_wave && v[0][0] == 1234.5678) y[0] = v[0][1];  // timing-only
 #else
-    chain_emit<N, 1, (RmwPrefetch<N>::value > 0), CW, DF>(y, raw, v, lane, wave, rd, in_wave,
-                                                          carry, accumulate, prev);
+    SeamOut so;
+    if constexpr (SEAM) so.base = sp.buf + sp.colour[chain] * sp.n_node;
+    chain_emit<N, 1, PRE, CW, DF, SEAM>(y, raw, v, lane, wave, rd, in_wave, carry, accumulate,
+                                        prev, so);
 #endif
   }
   if constexpr (DF) df_publish(df, c0, sdf);
+}
+
+// second launch of the seam plan: y[gid] (+)= the colour slots, in colour
+// order (the order of the colour launches' read-modify-writes: the same
+// rounding).  mask bits 0-7: colours that wrote the node; bit 8: y already
+// holds a value (SEM_NODE_PRIOR)
+__global__ void k_seam_sum(double* __restrict__ y, const uint32_t* __restrict__ gid,
+                           const uint16_t* __restrict__ mask, int64_t n,
+                           const double* __restrict__ buf, int64_t n_node, int ns,
+                           int accumulate) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t g = gid[i];
+    const uint32_t m = mask[i];
+    double s = (accumulate || (m & 0x100u)) ? y[g] : 0.0;
+    bool first = !(accumulate || (m & 0x100u));
+    for (int c = 0; c < ns; ++c)
+      if (m & (1u << c)) {
+        const double b = __builtin_nontemporal_load(buf + c * n_node + g);
+        s = first ? b : s + b;
+        first = false;
+      }
+    y[g] = s;
+  }
 }
 
 // before every one-launch action: ticket counter to 0, next epoch

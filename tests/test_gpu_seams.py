@@ -1,0 +1,93 @@
+"""The seam plan of the Poisson column kernel (SEM_SEAM=1; DESIGN.md §5,
+SeamPlan / k_seam_sum in csrc/sem_kernels.h): every chain in ONE launch in
+element order, nodes written by several chains stored per writer colour and
+summed by a second launch in colour order.
+
+The seam sums add the same partial sums in the same order as the colour
+launches' read-modify-writes, so the two plans agree to the last bit on the
+structured meshes (checked at 1e-15 to stay robust to a compiler contracting
+a multiply-add differently in the two kernel instantiations), and both meet
+the oracle (1e-12; the north-star bar is 1e-10)."""
+import numpy as np
+import pytest
+
+from conftest import rel_l2
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-12
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda", 0)
+
+
+def _oracle(gll, nodes, e2n, p, u):
+    import sem_oracle
+    return (sem_oracle.PoissonProblem(nodes, e2n, gll["half_%d" % p], batched_geometry=True).apply(u),
+            sem_oracle.poisson_apply_extended(nodes, e2n, gll["half_%d" % p], u))
+
+
+@pytest.mark.parametrize("p,nex,ney,geometry", [(2, 40, 33, "auto"), (4, 30, 29, "auto"),
+                                                (6, 21, 17, "stored"), (8, 64, 48, "nodal"),
+                                                (8, 64, 48, "stored"), (12, 13, 11, "auto"),
+                                                (16, 9, 8, "auto")])
+def test_seams_match_colour_launches(gpu, gll, monkeypatch, p, nex, ney, geometry):
+    from spectralelementmethod_amd import meshgen
+    from spectralelementmethod_amd.operators import SEMOperator
+    nodes, e2n = meshgen.structured_square(nex, ney, p, warp=0.05)
+    u = np.random.default_rng(p).standard_normal(nodes.shape[1])
+    ut = torch.from_numpy(u).to(gpu)
+    monkeypatch.setenv("SEM_PLAN", "0")
+    monkeypatch.setenv("SEM_SEAM", "1")
+    ops = SEMOperator(p, e2n, nodes, device=gpu, kernel="column", geometry=geometry)
+    info = ops.plan_info()
+    assert info["plan"] == "chains-seams", info
+    assert info["seam_nodes"] > 0 and info["colours"] == 1
+    ys = ops.apply(ut)
+    monkeypatch.setenv("SEM_SEAM", "0")
+    opc = SEMOperator(p, e2n, nodes, device=gpu, kernel="column", geometry=geometry)
+    assert opc.plan_info()["plan"] == "chains"
+    yc = opc.apply(ut)
+    assert rel_l2(ys.cpu().numpy(), yc.cpu().numpy()) <= 1e-15
+    # accumulate: y0 + K u in both plans
+    y0 = torch.from_numpy(np.random.default_rng(3).standard_normal(nodes.shape[1])).to(gpu)
+    a_s, a_c = y0.clone(), y0.clone()
+    ops.apply(ut, out=a_s, accumulate=True)
+    opc.apply(ut, out=a_c, accumulate=True)
+    assert rel_l2(a_s.cpu().numpy(), a_c.cpu().numpy()) <= 1e-15
+    ref, ext = _oracle(gll, nodes, e2n, p, u)
+    y = ys.cpu().numpy()
+    if rel_l2(y, ref) >= TOL:  # p > 10: judge against extended precision
+        assert rel_l2(y, ext) <= max(1.5 * rel_l2(ref, ext), TOL)
+
+
+def test_seams_fall_back_on_irregular_meshes(gpu, gll, monkeypatch):
+    """Split-triangle quads: in-round sharing the chains cannot express; the
+    planner drops the seam plan (element-coloured chains or the atomic
+    fallback instead) and the action stays exact."""
+    import sem_oracle
+    from spectralelementmethod_amd import meshgen
+    from spectralelementmethod_amd.operators import SEMOperator
+    monkeypatch.setenv("SEM_SEAM", "1")
+    nodes, e2n = meshgen.quads_from_triangles(14, 11, 4, seed=3)
+    u = np.random.default_rng(1).standard_normal(nodes.shape[1])
+    op = SEMOperator(4, e2n, nodes, device=gpu)
+    assert op.plan_info()["plan"] != "chains-seams"
+    y = op.apply(torch.from_numpy(u).to(gpu)).cpu().numpy()
+    assert rel_l2(y, sem_oracle.PoissonProblem(nodes, e2n, gll["half_4"]).apply(u)) < TOL
+
+
+def test_seams_multirank_one_gpu(gpu, monkeypatch):
+    """The decomposition's interior and interface operators on the seam plan
+    (shared-output node states: interface nodes PRIOR for the interior
+    operator): the 2-rank action on one device equals the single-operator
+    action."""
+    import importlib
+    monkeypatch.setenv("SEM_SEAM", "1")
+    mr = importlib.import_module("test_gpu_multirank")
+    mr.test_overlapped_operator_ranks_on_one_gpu(gpu, 2, "strip", 8, 24, 20)
