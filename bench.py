@@ -453,7 +453,7 @@ def main():
             "gpu_setup_sec": t_setup, "gpu_setup_sec_per_elem": t_setup / max(1, n_elem_local),
             "scatter_plan": {k: plan[k] for k in ("plan", "colours", "chains_per_colour", "rounds",
                                                   "zero_list", "atomic_groups", "dependencies",
-                                                  "lag", "wait_timeouts")},
+                                                  "lag", "wait_timeouts", "seam_nodes")},
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -469,6 +469,9 @@ def main():
                        % (p + 1)),
             "launch": ("one sem_apply = one launch of %d chains (k_df_begin + the action)"
                        % plan["chains_per_colour"][0] if plan["plan"] == "chains-one-launch" else
+                       "one sem_apply = one launch of %d chains + k_seam_sum over %d seam nodes"
+                       % (plan["chains_per_colour"][0], plan["seam_nodes"])
+                       if plan["plan"] == "chains-seams" else
                        "one sem_apply = %d colour launches" % plan["colours"]) if world == 1 else
             "one sem_dd_apply (interface + interior elements + exchange), per rank",
             "fp64_tflops": F / kern_avg_s / 1e12, "fp64_peak_tflops": FP64_PEAK_TFLOPS,

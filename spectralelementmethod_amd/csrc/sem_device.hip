@@ -175,9 +175,20 @@ inline int grid_for(int64_t n, int per_block = BLOCK, int cap = 8192) {
 constexpr int MAX_COLOURS = 8;  // + one trailing all-atomic class
 // colour lag of the one-launch plan's ticket order, in chains (about two
 // generations of resident workgroups at p = 8: 4 per CU x 256 CUs)
-#ifndef SEM_SEAM_DEFAULT
-#define SEM_SEAM_DEFAULT 0
+// AUTO choice of the seam plan (Poisson column kernel), from the MI355X A/B
+// of profiles/r02/seams2 (ms per action, colour launches -> seams): it wins
+// where a colour launch is about one generation of resident workgroups or
+// less -- p = 16 198^2 0.164 -> 0.134, p = 12 263^2 0.139 -> 0.114, p = 8
+// 256^2 0.0635 -> 0.0477 -- and loses where the colour launches stream many
+// generations and the seams are a large share of the nodes: p = 8 1024^2
+// 0.640 -> 0.668, p = 6 527^2 0.118 -> 0.122, p = 4 790^2 0.113 -> 0.129,
+// p = 2 1581^2 0.132 -> 0.161.
+#ifndef SEM_SEAM_MAX_CHAINS
+#define SEM_SEAM_MAX_CHAINS 1024  // chains per colour at or below which seams win
 #endif
+bool seam_auto(int n, int64_t chains_per_colour) {
+  return n >= 11 || chains_per_colour <= SEM_SEAM_MAX_CHAINS;
+}
 #ifndef SEM_DF_LAG_DEFAULT
 #define SEM_DF_LAG_DEFAULT 2048
 #endif
@@ -568,7 +579,7 @@ struct Plan {
 // SEM_NODE_OTHER = another operator writes it (not zeroed when unreferenced).
 int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node, int n,
                int rounds, const std::vector<uint8_t>& node_state, Plan& P,
-               int64_t df_lag = 0, bool seam = false) {
+               int64_t df_lag = 0, int seam = 0) {
   const int epw = WAVE / n, lw = epw * n, nn = n * n;
   const int64_t n_groups = (n_elem + epw - 1) / epw;
   const int CW = chain_waves_of(n);  // groups of a chain that run concurrently
@@ -639,7 +650,12 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
   // one-launch plan the ticket order chain + colour * lag, or for the seam
   // plan element order in one launch
   std::vector<int64_t> order(n_chains);
-  P.seam = seam && conforming;
+  if (seam == 2) {  // AUTO (seam_auto): high orders, or colour classes below ~1 generation
+    std::vector<int64_t> per(MAX_COLOURS + 1, 0);
+    for (int64_t ch = 0; ch < n_chains; ++ch) per[colour[ch]]++;
+    seam = seam_auto(n, *std::max_element(per.begin(), per.end())) ? 1 : 0;
+  }
+  P.seam = seam == 1 && conforming;
   for (int64_t ch = 0; ch < n_chains && P.seam; ++ch)
     if (colour[ch] >= MAX_COLOURS) P.seam = false;
   P.df = !P.seam && df_lag > 0 && conforming && n_chains > 1;
@@ -1296,17 +1312,18 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
       df_lag = l ? std::max<int64_t>(1, std::atoll(l)) : SEM_DF_LAG_DEFAULT;
     }
   }
-  // seam plan (SEM_SEAM=1; Poisson contexts): one launch + seam sums
-  bool seam = false;
+  // seam plan (Poisson contexts): one launch + seam sums; SEM_SEAM=1 / 0
+  // forces / forbids it, default AUTO (seam_auto)
+  int seam = 0;
   if (!mfma && c->dpn == 1) {
     const char* e = std::getenv("SEM_SEAM");
-    seam = e ? std::atoi(e) == 1 : SEM_SEAM_DEFAULT;
+    seam = e ? (std::atoi(e) == 1 ? 1 : 0) : 2;
   }
   int rc = mfma ? build_plan_elem(h, c->n_elem, c->n_node, n, state, P)
                 : build_plan(h, c->n_elem, c->n_node, n, rounds, state, P, df_lag, seam);
   if (!rc && P.seam_failed) {
     P = Plan();
-    rc = build_plan(h, c->n_elem, c->n_node, n, rounds, state, P, df_lag, false);
+    rc = build_plan(h, c->n_elem, c->n_node, n, rounds, state, P, df_lag, 0);
   }
   if (rc) return rc;
   // element-coloured fallback for orders that defeat the chain patterns

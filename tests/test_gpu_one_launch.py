@@ -54,6 +54,7 @@ def test_one_launch_vs_colour_launches(gpu, gll, monkeypatch, p, nex, ney):
     u = np.random.default_rng(p).standard_normal(nodes.shape[1])
     ut = torch.from_numpy(u).to(gpu)
     monkeypatch.setenv("SEM_PLAN", "0")
+    monkeypatch.setenv("SEM_SEAM", "0")
     monkeypatch.setenv("SEM_DF", "1")
     monkeypatch.setenv("SEM_DF_LAG", "4")  # small mesh: a lag below the chain count
     op1 = SEMOperator(p, e2n, nodes, device=gpu, kernel="column")
@@ -83,6 +84,7 @@ def test_one_launch_lag_and_dispatch(gpu, gll, monkeypatch, lag, ticket, geometr
     p = 8
     nodes, e2n = _mesh(p, 128, 96)
     u = np.random.default_rng(11).standard_normal(nodes.shape[1])
+    monkeypatch.setenv("SEM_SEAM", "0")
     monkeypatch.setenv("SEM_DF", "1")
     monkeypatch.setenv("SEM_DF_LAG", str(lag))
     monkeypatch.setenv("SEM_DF_TICKET", ticket)
@@ -106,6 +108,7 @@ def test_one_launch_accumulate_and_graph_replay(gpu, gll, monkeypatch):
     from spectralelementmethod_amd.operators import SEMOperator
     p = 6
     nodes, e2n = _mesh(p, 48, 40)
+    monkeypatch.setenv("SEM_SEAM", "0")
     monkeypatch.setenv("SEM_DF", "1")
     op = SEMOperator(p, e2n, nodes, device=gpu)
     assert op.plan_info()["plan"] == "chains-one-launch"

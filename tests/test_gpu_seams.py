@@ -32,10 +32,12 @@ def _oracle(gll, nodes, e2n, p, u):
             sem_oracle.poisson_apply_extended(nodes, e2n, gll["half_%d" % p], u))
 
 
-@pytest.mark.parametrize("p,nex,ney,geometry", [(2, 40, 33, "auto"), (4, 30, 29, "auto"),
-                                                (6, 21, 17, "stored"), (8, 64, 48, "nodal"),
-                                                (8, 64, 48, "stored"), (12, 13, 11, "auto"),
-                                                (16, 9, 8, "auto")])
+# ney = whole chains per element column (chains that wrap into the next
+# column share nodes irregularly: atomic chains, and no seam plan)
+@pytest.mark.parametrize("p,nex,ney,geometry", [(2, 7, 168, "auto"), (4, 9, 96, "auto"),
+                                                (6, 8, 72, "stored"), (8, 17, 112, "nodal"),
+                                                (8, 17, 112, "stored"), (12, 9, 32, "auto"),
+                                                (16, 7, 12, "auto")])
 def test_seams_match_colour_launches(gpu, gll, monkeypatch, p, nex, ney, geometry):
     from spectralelementmethod_amd import meshgen
     from spectralelementmethod_amd.operators import SEMOperator
