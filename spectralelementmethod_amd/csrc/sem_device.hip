@@ -176,18 +176,20 @@ constexpr int MAX_COLOURS = 8;  // + one trailing all-atomic class
 // colour lag of the one-launch plan's ticket order, in chains (about two
 // generations of resident workgroups at p = 8: 4 per CU x 256 CUs)
 // AUTO choice of the seam plan (Poisson column kernel), from the MI355X A/B
-// of profiles/r02/seams2 (ms per action, colour launches -> seams): it wins
-// where a colour launch is about one generation of resident workgroups or
-// less -- p = 16 198^2 0.164 -> 0.134, p = 12 263^2 0.139 -> 0.114, p = 8
-// 256^2 0.0635 -> 0.0477 -- and loses where the colour launches stream many
-// generations and the seams are a large share of the nodes: p = 8 1024^2
-// 0.640 -> 0.668, p = 6 527^2 0.118 -> 0.122, p = 4 790^2 0.113 -> 0.129,
-// p = 2 1581^2 0.132 -> 0.161.
-#ifndef SEM_SEAM_MAX_CHAINS
-#define SEM_SEAM_MAX_CHAINS 1024  // chains per colour at or below which seams win
-#endif
+// of profiles/r02/seams2 (ms per action, colour launches -> seams; cpc =
+// chains per colour): it wins where a colour launch is a few generations of
+// resident workgroups or less -- p = 16 198^2 (cpc 1,633) 0.164 -> 0.134,
+// p = 12 263^2 0.139 -> 0.114, p = 10 316^2 (1,296) 0.158 -> 0.128, p = 9
+// 351^2 (1,297) 0.120 -> 0.113, p = 8 512^2 (2,342) 0.185 -> 0.179, 384^2
+// (1,372) 0.107 -> 0.095, 128 x 1024 (1,171; one rank's strip of the
+// 8-GPU split) 0.098 -> 0.089, 256^2 (585) 0.0635 -> 0.0477, p = 6 256^2
+// (488) 0.040 -> 0.030, p = 4 395^2 (815) 0.045 -> 0.036 -- and loses where
+// the colour launches stream many generations and the seams are a large
+// share of the nodes: p = 8 1024^2 (9,365) 0.640 -> 0.668, p = 6 527^2
+// (1,928) 0.118 -> 0.122, p = 4 790^2 (3,250) 0.113 -> 0.129, p = 2 1581^2
+// 0.132 -> 0.161.
 bool seam_auto(int n, int64_t chains_per_colour) {
-  return n >= 11 || chains_per_colour <= SEM_SEAM_MAX_CHAINS;
+  return n >= 11 || chains_per_colour <= 1024 || (n >= 9 && chains_per_colour <= 2400);
 }
 #ifndef SEM_DF_LAG_DEFAULT
 #define SEM_DF_LAG_DEFAULT 2048
