@@ -326,13 +326,14 @@ bool nodal_mode(const sem_ctx* c) {
 
 // AUTO: the MFMA element kernel from SEM_MFMA_MIN_N nodes per line up,
 // Poisson only (dpn = 1), one 16 x 16 tile (n <= 16), and not when nodal
-// geometry was requested explicitly.  Measured on MI355X at ~1e7 DOF
-// (profiles/r01/mfma_v2, profiles/r01c/geosweep): after the
-// column kernel's latency work (4 waves, RMW prefetch, 16-bit map) it wins
-// up to p = 12 (0.139 vs 0.155 ms), the MFMA kernel from p = 13 (n = 14)
-// to p = 15.
+// geometry was requested explicitly.  Round 1 measured it ahead of the
+// column kernel on colour launches at p = 13..15 (profiles/r01c/geosweep);
+// the column kernel on the seam plan is ahead at every order (MI355X, ~1e7
+// DOF, ms per action, MFMA / column: p = 10 0.160 / 0.126, p = 13 0.147 /
+// 0.129, p = 14 0.143 / 0.141, p = 15 0.142 / 0.112; profiles/r02/final),
+// so AUTO no longer picks it (SEM_KERNEL_MFMA still does).
 #ifndef SEM_MFMA_MIN_N
-#define SEM_MFMA_MIN_N 14
+#define SEM_MFMA_MIN_N 17
 #endif
 bool want_mfma(const sem_ctx* c) {
   if (c->dpn != 1 || c->n > 16) return false;
@@ -423,10 +424,20 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
   if (c->seam && op_kind == SEM_OP_POISSON) {  // one launch + the seam sums (SeamPlan)
     launch_chains<N, false, true>(c, op_kind, nodal, u, y, acc, lin, c->colour_start.front(),
                                   c->colour_start.back(), D, w, DFPlan{}, st);
-    if (c->n_seam)
-      hipLaunchKernelGGL(k_seam_sum, dim3(grid_for(c->n_seam)), dim3(BLOCK), 0, st, y,
-                         c->d_seam_gid, c->d_seam_mask, c->n_seam, c->d_seam_buf, c->n_node,
-                         c->seam_ns, acc);
+    if (c->n_seam) {
+      const dim3 g(grid_for(c->n_seam)), b(BLOCK);
+      switch (c->seam_ns) {
+#define SEAM_NS(K)                                                                           \
+  case K:                                                                                  \
+    hipLaunchKernelGGL(k_seam_sum<K>, g, b, 0, st, y, c->d_seam_gid, c->d_seam_mask,       \
+                       c->n_seam, c->d_seam_buf, c->n_node, acc);                          \
+    break;
+        SEAM_NS(1) SEAM_NS(2) SEAM_NS(3) SEAM_NS(4) SEAM_NS(5) SEAM_NS(6) SEAM_NS(7) SEAM_NS(8)
+#undef SEAM_NS
+        default:
+          return fail(SEM_E_STATE, "seam plan with more than 8 colours");
+      }
+    }
     return SEM_OK;
   }
   if (c->df) {  // every chain in one launch (DFPlan, sem_kernels.h)

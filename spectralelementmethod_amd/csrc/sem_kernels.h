@@ -1046,20 +1046,34 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
 // order (the order of the colour launches' read-modify-writes: the same
 // rounding).  mask bits 0-7: colours that wrote the node; bit 8: y already
 // holds a value (SEM_NODE_PRIOR)
+// NS colours: the slot loads of a node are issued together (predicated
+// buffer loads: an unused slot reads past the range, 0 and no traffic).
+template <int NS>
 __global__ void k_seam_sum(double* __restrict__ y, const uint32_t* __restrict__ gid,
                            const uint16_t* __restrict__ mask, int64_t n,
-                           const double* __restrict__ buf, int64_t n_node, int ns,
-                           int accumulate) {
+                           const double* __restrict__ buf, int64_t n_node, int accumulate) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t g = gid[i];
     const uint32_t m = mask[i];
-    double s = (accumulate || (m & 0x100u)) ? y[g] : 0.0;
-    bool first = !(accumulate || (m & 0x100u));
-    for (int c = 0; c < ns; ++c)
+    const bool prior = accumulate || (m & 0x100u);
+    const double y0 = prior ? y[g] : 0.0;
+    double b[NS];
+#pragma unroll
+    for (int c = 0; c < NS; ++c) {
+      // one buffer resource per colour plane (each < 2^31 bytes: n_node < 2^28)
+      const __amdgpu_buffer_rsrc_t rb =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(buf + c * n_node), 0, 0x80000000,
+                                            0x00020000);
+      const uint32_t off = (m & (1u << c)) ? g * 8u : 0x80000000u;
+      b[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rb, off, 0, CPOL_NT));
+    }
+    double s = y0;
+    bool first = !prior;
+#pragma unroll
+    for (int c = 0; c < NS; ++c)
       if (m & (1u << c)) {
-        const double b = __builtin_nontemporal_load(buf + c * n_node + g);
-        s = first ? b : s + b;
+        s = first ? b[c] : s + b[c];
         first = false;
       }
     y[g] = s;
