@@ -139,8 +139,16 @@ int sem_set_map_shared(sem_ctx* ctx, const uint32_t* d_e2n, const uint8_t* d_nod
  * chains from a ticket counter, and a chain starts once every chain that
  * wrote one of its shared nodes earlier in ticket order has published
  * (per-chain flags); [5] is then 1 and [8] the chain count.
+ * 4 the seam plan (Poisson, dofs_per_node == 1; AUTO where a colour launch
+ * would be about one generation of resident workgroups or less -- p >= 10,
+ * or few chains per colour; SEM_SEAM=1 / 0 forces / forbids):
+ * all chains in one launch in element order, nodes written by several
+ * chains stored per writer colour and summed in colour order by a second
+ * launch, bitwise equal to the colour launches; [5] is then 1 and [8] the
+ * chain count.
  * [21] the axisymmetric Stokes geometry mode (as [19]; 0 when
- * dofs_per_node != 2).  [22] dependency edges of the one-launch plan, [23]
+ * dofs_per_node != 2).  [22] seam nodes of the seam plan, or dependency
+ * edges of the one-launch plan, [23]
  * its colour lag in chains (SEM_DF_LAG), [24] dependency waits that hit
  * their spin limit since sem_set_map (never expected; read from the device,
  * so a request for 25 values synchronises with it).  Writes min(n_info, 25)
@@ -185,9 +193,9 @@ int sem_set_geom_mode(sem_ctx* ctx, int mode);
  *    element-level colouring; stored factors, or x_phys per node when
  *    SEM_GEOM_NODAL is requested; n = p + 1 <= 16 and dpn = 1, else
  *    SEM_E_NOTIMPL.
- *  SEM_KERNEL_AUTO (default): MFMA for 13 <= p <= 15 unless NODAL geometry
- *    was requested, COLUMN otherwise (measured on MI355X, DESIGN.md §4.6;
- *    the threshold SEM_MFMA_MIN_N is a build knob).
+ *  SEM_KERNEL_AUTO (default): COLUMN -- on its seam plan it measured ahead
+ *    of MFMA at every order on MI355X; the build knob
+ *    SEM_MFMA_MIN_N (default 17: never) restores an MFMA range.
  * The environment variable SEM_KERNEL (0/1/2) sets the initial value. */
 #define SEM_KERNEL_COLUMN 0
 #define SEM_KERNEL_MFMA 1

@@ -41,15 +41,16 @@ namespace semk {
 
 constexpr int WAVE = 64;
 constexpr int BLOCK = 256;
-// Groups per chain round = wavefronts per workgroup, per order: 4, and 2 at
-// n = 17 where a colour launch of the 4-wave form leaves the chip
-// under-filled (p = 16 at 1e7 DOF: 0.165 against 0.173 ms,
-// profiles/r02/variants).  SEM_CHAIN_WAVES (diagnostic builds) forces one
-// value for every order.
+// Groups per chain round = wavefronts per workgroup: 4.  At n = 17 the
+// colour launches ran faster with 2-wave chains (p = 16 at 1e7 DOF: 0.165
+// against 0.173 ms, profiles/r02/variants), but AUTO takes the seam plan
+// there (one launch), on which 4-wave chains are ahead: 0.131
+// against 0.136 ms (profiles/r02/final/chain_width).  SEM_CHAIN_WAVES
+// (diagnostic builds) forces one value for every order.
 #ifdef SEM_CHAIN_WAVES
 constexpr int chain_waves_of(int) { return SEM_CHAIN_WAVES; }
 #else
-constexpr int chain_waves_of(int n) { return n >= 17 ? 2 : 4; }
+constexpr int chain_waves_of(int) { return 4; }
 #endif
 template <int N>
 struct ChainWaves {

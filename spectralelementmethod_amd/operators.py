@@ -97,8 +97,8 @@ class SEMOperator(object):
     kernel : {"auto", "column", "mfma"}
         Kernel family of the Poisson action: the LDS column kernel or the
         fp64 matrix-core element kernel (p <= 15); "auto" (default) resolves
-        to the library's measured choice (mfma for 13 <= p <= 15 unless nodal
-        geometry is requested).  See include/sem_hip.h
+        to the library's measured choice (the column kernel: on its seam
+        plan it is ahead of mfma at every order).  See include/sem_hip.h
         sem_set_kernel.
     node_state : array-like uint8 [n_node], optional
         For operators that share the output vector with others applied
