@@ -389,28 +389,29 @@ void launch_chains(sem_ctx* c, int op_kind, bool nodal, const double* u, double*
     else
       hipLaunchKernelGGL((k_poisson_apply<N, false, false, DF, SEAM>), g, b, 0, st, mr, GP, XG,
                          u, y, c0, c1, R, acc, D, w, df, sp);
-  } else if constexpr (SEAM) {
-    // Poisson only (the seam plan is built for dpn = 1 contexts)
   } else if (op_kind == SEM_OP_AXISYM_STOKES && nodal) {
+    const SeamPlan sp{c->d_ccol, c->d_seam_buf, c->n_node};
     if (c->map16)
-      hipLaunchKernelGGL((k_axisym_nodal<N, true, DF>), g, b, 0, st, mr, c->d_XG, u, y, c0, c1, R,
-                         acc, D, w, df);
+      hipLaunchKernelGGL((k_axisym_nodal<N, true, DF, SEAM>), g, b, 0, st, mr, c->d_XG, u, y, c0,
+                         c1, R, acc, D, w, df, sp);
     else
-      hipLaunchKernelGGL((k_axisym_nodal<N, false, DF>), g, b, 0, st, mr, c->d_XG, u, y, c0, c1,
-                         R, acc, D, w, df);
+      hipLaunchKernelGGL((k_axisym_nodal<N, false, DF, SEAM>), g, b, 0, st, mr, c->d_XG, u, y, c0,
+                         c1, R, acc, D, w, df, sp);
   } else if (op_kind == SEM_OP_AXISYM_STOKES) {
-    hipLaunchKernelGGL((k_axisym_apply<N, 0, DF>), g, b, 0, st, c->d_mapP, c->d_GP[1], u, y, c0,
-                       c1, R, acc, D, w, AxiNS(), df);
+    const SeamPlan sp{c->d_ccol, c->d_seam_buf, c->n_node};
+    hipLaunchKernelGGL((k_axisym_apply<N, 0, DF, SEAM>), g, b, 0, st, c->d_mapP, c->d_GP[1], u, y,
+                       c0, c1, R, acc, D, w, AxiNS(), df, sp);
   } else {
+    const SeamPlan sp{c->d_ccol, c->d_seam_buf, c->n_node};
     AxiNS ns;
     ns.re = c->reynolds;
     ns.lin = (op_kind == SEM_OP_AXISYM_NS_JVP || lin) ? c->d_lin : nullptr;
     if (op_kind == SEM_OP_AXISYM_NS)
-      hipLaunchKernelGGL((k_axisym_apply<N, 1, DF>), g, b, 0, st, c->d_mapP, c->d_GP[2], u, y, c0,
-                         c1, R, acc, D, w, ns, df);
+      hipLaunchKernelGGL((k_axisym_apply<N, 1, DF, SEAM>), g, b, 0, st, c->d_mapP, c->d_GP[2], u,
+                         y, c0, c1, R, acc, D, w, ns, df, sp);
     else
-      hipLaunchKernelGGL((k_axisym_apply<N, 2, DF>), g, b, 0, st, c->d_mapP, c->d_GP[2], u, y, c0,
-                         c1, R, acc, D, w, ns, df);
+      hipLaunchKernelGGL((k_axisym_apply<N, 2, DF, SEAM>), g, b, 0, st, c->d_mapP, c->d_GP[2], u,
+                         y, c0, c1, R, acc, D, w, ns, df, sp);
   }
 }
 
@@ -421,7 +422,7 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
   WVec<N> w;
   std::memcpy(w.v, c->hw, sizeof(w.v));
   const bool nodal = use_nodal(c, op_kind);
-  if (c->seam && op_kind == SEM_OP_POISSON) {  // one launch + the seam sums (SeamPlan)
+  if (c->seam) {  // one launch + the seam sums (SeamPlan)
     launch_chains<N, false, true>(c, op_kind, nodal, u, y, acc, lin, c->colour_start.front(),
                                   c->colour_start.back(), D, w, DFPlan{}, st);
     if (c->n_seam) {
@@ -429,8 +430,12 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
       switch (c->seam_ns) {
 #define SEAM_NS(K)                                                                           \
   case K:                                                                                  \
-    hipLaunchKernelGGL(k_seam_sum<K>, g, b, 0, st, y, c->d_seam_gid, c->d_seam_mask,       \
-                       c->n_seam, c->d_seam_buf, c->n_node, acc);                          \
+    if (c->dpn == 2)                                                                       \
+      hipLaunchKernelGGL(k_seam_sum2<K>, g, b, 0, st, y, c->d_seam_gid, c->d_seam_mask,    \
+                         c->n_seam, c->d_seam_buf, c->n_node, acc);                        \
+    else                                                                                   \
+      hipLaunchKernelGGL(k_seam_sum<K>, g, b, 0, st, y, c->d_seam_gid, c->d_seam_mask,     \
+                         c->n_seam, c->d_seam_buf, c->n_node, acc);                        \
     break;
         SEAM_NS(1) SEAM_NS(2) SEAM_NS(3) SEAM_NS(4) SEAM_NS(5) SEAM_NS(6) SEAM_NS(7) SEAM_NS(8)
 #undef SEAM_NS
@@ -1325,12 +1330,15 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
       df_lag = l ? std::max<int64_t>(1, std::atoll(l)) : SEM_DF_LAG_DEFAULT;
     }
   }
-  // seam plan (Poisson contexts): one launch + seam sums; SEM_SEAM=1 / 0
-  // forces / forbids it, default AUTO (seam_auto)
+  // seam plan: one launch + seam sums; SEM_SEAM=1 / 0 forces / forbids it;
+  // default AUTO (seam_auto) for Poisson contexts.  Two DOFs per node
+  // (axisymmetric kernels) only when forced: the nodal axisymmetric kernel's
+  // seam instantiation drops to 1 wave per SIMD (2 on the colour plan), and
+  // its BASELINE size (cfg5, 512^2) has too many chains per colour to gain
   int seam = 0;
-  if (!mfma && c->dpn == 1) {
+  if (!mfma) {
     const char* e = std::getenv("SEM_SEAM");
-    seam = e ? (std::atoi(e) == 1 ? 1 : 0) : 2;
+    seam = e ? (std::atoi(e) == 1 ? 1 : 0) : (c->dpn == 1 ? 2 : 0);
   }
   int rc = mfma ? build_plan_elem(h, c->n_elem, c->n_node, n, state, P)
                 : build_plan(h, c->n_elem, c->n_node, n, rounds, state, P, df_lag, seam);
@@ -1458,7 +1466,8 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
       HIP_TRY(hipMemcpy(c->d_seam_mask, P.seam_mask.data(), c->n_seam * sizeof(uint16_t),
                         hipMemcpyHostToDevice));
       // slots addressed by node id (only seam nodes' slots are touched)
-      HIP_TRY(hipMalloc(&c->d_seam_buf, (size_t)c->n_node * c->seam_ns * sizeof(double)));
+      HIP_TRY(hipMalloc(&c->d_seam_buf,
+                        (size_t)c->n_node * c->seam_ns * c->dpn * sizeof(double)));
     }
   }
   c->n_atomic_groups = P.n_atomic_groups;

@@ -344,7 +344,7 @@ __device__ __forceinline__ void emit1p(double* __restrict__ y, uint32_t raw, dou
 // between chains.  The code action 3 (W_ATOMIC) means "seam slot" in this
 // plan (the plan has no atomic chains).
 struct SeamOut {
-  double* base = nullptr;  // buf + colour * n_node of the chain
+  double* base = nullptr;  // buf + colour * n_node * dpn of the chain
 };
 __device__ __forceinline__ void emit1_seam(double* __restrict__ y, uint32_t raw, double v,
                                            int accumulate, const SeamOut& so) {
@@ -945,6 +945,9 @@ __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_
         emit1(y, raw[p], v[0][p], accumulate);
       else if (DF)
         emit2_df(y, raw[p], v[0][p], v[NC - 1][p], accumulate);
+      else if (SEAM && ((raw[p] >> CODE_SHIFT) & 3u) == W_ATOMIC)  // seam slot (2 DOFs)
+        reinterpret_cast<double2*>(so.base)[raw[p] & GID_MASK] =
+            make_double2(v[0][p], v[NC - 1][p]);
       else
         emit2(y, raw[p], v[0][p], v[NC - 1][p], accumulate);
     }
@@ -1049,6 +1052,34 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
 // holds a value (SEM_NODE_PRIOR)
 // NS colours: the slot loads of a node are issued together (predicated
 // buffer loads: an unused slot reads past the range, 0 and no traffic).
+template <int NS>
+__global__ void k_seam_sum(double* __restrict__ y, const uint32_t* __restrict__ gid,
+                           const uint16_t* __restrict__ mask, int64_t n,
+                           const double* __restrict__ buf, int64_t n_node, int accumulate);
+
+// two DOFs per node (axisymmetric block): slots are double2, buf[colour][node]
+template <int NS>
+__global__ void k_seam_sum2(double* __restrict__ y, const uint32_t* __restrict__ gid,
+                            const uint16_t* __restrict__ mask, int64_t n,
+                            const double* __restrict__ buf, int64_t n_node, int accumulate) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t g = gid[i];
+    const uint32_t m = mask[i];
+    const bool prior = accumulate || (m & 0x100u);
+    double2 s = prior ? reinterpret_cast<const double2*>(y)[g] : make_double2(0.0, 0.0);
+    bool first = !prior;
+#pragma unroll
+    for (int c = 0; c < NS; ++c)
+      if (m & (1u << c)) {
+        const double2 b = reinterpret_cast<const double2*>(buf + 2 * c * n_node)[g];
+        s = first ? b : make_double2(s.x + b.x, s.y + b.y);
+        first = false;
+      }
+    reinterpret_cast<double2*>(y)[g] = s;
+  }
+}
+
 template <int NS>
 __global__ void k_seam_sum(double* __restrict__ y, const uint32_t* __restrict__ gid,
                            const uint16_t* __restrict__ mask, int64_t n,
@@ -1411,11 +1442,11 @@ __device__ __forceinline__ void axisym_group_nodal(const MapRef& mref,
   wave_sync();
 }
 
-template <int N, bool M16, bool DF = false>
+template <int N, bool M16, bool DF = false, bool SEAM = false>
 __global__ void __launch_bounds__(ChainWaves<N>::block, SEM_AXI_MIN_WAVES)
     k_axisym_nodal(const MapRef mref, const double2* __restrict__ XG, const double* __restrict__ u,
                    double* __restrict__ y, int64_t c0, int64_t c1, int rounds, int accumulate,
-                   const DEO<N> D, const WVec<N> w, const DFPlan df) {
+                   const DEO<N> D, const WVec<N> w, const DFPlan df, const SeamPlan sp) {
   using T = Tile<N>;
   __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * 2 * T::ES];
   constexpr int CW = ChainWaves<N>::value;
@@ -1437,17 +1468,20 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, SEM_AXI_MIN_WAVES)
     double v[2][N];  // [0] omega row (y[2k]), [1] psi row (y[2k+1])
     axisym_group_nodal<N, M16>(mref, XG, u, g, lane, j, in_wave, LP, LO, D, w, wj, raw, v[0],
                                v[1]);
-    chain_emit<N, 2, false, CW, DF>(y, raw, v, lane, wave, rd, in_wave, carry, accumulate);
+    SeamOut so;
+    if constexpr (SEAM) so.base = sp.buf + sp.colour[chain] * sp.n_node * 2;
+    chain_emit<N, 2, false, CW, DF, SEAM>(y, raw, v, lane, wave, rd, in_wave, carry, accumulate,
+                                          nullptr, so);
   }
   if constexpr (DF) df_publish(df, c0, sdf);
 }
 
-template <int N, int MODE, bool DF = false>
+template <int N, int MODE, bool DF = false, bool SEAM = false>
 __global__ void __launch_bounds__(ChainWaves<N>::block)
     k_axisym_apply(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
                    const double* __restrict__ u, double* __restrict__ y, int64_t c0, int64_t c1,
                    int rounds, int accumulate, const DEO<N> D, const WVec<N> w, const AxiNS ns,
-                   const DFPlan df) {
+                   const DFPlan df, const SeamPlan sp) {
   using T = Tile<N>;
   __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * 2 * T::ES];
   constexpr int CW = ChainWaves<N>::value;
@@ -1469,7 +1503,10 @@ __global__ void __launch_bounds__(ChainWaves<N>::block)
     double v[2][N];  // [0] omega row (y[2k]), [1] psi row (y[2k+1])
     axisym_group<N, MODE>(mapP, GP, u, g, lane, j, in_wave, LP, LO, D, w, wj, ns, raw, v[0],
                           v[1]);
-    chain_emit<N, 2, false, CW, DF>(y, raw, v, lane, wave, rd, in_wave, carry, accumulate);
+    SeamOut so;
+    if constexpr (SEAM) so.base = sp.buf + sp.colour[chain] * sp.n_node * 2;
+    chain_emit<N, 2, false, CW, DF, SEAM>(y, raw, v, lane, wave, rd, in_wave, carry, accumulate,
+                                          nullptr, so);
   }
   if constexpr (DF) df_publish(df, c0, sdf);
 }

@@ -154,6 +154,7 @@ def test_one_launch_axisymmetric(gpu, gll, monkeypatch, geometry):
     sol = torch.from_numpy(rng.standard_normal(2 * nodes.shape[1])).to(gpu)
     dirn = torch.from_numpy(rng.standard_normal(2 * nodes.shape[1])).to(gpu)
     monkeypatch.setenv("SEM_DF_LAG", "8")
+    monkeypatch.setenv("SEM_SEAM", "0")
     out = {}
     for df in ("1", "0"):
         monkeypatch.setenv("SEM_DF", df)
