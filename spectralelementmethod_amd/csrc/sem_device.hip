@@ -188,7 +188,12 @@ constexpr int MAX_COLOURS = 8;  // + one trailing all-atomic class
 // share of the nodes: p = 8 1024^2 (9,365) 0.640 -> 0.668, p = 6 527^2
 // (1,928) 0.118 -> 0.122, p = 4 790^2 (3,250) 0.113 -> 0.129, p = 2 1581^2
 // 0.132 -> 0.161.
-bool seam_auto(int n, int64_t chains_per_colour) {
+// Two DOFs per node (axisymmetric block, p = 6, profiles/r02/final/
+// axisym_seams): 128^2 (cpc 114) 0.0441 -> 0.0236, 512^2 (cpc 1,820) 0.227
+// -> 0.274 (the nodal kernel's seam instantiation runs 1 wave per SIMD
+// instead of 2).
+bool seam_auto(int n, int64_t chains_per_colour, int dpn = 1) {
+  if (dpn == 2) return chains_per_colour <= 512;
   return n >= 11 || chains_per_colour <= 1024 || (n >= 9 && chains_per_colour <= 2400);
 }
 #ifndef SEM_DF_LAG_DEFAULT
@@ -597,7 +602,7 @@ struct Plan {
 // SEM_NODE_OTHER = another operator writes it (not zeroed when unreferenced).
 int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node, int n,
                int rounds, const std::vector<uint8_t>& node_state, Plan& P,
-               int64_t df_lag = 0, int seam = 0) {
+               int64_t df_lag = 0, int seam = 0, int seam_dpn = 1) {
   const int epw = WAVE / n, lw = epw * n, nn = n * n;
   const int64_t n_groups = (n_elem + epw - 1) / epw;
   const int CW = chain_waves_of(n);  // groups of a chain that run concurrently
@@ -671,7 +676,7 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
   if (seam == 2) {  // AUTO (seam_auto): high orders, or colour classes below ~1 generation
     std::vector<int64_t> per(MAX_COLOURS + 1, 0);
     for (int64_t ch = 0; ch < n_chains; ++ch) per[colour[ch]]++;
-    seam = seam_auto(n, *std::max_element(per.begin(), per.end())) ? 1 : 0;
+    seam = seam_auto(n, *std::max_element(per.begin(), per.end()), seam_dpn) ? 1 : 0;
   }
   P.seam = seam == 1 && conforming;
   for (int64_t ch = 0; ch < n_chains && P.seam; ++ch)
@@ -1331,17 +1336,14 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
     }
   }
   // seam plan: one launch + seam sums; SEM_SEAM=1 / 0 forces / forbids it;
-  // default AUTO (seam_auto) for Poisson contexts.  Two DOFs per node
-  // (axisymmetric kernels) only when forced: the nodal axisymmetric kernel's
-  // seam instantiation drops to 1 wave per SIMD (2 on the colour plan), and
-  // its BASELINE size (cfg5, 512^2) has too many chains per colour to gain
+  // default AUTO (seam_auto, per dofs per node)
   int seam = 0;
   if (!mfma) {
     const char* e = std::getenv("SEM_SEAM");
-    seam = e ? (std::atoi(e) == 1 ? 1 : 0) : (c->dpn == 1 ? 2 : 0);
+    seam = e ? (std::atoi(e) == 1 ? 1 : 0) : 2;
   }
   int rc = mfma ? build_plan_elem(h, c->n_elem, c->n_node, n, state, P)
-                : build_plan(h, c->n_elem, c->n_node, n, rounds, state, P, df_lag, seam);
+                : build_plan(h, c->n_elem, c->n_node, n, rounds, state, P, df_lag, seam, c->dpn);
   if (!rc && P.seam_failed) {
     P = Plan();
     rc = build_plan(h, c->n_elem, c->n_node, n, rounds, state, P, df_lag, 0);
