@@ -43,8 +43,11 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FP64_PEAK_TFLOPS = 78.6  # MI355X vector fp64 (256 CUs x 128 FLOP/clk x 2.4 GHz)
 # PMC-measured HBM bytes of the headline workload (tools/gpu_profile.sh +
 # tools/pmc_traffic.py), per geometry mode
-DEFAULT_TRAFFIC = {"stored": "r01/pmc_traffic_p8_1024x1024.json",
-                   "nodal": "r02/pmc_traffic_nodal_p8_1024x1024.json"}
+# (copies of profiles/r01/pmc_traffic_p8_1024x1024.json and
+# profiles/r02/pmc_traffic_nodal_p8_1024x1024.json in bench_traffic/, which
+# travels to the GPU box; profiles/ does not)
+DEFAULT_TRAFFIC = {"stored": "pmc_traffic_stored_p8_1024x1024.json",
+                   "nodal": "pmc_traffic_nodal_p8_1024x1024.json"}
 
 
 def log(msg):
@@ -413,7 +416,7 @@ def main():
     traffic, traffic_src = None, args.traffic_json
     if (traffic_src is None and kind == POISSON and plan["kernel"] == "column" and world == 1
             and (p, args.nex, args.ney) == (8, 1024, 1024)):
-        traffic_src = os.path.join(ROOT, "profiles", DEFAULT_TRAFFIC[geometry])
+        traffic_src = os.path.join(ROOT, "bench_traffic", DEFAULT_TRAFFIC[geometry])
     if traffic_src and os.path.exists(traffic_src):
         with open(traffic_src) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
