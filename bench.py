@@ -201,9 +201,14 @@ def _free_port():
     return port
 
 
-def launch_ranks(n):
-    """Start n rank processes of this script (before any GPU call here) and
-    wait for them; rank 0 prints the JSON line."""
+def launch_ranks(n, deadline_s):
+    """Start n rank processes of this script (before any GPU call here), each
+    in its own process group, and watch them: the first rank that exits
+    non-zero (RCCL init, OOM, a bad partition) or the deadline ends the run --
+    the others are killed (they would otherwise wait in a collective for a
+    peer that is gone) and the launcher returns non-zero within seconds.
+    Rank 0 prints the JSON line."""
+    import signal
     port = _free_port()
     procs = []
     for r in range(n):
@@ -211,11 +216,45 @@ def launch_ranks(n):
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
-                                      env=env))
-    rc = 0
-    for pr in procs:
-        rc = max(rc, abs(pr.wait()))
-    return rc
+                                      env=env, start_new_session=True))
+
+    def kill_all():
+        for pr in procs:
+            if pr.poll() is None:
+                try:
+                    os.killpg(pr.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+        for pr in procs:
+            pr.wait()
+
+    t_end = time.monotonic() + deadline_s
+    while True:
+        codes = [pr.poll() for pr in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad:
+            log("rank %d exited with status %d: stopping the other ranks" % bad[0])
+            kill_all()
+            return 1
+        if all(c == 0 for c in codes):
+            return 0
+        if time.monotonic() > t_end:
+            log("deadline of %.0f s reached: stopping all ranks" % deadline_s)
+            kill_all()
+            return 124
+        time.sleep(0.2)
+
+
+def _inject_failure(rank):
+    """Test hook (tests/test_bench_launcher.py): SEM_BENCH_INJECT=fail:<r>
+    makes rank r exit with status 3 at start-up and every other rank wait as
+    if blocked in a collective on the missing peer."""
+    spec = os.environ.get("SEM_BENCH_INJECT", "")
+    if spec.startswith("fail:"):
+        if rank == int(spec[5:]):
+            log("rank %d: injected failure" % rank)
+            sys.exit(3)
+        time.sleep(3600)
 
 
 # ---------------------------------------------------------------- parity spot check
@@ -234,15 +273,29 @@ def parity_spot_check(op, y, u, part, p, warp, cols=2):
     nodes, e2n, off = meshgen.structured_strip(part.nex, part.ney, p, c0, c0 + cols, warp)
     loc = off - part.node_offset + np.arange(nodes.shape[1])
     u_sub = u[torch_index(loc, u.device)].cpu().numpy()
-    y_ref = sem_oracle.PoissonProblem(nodes, e2n, gll["half_%d" % p],
-                                      batched_geometry=True).apply(u_sub)
+    half = gll["half_%d" % p]
+    y_ref = sem_oracle.PoissonProblem(nodes, e2n, half, batched_geometry=True).apply(u_sub)
     Ny = part.Ny
     inner = np.arange(Ny, nodes.shape[1] - Ny)
     y_gpu = y[torch_index(loc[inner], y.device)].cpu().numpy()
     ref = y_ref[inner]
-    return dict(rel_l2=float(np.linalg.norm(y_gpu - ref) / np.linalg.norm(ref)),
-                nodes_checked=int(inner.size),
-                block="element columns [%d, %d) x %d rows" % (c0, c0 + cols, part.ney))
+
+    def rel(a, b):
+        return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+    out = dict(rel_l2=rel(y_gpu, ref), nodes_checked=int(inner.size),
+               block="element columns [%d, %d) x %d rows" % (c0, c0 + cols, part.ney),
+               against="float64 NumPy oracle of the reference path")
+    if p > 10:
+        # above p = 10 the reference's own float64 geometry (equispaced->GLL
+        # transform, cond(V_eq) 1e3..1e5) is the inaccurate side (DESIGN.md
+        # §6): the criterion is the extended-precision evaluation of the same
+        # action from the same float64 inputs, at the same 1e-10
+        ext = np.asarray(sem_oracle.poisson_apply_extended(nodes, e2n, half, u_sub),
+                         dtype=np.float64)[inner]
+        out.update(rel_l2_float64_oracle=out["rel_l2"], rel_l2=rel(y_gpu, ext),
+                   oracle_float64_vs_extended=rel(ref, ext),
+                   against="extended-precision oracle (poisson_apply_extended)")
+    return out
 
 
 def torch_index(a, device):
@@ -284,6 +337,9 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--cpu-workers", type=int, default=16)
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--deadline", type=float, default=900.0,
+                    help="seconds: the whole multi-rank run (launcher kills every rank after it) "
+                         "and the process-group timeout of each rank")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="diagnostic: every rank on cuda:0, gloo process group, torch transport "
                          "(exercises the multi-rank flow on a one-GPU box; timings meaningless)")
@@ -295,7 +351,7 @@ def main():
         print(json.dumps(cpu_baseline(args.p, args.warp, args.cpu_budget, args.cpu_workers)))
         return 0
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        return launch_ranks(args.gpus)
+        return launch_ranks(args.gpus, args.deadline)
 
     import torch
     import torch.distributed as dist
@@ -306,6 +362,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    _inject_failure(rank)
     if world != args.gpus:
         log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
     if args.rehearse_one_gpu:
@@ -314,10 +371,12 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
+        import datetime
+        pg_timeout = datetime.timedelta(seconds=args.deadline)
         if args.rehearse_one_gpu:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=pg_timeout)
         else:
-            dist.init_process_group("cpu:gloo,cuda:nccl", device_id=dev)
+            dist.init_process_group("cpu:gloo,cuda:nccl", device_id=dev, timeout=pg_timeout)
         dist.barrier()
 
     opname = args.op
@@ -379,6 +438,7 @@ def main():
     t_start = time.perf_counter()
     for k in range(args.steps):
         op.step(u, y, events[k])
+    t_enqueue = time.perf_counter() - t_start  # host time to enqueue the steps
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -399,10 +459,7 @@ def main():
         assert torch.isfinite(y).all().item(), "non-finite output"
         if kind == POISSON:
             parity = parity_spot_check(op, y, u, part, p, args.warp)
-            # above p = 10 the oracle's own float64 geometry (the reference's
-            # equispaced->GLL transform on O(1) coordinates, cond(V_eq) 1e3..1e5)
-            # is off by more than 1e-10 on small elements
-            parity["tolerance"] = 1e-10 if p <= 10 else 1e-8
+            parity["tolerance"] = 1e-10
             log("rank %d: parity spot check %s" % (rank, parity))
             assert parity["rel_l2"] < parity["tolerance"], parity
 
@@ -454,12 +511,15 @@ def main():
             "exchange_bytes_per_step_per_rank": 2 * op.exchange_bytes,
             "interface_elements": op.n_iface_elem,
             "kernel_ms_avg": kern_avg_s * 1e3, "kernel_ms_min": float(np.min(kern_ms)),
+            "kernel_ms_quartiles": [float(q) for q in np.percentile(kern_ms, [25, 50, 75])],
+            "kernel_ms_max": float(np.max(kern_ms)),
+            "host_enqueue_ms_per_step": t_enqueue / args.steps * 1e3,
+            "decomposition": op.dd_info(),
             "gflops_kernel": F / kern_avg_s / 1e9,
             "kernel_family": plan["kernel"], "map_entry_bytes": map_bytes,
             "gpu_setup_sec": t_setup, "gpu_setup_sec_per_elem": t_setup / max(1, n_elem_local),
             "scatter_plan": {k: plan[k] for k in ("plan", "colours", "chains_per_colour", "rounds",
-                                                  "zero_list", "atomic_groups", "dependencies",
-                                                  "lag", "wait_timeouts", "seam_nodes")},
+                                                  "zero_list", "atomic_groups", "seam_nodes")},
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -473,9 +533,7 @@ def main():
                         "k_poisson_apply<%d>") % (p + 1) if kind == POISSON else
                        ("k_axisym_nodal<%d>" if geometry == "nodal" else "k_axisym_apply<%d>")
                        % (p + 1)),
-            "launch": ("one sem_apply = one launch of %d chains (k_df_begin + the action)"
-                       % plan["chains_per_colour"][0] if plan["plan"] == "chains-one-launch" else
-                       "one sem_apply = one launch of %d chains + k_seam_sum over %d seam nodes"
+            "launch": ("one sem_apply = one launch of %d chains + k_seam_sum over %d seam nodes"
                        % (plan["chains_per_colour"][0], plan["seam_nodes"])
                        if plan["plan"] == "chains-seams" else
                        "one sem_apply = %d colour launches" % plan["colours"]) if world == 1 else

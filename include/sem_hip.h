@@ -133,27 +133,20 @@ int sem_set_map_shared(sem_ctx* ctx, const uint32_t* d_e2n, const uint8_t* d_nod
  * 1 element-coloured chains (chosen when the element order defeats the chain
  * patterns: more than half of the groups would need atomics; SEM_PLAN=1 / 0
  * in the environment forces / forbids it), 2 one element per wavefront
- * (MFMA kernel), 3 chains of consecutive elements in ONE launch (SEM_DF=1
- * in the environment; measured slower than the colour launches on MI355X,
- * DESIGN.md §5, so not the default): workgroups take
- * chains from a ticket counter, and a chain starts once every chain that
- * wrote one of its shared nodes earlier in ticket order has published
- * (per-chain flags); [5] is then 1 and [8] the chain count.
- * 4 the seam plan (Poisson, dofs_per_node == 1; AUTO where a colour launch
- * would be about one generation of resident workgroups or less -- p >= 10,
- * or few chains per colour; SEM_SEAM=1 / 0 forces / forbids):
- * all chains in one launch in element order, nodes written by several
- * chains stored per writer colour and summed in colour order by a second
- * launch, bitwise equal to the colour launches; [5] is then 1 and [8] the
- * chain count.
+ * (MFMA kernel), 4 the seam plan (Poisson, dofs_per_node == 1; AUTO where a
+ * colour launch would be about one generation of resident workgroups or
+ * less -- p >= 10, or few chains per colour; SEM_SEAM=1 / 0
+ * forces / forbids): all chains in one launch in element order, nodes
+ * written by several chains stored per writer colour and summed in colour
+ * order by a second launch, bitwise equal to the colour launches; [5] is
+ * then 1 and [8] the chain count.  (3 was a retired one-launch plan.)
  * [21] the axisymmetric Stokes geometry mode (as [19]; 0 when
- * dofs_per_node != 2).  [22] seam nodes of the seam plan, or dependency
- * edges of the one-launch plan, [23]
- * its colour lag in chains (SEM_DF_LAG), [24] dependency waits that hit
- * their spin limit since sem_set_map (never expected; read from the device,
- * so a request for 25 values synchronises with it).  Writes min(n_info, 25)
- * values.  A context's actions must not run concurrently with each other
- * (one stream at a time): the one-launch plan's counters are per context. */
+ * dofs_per_node != 2).  [22] seam nodes of the seam plan.  [23] 1 when the
+ * chains use the block layout (structured numberings: a chain is [6]
+ * stacked lines of elements, and the node row between two rounds is carried
+ * in registers; SEM_BLOCK_ROUNDS=R in the environment forces R rounds, 0
+ * turns it off), [24] the packed map entries so carried.
+ * Writes min(n_info, 25) values. */
 int sem_plan_info(sem_ctx* ctx, int64_t* info, int n_info);
 
 /* How the Poisson action obtains its geometric factors.
@@ -387,8 +380,18 @@ int sem_dd_set_transport(sem_dd* dd, sem_exchange_fn exchange, sem_allreduce_fn 
 int sem_copy_async(void* dst, const void* src, int64_t nbytes, void* stream);
 
 /* info[0] ndof_local, [1] n_iface_dofs, [2] peers, [3] exchanged values per
- * direction, [4] transport (0 none, 1 RCCL, 2 callbacks), [5] has interior. */
+ * direction, [4] transport (0 none, 1 RCCL, 2 callbacks), [5] has interior,
+ * [6] captured step on (sem_dd_set_graphs), [7] captures, [8] replays. */
 int sem_dd_info(sem_dd* dd, int64_t* info, int n_info);
+
+/* Captured step (default on; SEM_DD_GRAPH=0 in the environment turns it
+ * off): sem_dd_apply and the PCG operator action replay the step's launches
+ * as four HIP graphs around the transport call (side stream: gather,
+ * interface elements, pack | unpack; caller's stream: interior elements |
+ * final add), re-captured when the operator kind or the u / y pointers
+ * change.  Same kernels, same order, same results as the eager path; the
+ * host enqueues 4 graph launches instead of ~15 kernel launches. */
+int sem_dd_set_graphs(sem_dd* dd, int enable);
 
 /* y = K u on this rank's DOFs, shared DOFs summed over all ranks (u, y local
  * device vectors, must not alias). */

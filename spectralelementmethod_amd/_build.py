@@ -1,14 +1,22 @@
 """Build libsem_hip.so in-tree with hipcc for gfx950 (no JIT cache, no torch
-extension machinery: the library exposes a plain C ABI, include/sem_hip.h)."""
+extension machinery: the library exposes a plain C ABI, include/sem_hip.h).
+
+The operator kernels are instantiated per order in csrc/sem_launch.hip, which
+is compiled once per range of orders; all objects compile in parallel and are
+linked into one shared library."""
 import os
 import subprocess
+from concurrent.futures import ThreadPoolExecutor
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_NAME = "libsem_hip.so"
 LIB_PATH = os.environ.get("SEM_LIB_PATH", os.path.join(PKG_DIR, LIB_NAME))
 SOURCES = ["sem_device.hip", "sem_dd.hip", "sem_sc.hip", "sem_basis.cpp"]
-DEPS = SOURCES + ["sem_internal.h", "sem_kernels.h", "gll_table.h"]
+# (lo, hi) order ranges of sem_launch.hip, balanced by compile time (the
+# unrolled column kernels grow with n)
+LAUNCH_RANGES = [(2, 5), (6, 8), (9, 9), (10, 11), (12, 13), (14, 15), (16, 16), (17, 17)]
+DEPS = SOURCES + ["sem_launch.hip", "sem_internal.h", "sem_kernels.h", "sem_ctx.h", "gll_table.h"]
 ARCH = os.environ.get("SEM_OFFLOAD_ARCH", "gfx950")
 
 
@@ -30,22 +38,46 @@ def needs_rebuild():
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force=False, verbose=True, out=None, defines=()):
+def _jobs():
+    n = os.environ.get("MAX_JOBS") or str(os.cpu_count() or 4)
+    return max(1, min(16, int(n)))
+
+
+def build(force=False, verbose=True, out=None, defines=(), orders=None):
     """Compile the library (``out`` and ``defines`` build diagnostic
-    variants, e.g. for A/B timing in one process)."""
+    variants, e.g. for A/B timing in one process; ``orders`` = (lo, hi)
+    restricts the kernel instantiations to those orders)."""
     out = out or LIB_PATH
     if not force and out == LIB_PATH and not needs_rebuild():
         return LIB_PATH
-    cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-fPIC", "-shared", "-std=c++17",
-           "-munsafe-fp-atomics", "-Wall", "-Wno-unused-result",
-           *["-D" + d for d in defines],
-           *[os.path.join(CSRC, s) for s in SOURCES],
-           # RCCL for the multi-GPU interface sum (resolves to the librccl.so.1
-           # torch already loaded when imported through _lib)
-           "-L" + os.path.join(rocm_path(), "lib"), "-lrccl", "-o", out + ".tmp"]
+    objdir = out + ".objs"
+    os.makedirs(objdir, exist_ok=True)
+    common = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17",
+              "-munsafe-fp-atomics", "-Wall", "-Wno-unused-result",
+              *["-D" + d for d in defines]]
+    units = [(s, [], os.path.join(objdir, s + ".o")) for s in SOURCES]
+    ranges = [orders] if orders else LAUNCH_RANGES
+    for lo, hi in ranges:
+        units.append(("sem_launch.hip", ["-DSEM_N_LO=%d" % lo, "-DSEM_N_HI=%d" % hi],
+                      os.path.join(objdir, "sem_launch_%d_%d.o" % (lo, hi))))
+
+    def compile_one(u):
+        src, extra, obj = u
+        cmd = common + extra + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print("[sem build]", " ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        return obj
+
+    with ThreadPoolExecutor(_jobs()) as ex:
+        objs = list(ex.map(compile_one, units))
+    # RCCL for the multi-GPU interface sum (resolves to the librccl.so.1 torch
+    # already loaded when imported through _lib)
+    link = [hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC", *objs,
+            "-L" + os.path.join(rocm_path(), "lib"), "-lrccl", "-o", out + ".tmp"]
     if verbose:
-        print("[sem build]", " ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
+        print("[sem build]", " ".join(link), flush=True)
+    subprocess.run(link, check=True)
     os.replace(out + ".tmp", out)
     return out
 

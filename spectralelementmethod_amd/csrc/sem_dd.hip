@@ -257,6 +257,18 @@ struct sem_dd {
   sem_allreduce_fn rfn = nullptr;
   void* user = nullptr;
   int world = 1, rank = 0;
+  // captured step (sem_dd_set_graphs): the launches of one action as four
+  // HIP graphs around the transport call -- S: gather, interface elements,
+  // pack (side stream); M: interior elements (caller's stream); F: unpack
+  // per peer (side); G: y[cidx] += y_c (caller's) -- replayed while the
+  // kind and the u / y pointers stay the same
+  bool graphs = true;
+  hipStream_t cap = nullptr;  // capture stream of M and G
+  hipGraphExec_t gS = nullptr, gM = nullptr, gF = nullptr, gG = nullptr;
+  int g_kind = -1;
+  const double* g_u = nullptr;
+  double* g_y = nullptr;
+  int64_t n_captures = 0, n_replays = 0;
 };
 
 namespace {
@@ -266,28 +278,33 @@ int64_t n_exchanged(const sem_dd* d) { return d->off.empty() ? 0 : d->off.back()
 // compute part of one step: interface elements on the side stream into y_c
 // and packed into the send buffer, interior elements on `st` into y.
 // DIAG: the operator diagonal (Jacobi) instead of the action.
+// side-stream part: interface elements into y_c, packed into the send buffer
+int dd_side(sem_dd* d, int op_kind, bool diag, const double* u, hipStream_t sd) {
+  if (!d->iface) return SEM_OK;
+  if (diag) {
+    SEM_TRY(sem_diag(d->iface, op_kind, d->d_yc, sd));
+  } else {
+    SEM_TRY(sem_gather(u, d->d_cidx, d->nc, d->d_uc, sd));
+    SEM_TRY(sem_apply(d->iface, op_kind, d->d_uc, d->d_yc, 0, sd));
+  }
+  return sem_gather(d->d_yc, d->d_pidx, n_exchanged(d), d->d_send, sd);
+}
+
+// main-stream part: interior elements into y
+int dd_main(sem_dd* d, int op_kind, bool diag, const double* u, double* y, hipStream_t st) {
+  if (d->interior) {
+    if (diag) return sem_diag(d->interior, op_kind, y, st);
+    return sem_apply(d->interior, op_kind, u, y, 0, st);
+  }
+  HIP_TRY(hipMemsetAsync(y, 0, d->ndof * sizeof(double), st));
+  return SEM_OK;
+}
+
 int dd_begin(sem_dd* d, int op_kind, bool diag, const double* u, double* y, hipStream_t st) {
   HIP_TRY(hipEventRecord(d->ev0, st));
   HIP_TRY(hipStreamWaitEvent(d->side, d->ev0, 0));
-  void* sd = d->side;
-  if (d->iface) {
-    if (diag) {
-      SEM_TRY(sem_diag(d->iface, op_kind, d->d_yc, sd));
-    } else {
-      SEM_TRY(sem_gather(u, d->d_cidx, d->nc, d->d_uc, sd));
-      SEM_TRY(sem_apply(d->iface, op_kind, d->d_uc, d->d_yc, 0, sd));
-    }
-    SEM_TRY(sem_gather(d->d_yc, d->d_pidx, n_exchanged(d), d->d_send, sd));
-  }
-  if (d->interior) {
-    if (diag)
-      SEM_TRY(sem_diag(d->interior, op_kind, y, st));
-    else
-      SEM_TRY(sem_apply(d->interior, op_kind, u, y, 0, st));
-  } else {
-    HIP_TRY(hipMemsetAsync(y, 0, d->ndof * sizeof(double), st));
-  }
-  return SEM_OK;
+  SEM_TRY(dd_side(d, op_kind, diag, u, d->side));
+  return dd_main(d, op_kind, diag, u, y, st);
 }
 
 int dd_exchange(sem_dd* d) {
@@ -315,17 +332,88 @@ int dd_exchange(sem_dd* d) {
 // neighbours' partial sums into y_c (one launch per peer: a DOF may be
 // shared with several peers), then y[cidx] += y_c on `st` after the side
 // stream's work
-int dd_finish(sem_dd* d, double* y, hipStream_t st) {
+int dd_unpack(sem_dd* d, hipStream_t sd) {
   for (size_t k = 0; k + 1 < d->off.size(); ++k) {
     const int64_t cnt = d->off[k + 1] - d->off[k];
     if (cnt)
-      hipLaunchKernelGGL(k_scatter_add_peer, dim3(grid_for(cnt)), dim3(BLK), 0, d->side, d->d_yc,
+      hipLaunchKernelGGL(k_scatter_add_peer, dim3(grid_for(cnt)), dim3(BLK), 0, sd, d->d_yc,
                          d->d_pidx + d->off[k], cnt, d->d_recv + d->off[k]);
   }
   HIP_TRY(hipGetLastError());
+  return SEM_OK;
+}
+
+int dd_add(sem_dd* d, double* y, hipStream_t st) {
+  return d->nc ? sem_scatter_add(y, d->d_cidx, d->nc, d->d_yc, st) : SEM_OK;
+}
+
+int dd_finish(sem_dd* d, double* y, hipStream_t st) {
+  SEM_TRY(dd_unpack(d, d->side));
   HIP_TRY(hipEventRecord(d->ev1, d->side));
   HIP_TRY(hipStreamWaitEvent(st, d->ev1, 0));
-  return d->nc ? sem_scatter_add(y, d->d_cidx, d->nc, d->d_yc, st) : SEM_OK;
+  return dd_add(d, y, st);
+}
+
+// ---------------------------------------------------------------- captured step
+void drop_graphs(sem_dd* d) {
+  for (hipGraphExec_t* g : {&d->gS, &d->gM, &d->gF, &d->gG})
+    if (*g) {
+      (void)hipGraphExecDestroy(*g);
+      *g = nullptr;
+    }
+  d->g_kind = -1;
+}
+
+// body() enqueues onto `s` (a capturable, non-default stream) -> *out
+template <class F>
+int capture(hipStream_t s, F body, hipGraphExec_t* out) {
+  HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+  const int rc = body();
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(s, &g);
+  if (rc || e != hipSuccess) {
+    if (g) (void)hipGraphDestroy(g);
+    if (rc) return rc;
+    HIP_TRY(e);
+  }
+  const hipError_t ei = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  HIP_TRY(ei);
+  return SEM_OK;
+}
+
+int dd_capture(sem_dd* d, int op_kind, const double* u, double* y) {
+  drop_graphs(d);
+  if (!d->cap) HIP_TRY(hipStreamCreateWithFlags(&d->cap, hipStreamNonBlocking));
+  if (d->iface) {
+    SEM_TRY(capture(d->side, [&] { return dd_side(d, op_kind, false, u, d->side); }, &d->gS));
+    SEM_TRY(capture(d->side, [&] { return dd_unpack(d, d->side); }, &d->gF));
+    SEM_TRY(capture(d->cap, [&] { return dd_add(d, y, d->cap); }, &d->gG));
+  }
+  SEM_TRY(capture(d->cap, [&] { return dd_main(d, op_kind, false, u, y, d->cap); }, &d->gM));
+  d->g_kind = op_kind;
+  d->g_u = u;
+  d->g_y = y;
+  d->n_captures++;
+  return SEM_OK;
+}
+
+// one action through the captured graphs: the same dependency structure as
+// dd_begin / dd_exchange / dd_finish, four graph launches instead of ~15
+// kernel launches
+int dd_apply_graphs(sem_dd* d, int op_kind, const double* u, double* y, hipStream_t st) {
+  if (d->g_kind != op_kind || d->g_u != u || d->g_y != y) SEM_TRY(dd_capture(d, op_kind, u, y));
+  HIP_TRY(hipEventRecord(d->ev0, st));
+  HIP_TRY(hipStreamWaitEvent(d->side, d->ev0, 0));
+  if (d->gS) HIP_TRY(hipGraphLaunch(d->gS, d->side));
+  HIP_TRY(hipGraphLaunch(d->gM, st));
+  SEM_TRY(dd_exchange(d));
+  if (d->gF) HIP_TRY(hipGraphLaunch(d->gF, d->side));
+  HIP_TRY(hipEventRecord(d->ev1, d->side));
+  HIP_TRY(hipStreamWaitEvent(st, d->ev1, 0));
+  if (d->gG) HIP_TRY(hipGraphLaunch(d->gG, st));
+  d->n_replays++;
+  return SEM_OK;
 }
 
 int dd_allreduce(sem_dd* d, double* buf, int count, hipStream_t st) {
@@ -363,6 +451,7 @@ struct PcgOp {
       return SEM_OK;
     }
     if (dd) {
+      if (dd->graphs) return dd_apply_graphs(dd, kind, p, q, st);
       SEM_TRY(dd_begin(dd, kind, false, p, q, st));
       SEM_TRY(dd_exchange(dd));
       return dd_finish(dd, q, st);
@@ -588,6 +677,7 @@ int sem_dd_create(sem_dd** out, sem_ctx* iface, sem_ctx* interior, int64_t ndof_
   }
   // the device-to-device copies above may still run on the legacy stream
   if (bad(hipDeviceSynchronize())) return fail(SEM_E_HIP, "sem_dd_create: synchronize failed");
+  if (const char* e = std::getenv("SEM_DD_GRAPH")) d->graphs = std::atoi(e) != 0;
   *out = d;
   return SEM_OK;
 }
@@ -596,6 +686,9 @@ void sem_dd_destroy(sem_dd* d) {
   if (!d) return;
   DeviceGuard g(d->device);
   if (d->side) (void)hipStreamSynchronize(d->side);
+  if (d->cap) (void)hipStreamSynchronize(d->cap);
+  drop_graphs(d);
+  if (d->cap) (void)hipStreamDestroy(d->cap);
   if (d->comm) (void)ncclCommDestroy(d->comm);
   (void)hipFree(d->d_cidx);
   (void)hipFree(d->d_pidx);
@@ -646,9 +739,19 @@ int sem_dd_set_transport(sem_dd* d, sem_exchange_fn xfn, sem_allreduce_fn rfn, v
 
 int sem_dd_info(sem_dd* d, int64_t* info, int n_info) {
   if (!d || !info || n_info < 1) return fail(SEM_E_INVALID, "bad arguments");
-  const int64_t v[6] = {d->ndof, d->nc, (int64_t)d->peer.size(), n_exchanged(d),
-                        d->comm ? 1 : (d->xfn ? 2 : 0), d->interior ? 1 : 0};
-  for (int i = 0; i < n_info && i < 6; ++i) info[i] = v[i];
+  const int64_t v[9] = {d->ndof, d->nc, (int64_t)d->peer.size(), n_exchanged(d),
+                        d->comm ? 1 : (d->xfn ? 2 : 0), d->interior ? 1 : 0,
+                        d->graphs ? 1 : 0, d->n_captures, d->n_replays};
+  for (int i = 0; i < n_info && i < 9; ++i) info[i] = v[i];
+  return SEM_OK;
+}
+
+int sem_dd_set_graphs(sem_dd* d, int enable) {
+  if (!d) return fail(SEM_E_INVALID, "null dd");
+  DeviceGuard g(d->device);
+  if (d->side) HIP_TRY(hipStreamSynchronize(d->side));
+  drop_graphs(d);
+  d->graphs = enable != 0;
   return SEM_OK;
 }
 
@@ -656,6 +759,7 @@ int sem_dd_apply(sem_dd* d, int op_kind, const double* d_u, double* d_y, void* s
   if (!d || !d_u || !d_y) return fail(SEM_E_INVALID, "null argument");
   if (d_u == d_y) return fail(SEM_E_INVALID, "sem_dd_apply: u and y must not alias");
   DeviceGuard g(d->device);
+  if (d->graphs) return dd_apply_graphs(d, op_kind, d_u, d_y, S(stream));
   SEM_TRY(dd_begin(d, op_kind, false, d_u, d_y, S(stream)));
   SEM_TRY(dd_exchange(d));
   return dd_finish(d, d_y, S(stream));

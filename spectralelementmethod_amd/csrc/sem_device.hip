@@ -1,28 +1,15 @@
-// Device half of libsem_hip.so: the operator context, the setup planner
-// (map packing, group colouring, write codes) and the C ABI that launches
-// the kernels of sem_kernels.h.
-#include <hip/hip_runtime.h>
-
-#include <algorithm>
+// Device half of libsem_hip.so: the setup planner (map packing, group
+// colouring, write codes), the small kernels and the C ABI.  The operator
+// kernels are instantiated per order in sem_launch.hip.
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
-#include <cstring>
-#include <string>
-#include <vector>
 
-#include "sem_internal.h"
-#include "sem_kernels.h"
+#include "sem_ctx.h"
 
 using sem::fail;
 using namespace semk;
-
-#define HIP_TRY(expr)                                                                  \
-  do {                                                                                 \
-    hipError_t _e = (expr);                                                            \
-    if (_e != hipSuccess)                                                              \
-      return fail(SEM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));      \
-  } while (0)
+using namespace semd;
 
 namespace {
 
@@ -160,279 +147,20 @@ __global__ void k_det_inv_2x2(int64_t n, const double* __restrict__ M, double* _
   }
 }
 
-inline int grid_for(int64_t n, int per_block = BLOCK, int cap = 8192) {
-  int64_t g = (n + per_block - 1) / per_block;
-  if (g < 1) g = 1;
-  if (g > cap) g = cap;
-  return (int)g;
-}
 
 }  // namespace
-
-// ---------------------------------------------------------------------------
-// context
-// ---------------------------------------------------------------------------
-constexpr int MAX_COLOURS = 8;  // + one trailing all-atomic class
-// colour lag of the one-launch plan's ticket order, in chains (about two
-// generations of resident workgroups at p = 8: 4 per CU x 256 CUs)
-// AUTO choice of the seam plan (Poisson column kernel), from the MI355X A/B
-// of profiles/r02/seams2 (ms per action, colour launches -> seams; cpc =
-// chains per colour): it wins where a colour launch is a few generations of
-// resident workgroups or less -- p = 16 198^2 (cpc 1,633) 0.164 -> 0.134,
-// p = 12 263^2 0.139 -> 0.114, p = 10 316^2 (1,296) 0.158 -> 0.128, p = 9
-// 351^2 (1,297) 0.120 -> 0.113, p = 8 512^2 (2,342) 0.185 -> 0.179, 384^2
-// (1,372) 0.107 -> 0.095, 128 x 1024 (1,171; one rank's strip of the
-// 8-GPU split) 0.098 -> 0.089, 256^2 (585) 0.0635 -> 0.0477, p = 6 256^2
-// (488) 0.040 -> 0.030, p = 4 395^2 (815) 0.045 -> 0.036 -- and loses where
-// the colour launches stream many generations and the seams are a large
-// share of the nodes: p = 8 1024^2 (9,365) 0.640 -> 0.668, p = 6 527^2
-// (1,928) 0.118 -> 0.122, p = 4 790^2 (3,250) 0.113 -> 0.129, p = 2 1581^2
-// 0.132 -> 0.161.
-// Two DOFs per node (axisymmetric block, p = 6, profiles/r02/final/
-// axisym_seams): 128^2 (cpc 114) 0.0441 -> 0.0236, 512^2 (cpc 1,820) 0.227
-// -> 0.274 (the nodal kernel's seam instantiation runs 1 wave per SIMD
-// instead of 2).
-bool seam_auto(int n, int64_t chains_per_colour, int dpn = 1) {
-  if (dpn == 2) return chains_per_colour <= 512;
-  return n >= 11 || chains_per_colour <= 1024 || (n >= 9 && chains_per_colour <= 2400);
-}
-#ifndef SEM_DF_LAG_DEFAULT
-#define SEM_DF_LAG_DEFAULT 2048
-#endif
-
-struct sem_ctx {
-  int p = 0, n = 0, dpn = 1, device = 0;
-  int64_t n_elem = 0, n_node = 0;
-  int epw = 0, lw = 0;
-  int64_t n_groups = 0;
-  double hD[SEM_MAXN * SEM_MAXN];
-  double hw[SEM_MAXN];
-  bool have_basis = false;
-  double* d_D = nullptr;
-  double* d_w = nullptr;
-  double* d_Vinv = nullptr;
-  double* d_deo = nullptr;  // even-odd D for n >= SEM_D_SCALAR_LOAD_N (scalar loads)
-  uint32_t* d_mapP = nullptr;   // packed coded map, launch (colour) order
-  uint16_t* d_map16 = nullptr;  // the same map as 16-bit row offsets (column kernel)
-  uint32_t* d_mbase = nullptr;  // their per-(slot, row) 32-bit bases
-  bool map16 = false;
-  int* d_epos = nullptr;         // element -> packed position slot * epw + k
-  const uint32_t* d_e2n = nullptr;
-  uint32_t* d_zero = nullptr;    // y entries no kernel stores first (unreferenced / first-atomic)
-  int64_t n_zero = 0;
-  int rounds = 1;                     // rounds of 4 groups per chain (workgroup)
-  int64_t n_slots = 0;                // packed group slots = chains * 4 * rounds
-  std::vector<int64_t> colour_start;  // chain ranges, one launch each
-  int64_t n_atomic_groups = 0;        // groups in atomic-fallback chains
-  bool conforming = true;
-  double* d_GP[3] = {nullptr, nullptr, nullptr};  // Poisson, axisym. Stokes, Navier-Stokes
-  double reynolds = 0.0;
-  double* d_lin = nullptr;  // Navier-Stokes linearisation, 5 per element node
-  bool lin_valid = false;
-  // NODAL geometry (Poisson): x_phys per global node + the node's first element
-  int geom_mode = SEM_GEOM_AUTO;
-  // kernel family of the Poisson action (sem_set_kernel), fixed by
-  // sem_set_map: the LDS column kernel or the fp64-MFMA element kernel (they
-  // need different plans and packed layouts)
-  int kernel = SEM_KERNEL_AUTO;
-  bool mfma = false;
-  bool ecol = false;  // column kernel on the element-coloured plan
-  double2* d_XG = nullptr;
-  uint32_t* d_owner = nullptr;
-  bool xg_valid = false;  // the Poisson action reads d_XG
-  bool xg_axi = false;    // the axisymmetric Stokes action reads d_XG
-  unsigned long long* d_bad = nullptr;
-  // one-launch plan of the Poisson column kernel (DFPlan, sem_kernels.h)
-  bool df = false;
-  int df_ticketed = 1;  // SEM_DF_TICKET=0: chain = blockIdx (timing experiments)
-  int64_t df_lag = 0;
-  int64_t n_deps = 0;
-  int* d_dep_start = nullptr;
-  int* d_dep_idx = nullptr;
-  uint32_t* d_df_flags = nullptr;
-  uint32_t* d_df_state = nullptr;
-  // seam plan of the Poisson column kernel (SeamPlan, sem_kernels.h)
-  bool seam = false;
-  int seam_ns = 0;
-  int64_t n_seam = 0;
-  uint8_t* d_ccol = nullptr;
-  uint32_t* d_seam_gid = nullptr;
-  uint16_t* d_seam_mask = nullptr;
-  double* d_seam_buf = nullptr;
-};
-
 namespace sem {
 int64_t ctx_ndof(const sem_ctx* c) { return c->n_node * c->dpn; }
 int ctx_device(const sem_ctx* c) { return c->device; }
 }  // namespace sem
 
-namespace {
-
-struct DeviceGuard {
-  int prev = -1;
-  explicit DeviceGuard(int dev) {
-    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    if (prev != dev) (void)hipSetDevice(dev);
-  }
-  ~DeviceGuard() {
-    int cur;
-    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-  }
-};
-
-inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
-
-// even-odd halves of D (row-major h[m*N + r]); see DEO in sem_kernels.h
-template <int N>
-DEOData<N> make_deo_data(const double* h) {
-  DEOData<N> d;
-  constexpr int H = N / 2;
-  for (int m = 0; m < H; ++m)
-    for (int r = 0; r < H; ++r) {
-      d.P[m * H + r] = 0.5 * (h[m * N + r] - h[m * N + N - 1 - r]);
-      d.Q[m * H + r] = 0.5 * (h[m * N + r] + h[m * N + N - 1 - r]);
-    }
-  if (DEOData<N>::C)
-    for (int m = 0; m < H; ++m) {
-      d.cc[m] = h[m * N + H];
-      d.rr[m] = h[H * N + m];
-    }
-  return d;
-}
-
-template <int N>
-DEO<N> make_deo(const sem_ctx* c) {
-  DEO<N> a;
-  if constexpr (N >= SEM_D_SCALAR_LOAD_N)
-    a.p = reinterpret_cast<const DEOData<N>*>(c->d_deo);
-  else
-    a.d = make_deo_data<N>(c->hD);
-  return a;
-}
-
-template <int N>
-void upload_deo(sem_ctx* c, hipError_t* err) {
-  const DEOData<N> d = make_deo_data<N>(c->hD);
-  *err = hipMemcpy(c->d_deo, &d, sizeof(d), hipMemcpyHostToDevice);
-}
-
-// AUTO geometry of the column kernel, per order from the MI355X sweep at
-// ~1e7 DOF (profiles/r01c/geosweep): NODAL (factors
-// re-derived from x_phys per node) at p = 1, 2, 4, 5, 8, STORED at p = 3, 6,
-// 7 and above 8.  The p = 3, 5, 6 picks are within 2-3 % (one run each);
-// the clear wins are p = 2, 4, 8 (nodal) and p >= 9 (stored).
-bool auto_nodal_order(int n) { return n == 2 || n == 3 || n == 5 || n == 6 || n == 9; }
-
-bool nodal_mode(const sem_ctx* c) {
-  if (c->mfma) return c->geom_mode == SEM_GEOM_NODAL;  // AUTO: stored factors
-  return c->geom_mode == SEM_GEOM_NODAL ||
-         (c->geom_mode == SEM_GEOM_AUTO && auto_nodal_order(c->n));
-}
-
-// AUTO: the MFMA element kernel from SEM_MFMA_MIN_N nodes per line up,
-// Poisson only (dpn = 1), one 16 x 16 tile (n <= 16), and not when nodal
-// geometry was requested explicitly.  Round 1 measured it ahead of the
-// column kernel on colour launches at p = 13..15 (profiles/r01c/geosweep);
-// the column kernel on the seam plan is ahead at every order (MI355X, ~1e7
-// DOF, ms per action, MFMA / column: p = 10 0.160 / 0.126, p = 13 0.147 /
-// 0.129, p = 14 0.143 / 0.141, p = 15 0.142 / 0.112; profiles/r02/final),
-// so AUTO no longer picks it (SEM_KERNEL_MFMA still does).
-#ifndef SEM_MFMA_MIN_N
-#define SEM_MFMA_MIN_N 17
-#endif
-bool want_mfma(const sem_ctx* c) {
-  if (c->dpn != 1 || c->n > 16) return false;
-  if (c->kernel == SEM_KERNEL_MFMA) return true;
-  if (c->kernel == SEM_KERNEL_COLUMN) return false;
-  return c->n >= SEM_MFMA_MIN_N && c->geom_mode != SEM_GEOM_NODAL;
-}
-
-// axisymmetric Stokes block (dpn = 2, column kernel only): AUTO picks NODAL
-// where it measured faster at ~9.4e6 nodes (DESIGN.md §4.2,
-// profiles/r02/axisym): p = 2 / 4 / 6 0.226 / 0.192 / 0.214 ms against
-// 0.367 / 0.306 / 0.305 stored, p = 16 0.428 vs 0.481; STORED at p = 8..12
-// (0.275 vs 0.286 at p = 8, 0.286 vs 0.421 at p = 10: the nodal kernel's
-// register demand drops it to one wave per SIMD).  Unmeasured orders follow
-// their neighbours.
-bool auto_nodal_axi_order(int n) { return n <= 7 || n == 17; }
-
-bool nodal_mode_op(const sem_ctx* c, int op_kind) {
-  if (op_kind == SEM_OP_POISSON) return nodal_mode(c);
-  if (op_kind == SEM_OP_AXISYM_STOKES)
-    return c->geom_mode == SEM_GEOM_NODAL ||
-           (c->geom_mode == SEM_GEOM_AUTO && auto_nodal_axi_order(c->n));
-  return false;  // Navier-Stokes: stored factors
-}
-
-bool use_nodal(const sem_ctx* c, int op_kind) {
-  if (op_kind == SEM_OP_POISSON) return nodal_mode(c) && c->xg_valid;
-  if (op_kind == SEM_OP_AXISYM_STOKES) return nodal_mode_op(c, op_kind) && c->xg_axi;
-  return false;
-}
-
-// one chain-kernel launch, one-launch plan (DF) or a colour class
-template <int N, bool DF, bool SEAM = false>
-void launch_chains(sem_ctx* c, int op_kind, bool nodal, const double* u, double* y, int acc,
-                   bool lin, int64_t c0, int64_t c1, const DEO<N>& D, const WVec<N>& w,
-                   const DFPlan& df, hipStream_t st) {
-  const dim3 g((unsigned)(c1 - c0)), b(ChainWaves<N>::block);
-  const MapRef mr{c->d_mapP, c->d_map16, c->d_mbase};
-  const int R = c->rounds;
-  if (op_kind == SEM_OP_POISSON) {
-    const double* GP = nodal ? nullptr : c->d_GP[0];
-    const double2* XG = nodal ? c->d_XG : nullptr;
-    const SeamPlan sp{c->d_ccol, c->d_seam_buf, c->n_node};
-    if (nodal && c->map16)
-      hipLaunchKernelGGL((k_poisson_apply<N, true, true, DF, SEAM>), g, b, 0, st, mr, GP, XG, u,
-                         y, c0, c1, R, acc, D, w, df, sp);
-    else if (nodal)
-      hipLaunchKernelGGL((k_poisson_apply<N, true, false, DF, SEAM>), g, b, 0, st, mr, GP, XG, u,
-                         y, c0, c1, R, acc, D, w, df, sp);
-    else if (c->map16)
-      hipLaunchKernelGGL((k_poisson_apply<N, false, true, DF, SEAM>), g, b, 0, st, mr, GP, XG, u,
-                         y, c0, c1, R, acc, D, w, df, sp);
-    else
-      hipLaunchKernelGGL((k_poisson_apply<N, false, false, DF, SEAM>), g, b, 0, st, mr, GP, XG,
-                         u, y, c0, c1, R, acc, D, w, df, sp);
-  } else if (op_kind == SEM_OP_AXISYM_STOKES && nodal) {
-    const SeamPlan sp{c->d_ccol, c->d_seam_buf, c->n_node};
-    if (c->map16)
-      hipLaunchKernelGGL((k_axisym_nodal<N, true, DF, SEAM>), g, b, 0, st, mr, c->d_XG, u, y, c0,
-                         c1, R, acc, D, w, df, sp);
-    else
-      hipLaunchKernelGGL((k_axisym_nodal<N, false, DF, SEAM>), g, b, 0, st, mr, c->d_XG, u, y, c0,
-                         c1, R, acc, D, w, df, sp);
-  } else if (op_kind == SEM_OP_AXISYM_STOKES) {
-    const SeamPlan sp{c->d_ccol, c->d_seam_buf, c->n_node};
-    hipLaunchKernelGGL((k_axisym_apply<N, 0, DF, SEAM>), g, b, 0, st, c->d_mapP, c->d_GP[1], u, y,
-                       c0, c1, R, acc, D, w, AxiNS(), df, sp);
-  } else {
-    const SeamPlan sp{c->d_ccol, c->d_seam_buf, c->n_node};
-    AxiNS ns;
-    ns.re = c->reynolds;
-    ns.lin = (op_kind == SEM_OP_AXISYM_NS_JVP || lin) ? c->d_lin : nullptr;
-    if (op_kind == SEM_OP_AXISYM_NS)
-      hipLaunchKernelGGL((k_axisym_apply<N, 1, DF, SEAM>), g, b, 0, st, c->d_mapP, c->d_GP[2], u,
-                         y, c0, c1, R, acc, D, w, ns, df, sp);
-    else
-      hipLaunchKernelGGL((k_axisym_apply<N, 2, DF, SEAM>), g, b, 0, st, c->d_mapP, c->d_GP[2], u,
-                         y, c0, c1, R, acc, D, w, ns, df, sp);
-  }
-}
-
-template <int N>
-int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc, bool lin,
-                   hipStream_t st) {
-  const DEO<N> D = make_deo<N>(c);
-  WVec<N> w;
-  std::memcpy(w.v, c->hw, sizeof(w.v));
-  const bool nodal = use_nodal(c, op_kind);
-  if (c->seam) {  // one launch + the seam sums (SeamPlan)
-    launch_chains<N, false, true>(c, op_kind, nodal, u, y, acc, lin, c->colour_start.front(),
-                                  c->colour_start.back(), D, w, DFPlan{}, st);
-    if (c->n_seam) {
-      const dim3 g(grid_for(c->n_seam)), b(BLOCK);
-      switch (c->seam_ns) {
+namespace semd {
+// second launch of the seam plan (k_seam_sum / k_seam_sum2 over the seam
+// nodes, one instantiation per colour count)
+int launch_seam_sum(sem_ctx* c, double* y, int acc, hipStream_t st) {
+  if (!c->n_seam) return SEM_OK;
+  const dim3 g(grid_for(c->n_seam)), b(BLOCK);
+  switch (c->seam_ns) {
 #define SEAM_NS(K)                                                                           \
   case K:                                                                                  \
     if (c->dpn == 2)                                                                       \
@@ -442,84 +170,16 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
       hipLaunchKernelGGL(k_seam_sum<K>, g, b, 0, st, y, c->d_seam_gid, c->d_seam_mask,     \
                          c->n_seam, c->d_seam_buf, c->n_node, acc);                        \
     break;
-        SEAM_NS(1) SEAM_NS(2) SEAM_NS(3) SEAM_NS(4) SEAM_NS(5) SEAM_NS(6) SEAM_NS(7) SEAM_NS(8)
+    SEAM_NS(1) SEAM_NS(2) SEAM_NS(3) SEAM_NS(4) SEAM_NS(5) SEAM_NS(6) SEAM_NS(7) SEAM_NS(8)
 #undef SEAM_NS
-        default:
-          return fail(SEM_E_STATE, "seam plan with more than 8 colours");
-      }
-    }
-    return SEM_OK;
-  }
-  if (c->df) {  // every chain in one launch (DFPlan, sem_kernels.h)
-    const DFPlan df{c->d_dep_start, c->d_dep_idx, c->d_df_flags, c->d_df_state, c->df_ticketed};
-    hipLaunchKernelGGL(k_df_begin, dim3(1), dim3(WAVE), 0, st, c->d_df_state);
-    launch_chains<N, true>(c, op_kind, nodal, u, y, acc, lin, c->colour_start.front(),
-                           c->colour_start.back(), D, w, df, st);
-    return SEM_OK;
-  }
-  const size_t nc = c->colour_start.size() - 1;
-  for (size_t k = 0; k < nc; ++k) {
-    const int64_t c0 = c->colour_start[k], c1 = c->colour_start[k + 1];
-    if (c1 <= c0) continue;
-    if (op_kind == SEM_OP_POISSON && c->mfma) {
-      if constexpr (N <= 16) {
-        constexpr int per_block = MFMA_EPB * (16 / N) * (16 / N);
-        const dim3 g((unsigned)((c1 - c0 + per_block - 1) / per_block));
-        if (nodal)
-          hipLaunchKernelGGL((k_poisson_mfma<N, true>), g, dim3(BLOCK), 0, st, c->d_mapP, nullptr,
-                             c->d_XG, u, y, c->d_D, w, c0, c1, acc);
-        else
-          hipLaunchKernelGGL((k_poisson_mfma<N, false>), g, dim3(BLOCK), 0, st, c->d_mapP,
-                             c->d_GP[0], nullptr, u, y, c->d_D, w, c0, c1, acc);
-      }
-    } else {
-      launch_chains<N, false>(c, op_kind, nodal, u, y, acc, lin, c0, c1, D, w, DFPlan{}, st);
-    }
+    default:
+      return sem::fail(SEM_E_STATE, "seam plan with more than 8 colours");
   }
   return SEM_OK;
 }
+}  // namespace semd
 
-// nodes -> factors/fields (XGin null), or XGin (x_phys per node) -> factors
-template <int N>
-void launch_geom_n(sem_ctx* c, const double* nodes, int op_kind, double* GP, double* xph,
-                   double* J, double* iJ, double* dJ, double* dJW, double2* XG,
-                   const double2* XGin, hipStream_t st) {
-  using Sh = GeomShape<N>;
-  const int grid = (int)((c->n_elem + Sh::EPB - 1) / Sh::EPB);
-  hipLaunchKernelGGL((k_geometry<N>), dim3(grid), dim3(Sh::THREADS), 0, st, nodes, c->n_node,
-                     c->d_e2n, c->n_elem, c->d_Vinv, c->d_D, c->d_w, op_kind, c->epw, c->d_epos, GP,
-                     xph,
-                     J, iJ, dJ, dJW, XG, XG ? c->d_owner : nullptr, XGin, c->d_bad);
-}
-
-#ifdef SEM_ONLY_N  // diagnostic variant builds: one order only (fast compiles)
-#define SEM_DISPATCH_N(n, FN, ...)                   \
-  switch (n) {                                       \
-    case SEM_ONLY_N: FN<SEM_ONLY_N>(__VA_ARGS__); break; \
-    default: break;                                  \
-  }
-#else
-#define SEM_DISPATCH_N(n, FN, ...)       \
-  switch (n) {                           \
-    case 2: FN<2>(__VA_ARGS__); break;   \
-    case 3: FN<3>(__VA_ARGS__); break;   \
-    case 4: FN<4>(__VA_ARGS__); break;   \
-    case 5: FN<5>(__VA_ARGS__); break;   \
-    case 6: FN<6>(__VA_ARGS__); break;   \
-    case 7: FN<7>(__VA_ARGS__); break;   \
-    case 8: FN<8>(__VA_ARGS__); break;   \
-    case 9: FN<9>(__VA_ARGS__); break;   \
-    case 10: FN<10>(__VA_ARGS__); break; \
-    case 11: FN<11>(__VA_ARGS__); break; \
-    case 12: FN<12>(__VA_ARGS__); break; \
-    case 13: FN<13>(__VA_ARGS__); break; \
-    case 14: FN<14>(__VA_ARGS__); break; \
-    case 15: FN<15>(__VA_ARGS__); break; \
-    case 16: FN<16>(__VA_ARGS__); break; \
-    case 17: FN<17>(__VA_ARGS__); break; \
-    default: break;                      \
-  }
-#endif
+namespace {
 
 int check_op(sem_ctx* c, int op_kind) {
   if (op_kind == SEM_OP_POISSON) {
@@ -557,8 +217,9 @@ int ensure_gp(sem_ctx* c, int op_kind, hipStream_t st) {
 
 // ---------------------------------------------------------------------------
 // Setup planner (host, once per map).
-//   1. groups = EPW consecutive elements (one wavefront each); chains =
-//      4 * rounds consecutive groups (one workgroup each);
+//   1. groups = EPW element slots (one wavefront each), chains = CH = 4 *
+//      rounds consecutive groups (one workgroup each), from a group table
+//      (groups_consecutive / groups_blocks below);
 //   2. greedy colouring of chains: chains of one colour share no node
 //      (per-node colour bitmask; chains needing > MAX_COLOURS colours, and
 //      every chain of a non-conforming mesh, go to a final all-atomic class);
@@ -568,11 +229,17 @@ int ensure_gp(sem_ctx* c, int op_kind, hipStream_t st) {
 //      two neighbouring lanes of one group (row r, lanes L, L+1: MERGE on L,
 //      SKIP on L+1) or (b) the last lane of group i-1 and lane 0 of group i
 //      (row r: SKIP on the former, CARRY on the latter); anything else makes
-//      the chain atomic;
+//      the chain atomic.  Across rounds, (c) row n-1 of a lane's element and
+//      row 0 of the same lane's element in the next round (the block layout)
+//      is carried in registers: SKIP | CARRY on the former, which is then no
+//      writer at all; any other node a chain touches again in a later round
+//      is a read-modify-write of its own earlier store;
 //   5. write codes in launch order: first writer of a node -> STORE, later
 //      writers -> RMW (atomic chains -> ATOMIC);
 //   6. zero list = unreferenced nodes + nodes whose first writer is atomic.
 // ---------------------------------------------------------------------------
+constexpr uint32_t W_ROWCARRY = W_SKIP | W_CARRY;  // sem_kernels.h k_poisson_apply
+
 struct Plan {
   std::vector<uint32_t> owner;  // first element referencing each node
   std::vector<uint32_t> mapP;
@@ -583,10 +250,8 @@ struct Plan {
   int64_t n_atomic_groups = 0;
   int64_t n_slots = 0;
   bool conforming = true;
-  // one-launch plan (df_lag > 0): chains in ticket order, and per chain the
-  // earlier chains that last wrote one of its shared nodes
-  bool df = false;
-  std::vector<int> dep_start, dep_idx;
+  bool blocks = false;     // block layout (groups_blocks)
+  int64_t row_carries = 0;  // entries carried to the next round in registers
   // seam plan: chains in element order, one launch; nodes written by several
   // chains go through per-colour slots summed by k_seam_sum
   bool seam = false;
@@ -597,17 +262,86 @@ struct Plan {
   bool seam_failed = false;
 };
 
+// groups of EPW consecutive elements, chains of CH consecutive groups
+void groups_consecutive(int64_t n_elem, int epw, int CH, std::vector<int64_t>& gel) {
+  const int64_t n_groups = (n_elem + epw - 1) / epw;
+  const int64_t n_chains = (n_groups + CH - 1) / CH;
+  gel.assign((size_t)(n_chains * CH * epw), -1);
+  for (int64_t e = 0; e < n_elem; ++e) gel[e] = e;
+}
+
+// Block layout for structured numberings: the elements form
+// "lines" -- runs of consecutive ids in which each element's last node column
+// is the next one's first -- of equal length L, and line l + 1 sits on line l
+// (element e + L has e's node row n-1 as its row 0).  A chain is a block of
+// R stacked lines x CW * EPW elements; round rd of the chain is line rd of the
+// block, so the node row between consecutive rounds is carried from one round
+// to the next in registers (same wave, same lane) instead of being written by
+// two chains.  Returns false (gel untouched) when the numbering is not of
+// that form; the caller then uses groups_consecutive.
+bool groups_blocks(const std::vector<uint32_t>& e2n, int64_t n_elem, int n, int epw, int CW,
+                   int R, std::vector<int64_t>& gel) {
+  const int nn = n * n;
+  auto at = [&](int64_t e, int r, int jj) { return e2n[e * nn + r * n + jj]; };
+  std::vector<int64_t> ls{0};
+  for (int64_t e = 0; e + 1 < n_elem; ++e) {
+    bool cont = true;
+    for (int r = 0; r < n && cont; ++r) cont = at(e, r, n - 1) == at(e + 1, r, 0);
+    if (!cont) ls.push_back(e + 1);
+  }
+  ls.push_back(n_elem);
+  const int64_t nl = (int64_t)ls.size() - 1;
+  if (nl < 2 || R < 2) return false;
+  const int64_t len = ls[1] - ls[0];
+  for (int64_t l = 0; l < nl; ++l)
+    if (ls[l + 1] - ls[l] != len) return false;
+  std::vector<uint8_t> on(nl, 0);  // line l + 1 sits on line l
+  int64_t n_on = 0;
+  for (int64_t l = 0; l + 1 < nl; ++l) {
+    bool ok = true;
+    for (int64_t i = 0; i < len && ok; ++i)
+      for (int jj = 0; jj < n && ok; ++jj) ok = at(ls[l] + i + len, 0, jj) == at(ls[l] + i, n - 1, jj);
+    on[l] = ok ? 1 : 0;
+    n_on += ok ? 1 : 0;
+  }
+  if (n_on * 2 < nl - 1) return false;
+  const int64_t seg = (int64_t)CW * epw;
+  const int64_t nseg = (len + seg - 1) / seg;
+  std::vector<int64_t> out;
+  out.reserve((size_t)((nl + R - 1) / R * nseg * R * seg));
+  for (int64_t l = 0; l < nl;) {
+    int r = 1;  // stacked lines of this block
+    while (r < R && l + r < nl && on[l + r - 1]) ++r;
+    for (int64_t sg = 0; sg < nseg; ++sg)
+      for (int rd = 0; rd < R; ++rd)
+        for (int w = 0; w < CW; ++w)
+          for (int k = 0; k < epw; ++k) {
+            const int64_t i = sg * seg + (int64_t)w * epw + k;
+            out.push_back(rd < r && i < len ? ls[l + rd] + i : -1);
+          }
+    l += r;
+  }
+  gel.swap(out);
+  return true;
+}
+
 // node_state (may be empty): SEM_NODE_PRIOR = y already holds a value when
 // this operator runs (first touches become read-modify-write, never zeroed);
 // SEM_NODE_OTHER = another operator writes it (not zeroed when unreferenced).
+// block_rounds >= 2: try the block layout with that many rounds (P.blocks
+// tells whether it applied; rounds is then block_rounds).
 int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node, int n,
-               int rounds, const std::vector<uint8_t>& node_state, Plan& P,
-               int64_t df_lag = 0, int seam = 0, int seam_dpn = 1) {
+               int rounds, const std::vector<uint8_t>& node_state, Plan& P, int seam = 0,
+               int seam_dpn = 1, int block_rounds = 0) {
   const int epw = WAVE / n, lw = epw * n, nn = n * n;
-  const int64_t n_groups = (n_elem + epw - 1) / epw;
   const int CW = chain_waves_of(n);  // groups of a chain that run concurrently
+  std::vector<int64_t> gel;          // [group][lane element] -> element or -1
+  P.blocks = block_rounds >= 2 && groups_blocks(e2n, n_elem, n, epw, CW, block_rounds, gel);
+  if (P.blocks) rounds = block_rounds;
   const int CH = CW * rounds;
-  const int64_t n_chains = (n_groups + CH - 1) / CH;
+  if (!P.blocks) groups_consecutive(n_elem, epw, CH, gel);
+  const int64_t n_groups = (int64_t)gel.size() / epw;
+  const int64_t n_chains = n_groups / CH;
   auto is_bnd = [n](int r, int jj) { return r == 0 || r == n - 1 || jj == 0 || jj == n - 1; };
   // references and conformity (interior local nodes must be unique)
   std::vector<uint32_t> cnt(n_node, 0);
@@ -626,10 +360,9 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
         }
   P.conforming = conforming;
   auto shared_local = [&](int r, int jj) { return !conforming || is_bnd(r, jj); };
-  auto chain_elems = [&](int64_t ch, int64_t& e0, int64_t& e1) {
-    e0 = ch * CH * epw;
-    e1 = std::min<int64_t>(n_elem, (ch + 1) * CH * epw);
-  };
+  // the elements of chain ch, lane order
+  auto chain_elem = [&](int64_t ch, int64_t t) { return gel[(size_t)(ch * CH * epw + t)]; };
+  const int64_t chain_len = (int64_t)CH * epw;
   // 2. chain colouring
   std::vector<uint8_t> cmask(n_node, 0);
   std::vector<int> colour(n_chains);
@@ -639,11 +372,11 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
     for (int64_t ch = 0; ch < n_chains; ++ch) {
       int c = MAX_COLOURS;
       if (conforming) {
-        int64_t e0, e1;
-        chain_elems(ch, e0, e1);
         cn.clear();
         uint32_t forb = 0;
-        for (int64_t e = e0; e < e1; ++e)
+        for (int64_t t = 0; t < chain_len; ++t) {
+          const int64_t e = chain_elem(ch, t);
+          if (e < 0) continue;
           for (int r = 0; r < n; ++r)
             for (int jj = 0; jj < n; ++jj)
               if (is_bnd(r, jj)) {
@@ -654,14 +387,12 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
                   forb |= cmask[gid];
                 }
               }
+        }
         for (int q = 0; q < MAX_COLOURS; ++q)
           if (!(forb & (1u << q))) {
             c = q;
             break;
           }
-#ifdef SEM_DIAG_ONE_COLOUR
-        c = 0;  // timing-only diagnostic: racy single launch
-#endif
         if (c < MAX_COLOURS)
           for (uint32_t gid : cn) cmask[gid] |= (uint8_t)(1u << c);
       }
@@ -669,8 +400,7 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
     }
   }
   std::vector<uint8_t>().swap(cmask);
-  // 3. launch order: colour-major (one launch per colour), or for the
-  // one-launch plan the ticket order chain + colour * lag, or for the seam
+  // 3. launch order: colour-major (one launch per colour), or for the seam
   // plan element order in one launch
   std::vector<int64_t> order(n_chains);
   if (seam == 2) {  // AUTO (seam_auto): high orders, or colour classes below ~1 generation
@@ -681,7 +411,6 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
   P.seam = seam == 1 && conforming;
   for (int64_t ch = 0; ch < n_chains && P.seam; ++ch)
     if (colour[ch] >= MAX_COLOURS) P.seam = false;
-  P.df = !P.seam && df_lag > 0 && conforming && n_chains > 1;
   std::vector<uint8_t> nw;      // seam plan: chains writing each node (saturating)
   std::vector<uint16_t> smask;  // and their colours
   if (P.seam) {
@@ -692,10 +421,10 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
     std::vector<int32_t> lastc2(n_node, -1);
     int maxc = 0;
     for (int64_t ch = 0; ch < n_chains; ++ch) {
-      int64_t e0, e1;
-      chain_elems(ch, e0, e1);
       maxc = std::max(maxc, colour[ch]);
-      for (int64_t e = e0; e < e1; ++e)
+      for (int64_t t = 0; t < chain_len; ++t) {
+        const int64_t e = chain_elem(ch, t);
+        if (e < 0) continue;
         for (int r = 0; r < n; ++r)
           for (int jj = 0; jj < n; ++jj)
             if (is_bnd(r, jj)) {
@@ -706,16 +435,11 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
                 smask[gid] |= (uint16_t)(1u << colour[ch]);
               }
             }
+      }
     }
     P.seam_ns = maxc + 1;
     P.chain_colour.resize(n_chains);
     for (int64_t ch = 0; ch < n_chains; ++ch) P.chain_colour[ch] = (uint8_t)colour[ch];
-  } else if (P.df) {
-    for (int64_t ch = 0; ch < n_chains; ++ch) order[ch] = ch;
-    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
-      return a + colour[a] * df_lag < b + colour[b] * df_lag;
-    });
-    P.colour_start = {0, n_chains};
   } else {
     std::vector<int64_t> count(MAX_COLOURS + 2, 0);
     for (int64_t ch = 0; ch < n_chains; ++ch) count[colour[ch] + 1]++;
@@ -730,11 +454,15 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
   for (int64_t q = 0; q < n_chains; ++q)
     for (int i = 0; i < CH; ++i) {
       const int64_t g = order[q] * CH + i;
-      if (g >= n_groups) continue;
       const int64_t slot = q * CH + i;
-      const int fill = (int)std::min<int64_t>(epw, n_elem - g * epw);
+      int fill = 0;
+      for (int k = 0; k < epw; ++k) {
+        const int64_t e = gel[g * epw + k];
+        if (e < 0) break;  // real elements first
+        P.epos[e] = (int)(slot * epw + k);
+        fill = k + 1;
+      }
       P.slot_fill[slot] = (uint8_t)fill;
-      for (int k = 0; k < fill; ++k) P.epos[g * epw + k] = (int)(slot * epw + k);
     }
   // 4./5. validation and write codes, chain by chain in launch order
   P.mapP.assign((size_t)P.n_slots * n * lw, W_SKIP << CODE_SHIFT);
@@ -743,30 +471,43 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
     for (int64_t i = 0; i < n_node; ++i) written[i] = (node_state[i] & SEM_NODE_PRIOR) ? 1 : 0;
   std::vector<int64_t> lastc(n_node, -1);  // chain of the last touch
   std::vector<int> lastt(n_node, -1);      // (group in chain) * n * lw + pos of the last touch
-  std::vector<uint8_t> act((size_t)CH * n * lw);  // per entry: 0 normal, 1 merge-skip, 2 carry-skip, 3 carry-in
+  // per entry: 0 normal, 1 merge-skip, 2 carry-skip, 3 carry-in, 4 row carry-out
+  std::vector<uint8_t> act((size_t)CH * n * lw);
   P.n_atomic_groups = 0;
-  std::vector<int> lastq;  // one-launch plan: ticket of the last chain writing each node
-  std::vector<int> deps;
-  if (P.df) {
-    lastq.assign(n_node, -1);
-    P.dep_start.assign(n_chains + 1, 0);
-  }
+  P.row_carries = 0;
+  bool seam_conflict = false;
+  auto lane_elem = [&](int64_t g, int lane) -> int64_t {
+    const int k = lane / n;
+    return k < epw ? gel[g * epw + k] : -1;
+  };
   for (int64_t q = 0; q < n_chains; ++q) {
     const int64_t ch = order[q];
     bool atomic_chain = colour[ch] >= MAX_COLOURS;
     std::fill(act.begin(), act.end(), (uint8_t)0);
     if (!atomic_chain) {
+      // (c) row carries between consecutive rounds of a wave
+      for (int i = 0; i + CW < CH; ++i) {
+        const int64_t g = ch * CH + i;
+        for (int lane = 0; lane < lw; ++lane) {
+          const int jj = lane % n;
+          const int64_t e = lane_elem(g, lane), f = lane_elem(g + CW, lane);
+          if (e < 0 || f < 0) continue;
+          if (e2n[f * nn + jj] == e2n[e * nn + (n - 1) * n + jj])
+            act[(size_t)i * n * lw + (n - 1) * lw + lane] = 4;
+        }
+      }
       for (int i = 0; i < CH && !atomic_chain; ++i) {
         const int64_t g = ch * CH + i;
         for (int r = 0; r < n && !atomic_chain; ++r)
           for (int lane = 0; lane < lw; ++lane) {
-            const int k = lane / n, jj = lane - k * n;
-            const int64_t e = g * epw + k;
-            if (g >= n_groups || e >= n_elem) continue;
+            const int jj = lane % n;
+            const int64_t e = lane_elem(g, lane);
+            if (e < 0) continue;
             if (!shared_local(r, jj)) continue;
-            const uint32_t gid = e2n[e * nn + r * n + jj];
             const int pos = r * lw + lane;
             const int tag = i * n * lw + pos;
+            if (act[tag] == 4) continue;  // carried to the next round: not a writer
+            const uint32_t gid = e2n[e * nn + r * n + jj];
             if (lastc[gid] == ch) {
               const int pi = lastt[gid] / (n * lw), ppos = lastt[gid] % (n * lw);
               const bool same_round = (pi / CW) == (i / CW);
@@ -778,6 +519,10 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
               } else if (same_round) {
                 atomic_chain = true;
                 break;
+              } else if (P.seam && nw[gid] >= 2) {
+                // an earlier round of this chain stored the node into its
+                // seam slot: a second plain slot store would drop it
+                seam_conflict = true;
               }
               // else: an earlier round of this chain -> sequential, RMW
             }
@@ -786,18 +531,19 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
           }
       }
     }
-    int64_t e0, e1;
-    chain_elems(ch, e0, e1);
-    if (atomic_chain) P.n_atomic_groups += (e1 - e0 + epw - 1) / epw;
+    if (atomic_chain) {
+      for (int i = 0; i < CH; ++i)
+        if (gel[(ch * CH + i) * epw] >= 0) P.n_atomic_groups++;
+    }
     for (int i = 0; i < CH; ++i) {
       const int64_t g = ch * CH + i;
       uint32_t* out = P.mapP.data() + (q * CH + i) * (int64_t)n * lw;
       for (int r = 0; r < n; ++r)
         for (int lane = 0; lane < lw; ++lane) {
           const int pos = r * lw + lane;
-          const int k = lane / n, jj = lane - k * n;
-          const int64_t e = g * epw + k;
-          if (g >= n_groups || e >= n_elem) continue;  // padding stays SKIP
+          const int jj = lane % n;
+          const int64_t e = lane_elem(g, lane);
+          if (e < 0) continue;  // padding stays SKIP
           const uint32_t gid = e2n[e * nn + r * n + jj];
           const uint8_t a = act[i * n * lw + pos];
           uint32_t code;
@@ -809,6 +555,9 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
               P.zero.push_back(gid);
               written[gid] = 1;
             }
+          } else if (a == 4) {
+            code = W_ROWCARRY;
+            P.row_carries++;
           } else if (a == 1) {
             code = W_SKIP;
             out[pos - 1] |= W_MERGE << CODE_SHIFT;
@@ -823,25 +572,14 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
             if (a == 3) code |= W_CARRY;
           }
           out[pos] = gid | (code << CODE_SHIFT);
-          if (P.df && shared_local(r, jj)) {
-            if (lastq[gid] >= 0 && lastq[gid] != q) deps.push_back(lastq[gid]);
-            lastq[gid] = (int)q;
-          }
         }
-    }
-    if (P.df) {
-      std::sort(deps.begin(), deps.end());
-      deps.erase(std::unique(deps.begin(), deps.end()), deps.end());
-      P.dep_idx.insert(P.dep_idx.end(), deps.begin(), deps.end());
-      P.dep_start[q + 1] = (int)P.dep_idx.size();
-      deps.clear();
     }
   }
   for (int64_t i = 0; i < n_node; ++i)
     if (cnt[i] == 0 && (node_state.empty() || !node_state[i])) P.zero.push_back((uint32_t)i);
   std::sort(P.zero.begin(), P.zero.end());
   if (P.seam) {
-    if (P.n_atomic_groups) {  // in-round sharing the chains cannot express: no seam plan
+    if (P.n_atomic_groups || seam_conflict) {  // sharing the seam slots cannot express
       P.seam = false;
       P.seam_failed = true;  // the caller plans again without seams
       return SEM_OK;
@@ -1000,9 +738,6 @@ int build_plan_elem(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_
           c = q;
           break;
         }
-#ifdef SEM_DIAG_ONE_COLOUR
-    if (!dup) c = 0;  // timing-only diagnostic: racy single launch
-#endif
     if (c < MAX_COLOURS)
       for (uint32_t gid : cn) cmask[gid] |= (uint8_t)(1u << c);
     colour[e] = c;
@@ -1209,7 +944,6 @@ int build_plan_ecol(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_
 }
 
 }  // namespace
-
 extern "C" {
 
 int sem_ctx_create(sem_ctx** out, int p, int64_t n_elem, int64_t n_node, int dpn, int device) {
@@ -1270,10 +1004,6 @@ void sem_ctx_destroy(sem_ctx* c) {
   (void)hipFree(c->d_XG);
   (void)hipFree(c->d_owner);
   (void)hipFree(c->d_bad);
-  (void)hipFree(c->d_dep_start);
-  (void)hipFree(c->d_dep_idx);
-  (void)hipFree(c->d_df_flags);
-  (void)hipFree(c->d_df_state);
   (void)hipFree(c->d_ccol);
   (void)hipFree(c->d_seam_gid);
   (void)hipFree(c->d_seam_mask);
@@ -1289,9 +1019,9 @@ int sem_set_basis(sem_ctx* c, const double* hD, const double* hw) {
   std::memcpy(c->hw, hw, sizeof(double) * n);
   HIP_TRY(hipMemcpy(c->d_D, hD, sizeof(double) * n * n, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(c->d_w, hw, sizeof(double) * n, hipMemcpyHostToDevice));
-  hipError_t err = hipSuccess;
-  SEM_DISPATCH_N(n, upload_deo, c, &err);
-  HIP_TRY(err);
+  int rc = SEM_OK;
+  SEM_DISPATCH_N(rc, n, upload_deo, c);
+  if (rc) return rc;
   c->have_basis = true;
   return SEM_OK;
 }
@@ -1323,18 +1053,11 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
   int rounds = 1;
   if (const char* s = std::getenv("SEM_CHAIN_ROUNDS")) rounds = std::max(1, std::atoi(s));
   const bool mfma = want_mfma(c);
-  // one-launch plan of the chain kernels (SEM_DF=1; measured slower than one
-  // launch per colour on MI355X at every BASELINE configuration but p = 12,
-  // DESIGN.md §5, profiles/r02/one_launch); SEM_DF_LAG = colour lag of the
-  // ticket order, in chains
-  int64_t df_lag = 0;
-  if (!mfma) {
-    const char* e = std::getenv("SEM_DF");
-    if (e && std::atoi(e) == 1) {
-      const char* l = std::getenv("SEM_DF_LAG");
-      df_lag = l ? std::max<int64_t>(1, std::atoll(l)) : SEM_DF_LAG_DEFAULT;
-    }
-  }
+  // block layout (groups_blocks): rounds stacked along the lines, the node
+  // row between rounds carried in registers; SEM_BLOCK_ROUNDS=R forces R
+  // (0 or 1: off), default block_rounds_auto
+  int brounds = block_rounds_auto(n, c->dpn);
+  if (const char* s = std::getenv("SEM_BLOCK_ROUNDS")) brounds = std::atoi(s);
   // seam plan: one launch + seam sums; SEM_SEAM=1 / 0 forces / forbids it;
   // default AUTO (seam_auto, per dofs per node)
   int seam = 0;
@@ -1343,12 +1066,13 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
     seam = e ? (std::atoi(e) == 1 ? 1 : 0) : 2;
   }
   int rc = mfma ? build_plan_elem(h, c->n_elem, c->n_node, n, state, P)
-                : build_plan(h, c->n_elem, c->n_node, n, rounds, state, P, df_lag, seam, c->dpn);
+                : build_plan(h, c->n_elem, c->n_node, n, rounds, state, P, seam, c->dpn, brounds);
   if (!rc && P.seam_failed) {
     P = Plan();
-    rc = build_plan(h, c->n_elem, c->n_node, n, rounds, state, P, df_lag, 0);
+    rc = build_plan(h, c->n_elem, c->n_node, n, rounds, state, P, 0, c->dpn, brounds);
   }
   if (rc) return rc;
+  if (P.blocks) rounds = brounds;
   // element-coloured fallback for orders that defeat the chain patterns
   // (SEM_PLAN=1 forces it, SEM_PLAN=0 forbids it)
   const char* penv = std::getenv("SEM_PLAN");
@@ -1372,6 +1096,8 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
   c->lw = c->epw * n;
   c->n_groups = (c->n_elem + c->epw - 1) / c->epw;
   c->rounds = mfma ? 1 : rounds;
+  c->blocks = !mfma && !c->ecol && P.blocks;
+  c->row_carries = c->blocks ? P.row_carries : 0;
   c->n_slots = P.n_slots;
   std::vector<uint32_t>().swap(h);
   c->d_e2n = d_e2n;
@@ -1414,37 +1140,6 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
                       hipMemcpyHostToDevice));
   }
   c->colour_start = P.colour_start;
-  c->df = P.df;
-  c->df_lag = P.df ? df_lag : 0;
-  {
-    const char* t = std::getenv("SEM_DF_TICKET");
-    c->df_ticketed = t ? std::atoi(t) : 1;
-  }
-  c->n_deps = (int64_t)P.dep_idx.size();
-  (void)hipFree(c->d_dep_start);
-  (void)hipFree(c->d_dep_idx);
-  (void)hipFree(c->d_df_flags);
-  c->d_dep_start = nullptr;
-  c->d_dep_idx = nullptr;
-  c->d_df_flags = nullptr;
-  if (P.df) {
-    const int64_t nch = (int64_t)P.dep_start.size() - 1;
-    HIP_TRY(hipMalloc(&c->d_dep_start, P.dep_start.size() * sizeof(int)));
-    HIP_TRY(hipMemcpy(c->d_dep_start, P.dep_start.data(), P.dep_start.size() * sizeof(int),
-                      hipMemcpyHostToDevice));
-    HIP_TRY(hipMalloc(&c->d_dep_idx, std::max<size_t>(1, P.dep_idx.size()) * sizeof(int)));
-    if (!P.dep_idx.empty())
-      HIP_TRY(hipMemcpy(c->d_dep_idx, P.dep_idx.data(), P.dep_idx.size() * sizeof(int),
-                        hipMemcpyHostToDevice));
-    HIP_TRY(hipMalloc(&c->d_df_flags, nch * sizeof(uint32_t)));
-    HIP_TRY(hipMemset(c->d_df_flags, 0, nch * sizeof(uint32_t)));
-    if (!c->d_df_state) {
-      HIP_TRY(hipMalloc(&c->d_df_state, 128 * sizeof(uint32_t)));
-      HIP_TRY(hipMemset(c->d_df_state, 0, 128 * sizeof(uint32_t)));
-    }
-    // flags hold the epoch of their last action: restart both from 0
-    HIP_TRY(hipMemset(c->d_df_state, 0, 128 * sizeof(uint32_t)));
-  }
   c->seam = P.seam;
   c->seam_ns = P.seam_ns;
   c->n_seam = (int64_t)P.seam_gid.size();
@@ -1495,7 +1190,7 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
 int sem_plan_info(sem_ctx* c, int64_t* info, int n_info) {
   if (!c || !info || n_info < 1) return fail(SEM_E_INVALID, "bad arguments");
   const int64_t nc = c->colour_start.empty() ? 0 : (int64_t)c->colour_start.size() - 1;
-  constexpr int NV = 8 + MAX_COLOURS + 1 + 1 + 1 + 1 + 1 + 1 + 3;
+  constexpr int NV = 8 + MAX_COLOURS + 1 + 1 + 1 + 1 + 1 + 1 + 1 + 2;
   int64_t vals[NV] = {c->n_groups, c->n_zero, c->n_atomic_groups, c->conforming ? 1 : 0,
                       c->epw,      nc,        c->rounds,          c->n_slots};
   for (int64_t q = 0; q < nc && q <= MAX_COLOURS; ++q)
@@ -1507,23 +1202,16 @@ int sem_plan_info(sem_ctx* c, int64_t* info, int n_info) {
   // geometry, the mode sem_geom_from_nodes will resolve to
   const bool eff_nodal = c->xg_valid ? true : (c->d_GP[0] ? false : nodal_mode(c));
   vals[NV - 6] = eff_nodal ? SEM_GEOM_NODAL : SEM_GEOM_STORED;
-  // plan: chains, element-coloured, element, chains in one launch
-  vals[NV - 5] = c->mfma ? 2 : (c->ecol ? 1 : (c->df ? 3 : (c->seam ? 4 : 0)));
+  // plan: 0 chains (colour launches), 1 element-coloured chains, 2 elements
+  // (MFMA kernel), 4 chains + seam sums (3 was the retired one-launch plan)
+  vals[NV - 5] = c->mfma ? 2 : (c->ecol ? 1 : (c->seam ? 4 : 0));
   // the same for the axisymmetric Stokes block (dofs_per_node = 2)
   const bool axi_nodal =
       c->xg_axi ? true : (c->d_GP[1] ? false : nodal_mode_op(c, SEM_OP_AXISYM_STOKES));
   vals[NV - 4] = c->dpn == 2 ? (axi_nodal ? SEM_GEOM_NODAL : SEM_GEOM_STORED) : 0;
-  // one-launch plan: dependency edges, colour lag, waits that timed out so
-  // far (read from the device: synchronises with the device)
-  vals[NV - 3] = c->seam ? c->n_seam : c->n_deps;
-  vals[NV - 2] = c->df_lag;
-  vals[NV - 1] = 0;
-  if (c->df && n_info >= NV) {
-    DeviceGuard g(c->device);
-    uint32_t err = 0;
-    HIP_TRY(hipMemcpy(&err, c->d_df_state + DF_ERR, sizeof(err), hipMemcpyDeviceToHost));
-    vals[NV - 1] = err;
-  }
+  vals[NV - 3] = c->seam ? c->n_seam : 0;  // seam nodes
+  vals[NV - 2] = c->blocks ? 1 : 0;          // block layout
+  vals[NV - 1] = c->row_carries;             // entries carried between rounds
   for (int i = 0; i < n_info && i < NV; ++i) info[i] = vals[i];
   return SEM_OK;
 }
@@ -1583,8 +1271,9 @@ int sem_geom_from_nodes(sem_ctx* c, const double* d_nodes, const double* h_Vinv,
   hipStream_t st = S(stream);
   HIP_TRY(hipMemsetAsync(c->d_bad, 0, sizeof(unsigned long long), st));
   if (nodal) HIP_TRY(hipMemsetAsync(c->d_XG, 0, c->n_node * sizeof(double2), st));
-  SEM_DISPATCH_N(c->n, launch_geom_n, c, d_nodes, op_kind, GP, nullptr, nullptr, nullptr, nullptr,
-                 nullptr, nodal ? c->d_XG : nullptr, nullptr, st);
+  SEM_DISPATCH_N(rc, c->n, launch_geom_n, c, d_nodes, op_kind, GP, nullptr, nullptr, nullptr,
+                 nullptr, nullptr, nodal ? c->d_XG : nullptr, nullptr, st);
+  if (rc) return rc;
   HIP_TRY(hipGetLastError());
   unsigned long long bad = 0;
   HIP_TRY(hipMemcpyAsync(&bad, c->d_bad, sizeof(bad), hipMemcpyDeviceToHost, st));
@@ -1607,8 +1296,9 @@ int sem_geom_fields(sem_ctx* c, const double* d_nodes, const double* h_Vinv, dou
   if (rc) return rc;
   hipStream_t st = S(stream);
   HIP_TRY(hipMemsetAsync(c->d_bad, 0, sizeof(unsigned long long), st));
-  SEM_DISPATCH_N(c->n, launch_geom_n, c, d_nodes, SEM_OP_POISSON, nullptr, x_phys, J, invJ, detJ,
-                 detJxW, nullptr, nullptr, st);
+  SEM_DISPATCH_N(rc, c->n, launch_geom_n, c, d_nodes, SEM_OP_POISSON, nullptr, x_phys, J, invJ,
+                 detJ, detJxW, nullptr, nullptr, st);
+  if (rc) return rc;
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(st));
   return SEM_OK;
@@ -1669,7 +1359,8 @@ int sem_apply(sem_ctx* c, int op_kind, const double* u, double* y, int flags, vo
   if (!accumulate && !(flags & SEM_APPLY_SKIP_ZERO) && c->n_zero)
     hipLaunchKernelGGL(k_zero_list, dim3(grid_for(c->n_zero, BLOCK, 4096)), dim3(BLOCK), 0, st, y,
                        c->d_zero, c->n_zero, c->dpn);
-  SEM_DISPATCH_N(c->n, launch_apply_n, c, op_kind, u, y, accumulate, lin, st);
+  SEM_DISPATCH_N(rc, c->n, launch_apply_n, c, op_kind, u, y, accumulate, lin, st);
+  if (rc) return rc;
   HIP_TRY(hipGetLastError());
   if (lin) c->lin_valid = true;
   return SEM_OK;
@@ -1694,8 +1385,9 @@ int sem_diag(sem_ctx* c, int op_kind, double* d_diag, void* stream) {
   hipStream_t st = S(stream);
   if (!c->d_GP[0]) {  // NODAL mode: derive the stored factors once from x_phys per node
     if ((rc = ensure_gp(c, op_kind, st))) return rc;
-    SEM_DISPATCH_N(c->n, launch_geom_n, c, nullptr, SEM_OP_POISSON, c->d_GP[0], nullptr, nullptr,
-                   nullptr, nullptr, nullptr, nullptr, c->d_XG, st);
+    SEM_DISPATCH_N(rc, c->n, launch_geom_n, c, nullptr, SEM_OP_POISSON, c->d_GP[0], nullptr,
+                   nullptr, nullptr, nullptr, nullptr, nullptr, c->d_XG, st);
+    if (rc) return rc;
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipMemsetAsync(d_diag, 0, c->n_node * sizeof(double), st));

@@ -68,6 +68,9 @@ constexpr uint32_t W_SKIP = 2;    // value merged into another lane / padding
 constexpr uint32_t W_ATOMIC = 3;  // fallback
 constexpr uint32_t W_MERGE = 4;   // add the next lane's value before writing
 constexpr uint32_t W_CARRY = 8;   // add the value handed over by the previous group
+// SKIP | CARRY: row n-1 entry whose value the same lane adds to row 0 of its
+// next round (block layout): not written by this round
+constexpr uint32_t W_ROWCARRY = W_SKIP | W_CARRY;
 
 #ifndef SEM_POISSON_MIN_WAVES
 #define SEM_POISSON_MIN_WAVES 0  // 0: per-order choice (PoissonMinWaves)
@@ -146,10 +149,6 @@ template <int N>
 __device__ __forceinline__ void deo_apply(const DEO<N>& D, const double (&x)[N],
                                           double (&v)[N]) {
   constexpr int H = N / 2;
-#ifdef SEM_DIAG_NO_COMPUTE
-  for (int r = 0; r < N; ++r) v[r] = x[r] * 0.5;  // timing-only: memory/LDS floor
-  return;
-#endif
   double e[H], o[H];
 #pragma unroll
   for (int r = 0; r < H; ++r) {
@@ -183,10 +182,6 @@ template <int N>
 __device__ __forceinline__ void deo_apply_t(const DEO<N>& D, const double (&x)[N],
                                             double (&v)[N]) {
   constexpr int H = N / 2;
-#ifdef SEM_DIAG_NO_COMPUTE
-  for (int r = 0; r < N; ++r) v[r] = x[r] * 0.5;
-  return;
-#endif
   double e[H], o[H];
 #pragma unroll
   for (int r = 0; r < H; ++r) {
@@ -261,13 +256,7 @@ __device__ __forceinline__ void emit1(double* __restrict__ y, uint32_t raw, doub
     else
       *dst = accumulate ? rmw_load(dst) + v : v;
   } else if (a == W_RMW) {
-#if defined(SEM_DIAG_RMW_AS_STORE)
-    *dst = v;  // timing-only
-#elif SEM_RMW_ATOMIC
-    atomic_add_f64(dst, v);  // no writer runs concurrently: ordered, no return
-#else
     *dst = rmw_load(dst) + v;
-#endif
   } else if (a == W_ATOMIC) {
     atomic_add_f64(dst, v);
   }
@@ -280,27 +269,13 @@ __device__ __forceinline__ void emit1(double* __restrict__ y, uint32_t raw, doub
 // an earlier operator in stream order -- never a concurrent wave.
 // buffer-instruction cache policies (gfx950): nt = 2, sc1 = 16
 constexpr int CPOL_NT = 2;
-constexpr int CPOL_SC1 = 16;
 
 // y as a buffer resource: node ids are < 2^28, so byte offsets stay below
 // the 2^31-byte range, and an offset of 2^31 reads 0 with no memory traffic
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t y_rsrc(const double* y) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(y), 0, 0x80000000, 0x00020000);
 }
-typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-// one-launch plan (DFPlan below): every y access that another workgroup may
-// follow is agent-coherent -- sc1 stores (written through, line dropped
-// from the XCD's L2) and sc1 loads (MI355X_MICROARCH.md, inter-workgroup
-// visibility, hand-off table row 1)
-__device__ __forceinline__ double y_load_sc1(const double* y, uint32_t gid) {
-  return __builtin_bit_cast(double,
-                            __builtin_amdgcn_raw_buffer_load_b64(y_rsrc(y), gid * 8u, 0, CPOL_SC1));
-}
-__device__ __forceinline__ void y_store_sc1(double* y, uint32_t gid, double v) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), y_rsrc(y), gid * 8u, 0,
-                                        CPOL_SC1);
-}
 
 template <int N, int AUX = CPOL_NT>
 __device__ __forceinline__ void rmw_prefetch(const double* __restrict__ y,
@@ -318,14 +293,10 @@ __device__ __forceinline__ void rmw_prefetch(const double* __restrict__ y,
   }
 }
 
-template <bool DF = false>
 __device__ __forceinline__ void emit1p(double* __restrict__ y, uint32_t raw, double v, double prev) {
   const uint32_t a = (raw >> CODE_SHIFT) & 3u;
   double* dst = y + (raw & GID_MASK);
   if (a == W_STORE || a == W_RMW) {  // prev = 0 for a first writer in overwrite mode
-    if constexpr (DF)
-      y_store_sc1(y, raw & GID_MASK, prev + v);
-    else
 #if SEM_NT_STORE
       __builtin_nontemporal_store(prev + v, dst);
 #else
@@ -335,6 +306,20 @@ __device__ __forceinline__ void emit1p(double* __restrict__ y, uint32_t raw, dou
     atomic_add_f64(dst, v);
   }
 }
+
+// read-modify-write prefetch policy of a chain kernel: colour launches
+// prefetch the operands, the seam plan has none (no read-modify-writes
+// between chains)
+struct NoWait {
+  static constexpr int aux = CPOL_NT;
+  static constexpr bool prefetch = true;
+  __device__ void operator()() const {}
+};
+struct NoPrefetch {
+  static constexpr int aux = CPOL_NT;
+  static constexpr bool prefetch = false;
+  __device__ void operator()() const {}
+};
 
 // Seam plan: a node written by several chains is not
 // read-modified-written in colour order; each chain stores its partial sum
@@ -359,130 +344,6 @@ __device__ __forceinline__ void emit1_seam(double* __restrict__ y, uint32_t raw,
     __builtin_nontemporal_store(v, so.base + gid);
 }
 
-// emit1 of the one-launch plan (no prefetch): sc1 operand loads and stores
-__device__ __forceinline__ void emit1_df(double* __restrict__ y, uint32_t raw, double v,
-                                         int accumulate) {
-  const uint32_t a = (raw >> CODE_SHIFT) & 3u;
-  const uint32_t gid = raw & GID_MASK;
-  if (a == W_STORE)
-    y_store_sc1(y, gid, accumulate ? y_load_sc1(y, gid) + v : v);
-  else if (a == W_RMW)
-    y_store_sc1(y, gid, y_load_sc1(y, gid) + v);
-  else if (a == W_ATOMIC)
-    atomic_add_f64(y + gid, v);
-}
-
-// ---------------------------------------------------------------------------
-// One-launch ("dataflow") plan of the Poisson column kernel.
-// All chains run in ONE launch instead of one launch per colour.  A
-// workgroup takes the next chain from a ticket counter (so a chain is only
-// ever waited on by chains with later tickets: the grid cannot deadlock
-// whatever the dispatch order), and before it starts it waits until every
-// chain that wrote one of its shared nodes earlier in ticket order has
-// published: per-chain flag = the action's epoch, written
-// by one lane after every wave's stores drained and a workgroup barrier.
-// The write codes are those of the ticket order, so each node still has
-// exactly one writer at a time and its writers run in a fixed order
-// (bitwise-deterministic results).  The ticket order interleaves colours
-// with a lag: chain key = chain index + colour * lag, so a chain's
-// lower-coloured neighbours were taken about `lag` tickets earlier
-// (finished, and their shared u / x_phys lines recently read).
-// state[0] = ticket counter, state[DF_EPOCH] = epoch (both advanced by
-// k_df_begin before every launch), state[DF_ERR] = waits that timed out.
-// ---------------------------------------------------------------------------
-constexpr int DF_EPOCH = 32;  // separate 128-B lines
-constexpr int DF_ERR = 64;
-#ifndef SEM_DF_SPIN_LIMIT
-#define SEM_DF_SPIN_LIMIT (1 << 22)
-#endif
-struct DFPlan {
-  const int* __restrict__ dep_start;  // [chain + 1]
-  const int* __restrict__ dep_idx;    // earlier-ticket chains this chain follows
-  uint32_t* flags;                    // [chain] = epoch once the chain's y writes are out
-  uint32_t* state;
-  int ticketed;                       // 0: chain = blockIdx (timing experiments only)
-};
-typedef __attribute__((address_space(1))) uint32_t g_u32;
-
-__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
-  return __hip_atomic_load((g_u32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// wave-level wait (each wave polls for itself, then issues its own sc1
-// loads of the handed-off y entries)
-__device__ __forceinline__ void df_wait(const DFPlan& df, int64_t chain, uint32_t epoch) {
-  const int d0 = df.dep_start[chain], d1 = df.dep_start[chain + 1];
-  const int lane = threadIdx.x % WAVE;
-  for (int b = d0; b < d1; b += WAVE) {
-    const int i = b + lane;
-    const bool mine = i < d1;
-    const uint32_t* f = df.flags + (mine ? df.dep_idx[i] : 0);
-    for (int s = 0;; ++s) {
-      const bool ok = !mine || ld_agent(f) == epoch;
-      if (__all(ok)) break;
-      if (s >= SEM_DF_SPIN_LIMIT) {  // never expected: count it, do not hang
-        if (lane == 0)
-          __hip_atomic_fetch_add(df.state + DF_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(4);
-    }
-  }
-}
-
-struct NoWait {
-  static constexpr int aux = CPOL_NT;
-  static constexpr bool prefetch = true;
-  __device__ void operator()() const {}
-};
-// seam plan: nothing to prefetch (no read-modify-writes between chains)
-struct NoPrefetch {
-  static constexpr int aux = CPOL_NT;
-  static constexpr bool prefetch = false;
-  __device__ void operator()() const {}
-};
-// the one-launch plan waits in the kernel's prologue, with nothing live
-// (waiting just before the read-modify-writes instead kept the plan's
-// pointers live through the contractions: 30 VGPRs spilled at p = 8); its
-// read-modify-write operands are read sc1
-struct DFWait {
-  static constexpr int aux = CPOL_SC1;
-  static constexpr bool prefetch = true;
-  __device__ void operator()() const {}
-};
-
-// prologue / epilogue of a one-launch chain kernel (s: the kernel's LDS)
-struct DFShared {
-  int ticket;
-  uint32_t epoch;
-};
-__device__ __forceinline__ int64_t df_take(const DFPlan& df, int64_t c0, int64_t c1,
-                                           DFShared& s) {
-  if (threadIdx.x == 0) {
-    s.ticket = df.ticketed ? (int)__hip_atomic_fetch_add(df.state, 1u, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT)
-                           : (int)blockIdx.x;
-    s.epoch = ld_agent(df.state + DF_EPOCH);
-  }
-  __syncthreads();
-  const int64_t chain = c0 + s.ticket;
-  if (chain < c1) df_wait(df, chain, s.epoch);
-  return chain;
-}
-// publish: every wave's y writes have left the CU, then one lane flags the
-// chain (hand-off table row 1: sc1 stores, vmcnt(0) in every storing wave,
-// workgroup barrier, one sc1 flag store); chain and epoch re-read from LDS so
-// nothing stays live through the kernel body
-__device__ __forceinline__ void df_publish(const DFPlan& df, int64_t c0, DFShared& s) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const volatile DFShared* vs = &s;
-    __hip_atomic_store((g_u32*)(df.flags + c0 + vs->ticket), vs->epoch, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 __device__ __forceinline__ void emit2(double* __restrict__ y, uint32_t raw, double v0, double v1,
                                       int accumulate) {
   const uint32_t a = (raw >> CODE_SHIFT) & 3u;
@@ -492,29 +353,6 @@ __device__ __forceinline__ void emit2(double* __restrict__ y, uint32_t raw, doub
   } else if (a == W_STORE || a == W_RMW) {
     const double o0 = rmw_load(dst), o1 = rmw_load(dst + 1);
     *reinterpret_cast<double2*>(dst) = make_double2(o0 + v0, o1 + v1);
-  } else if (a == W_ATOMIC) {
-    atomic_add_f64(dst, v0);
-    atomic_add_f64(dst + 1, v1);
-  }
-}
-
-// emit2 of the one-launch plan: sc1 operand loads and 16-B sc1 stores
-__device__ __forceinline__ void emit2_df(double* __restrict__ y, uint32_t raw, double v0,
-                                         double v1, int accumulate) {
-  const uint32_t a = (raw >> CODE_SHIFT) & 3u;
-  const uint32_t gid = raw & GID_MASK;
-  double* dst = y + 2 * (int64_t)gid;
-  if (a == W_STORE || a == W_RMW) {
-    const __amdgpu_buffer_rsrc_t ry = y_rsrc(y);
-    const uint32_t off = gid * 16u;
-    if (a == W_RMW || accumulate) {
-      const u32x4 o = __builtin_amdgcn_raw_buffer_load_b128(ry, off, 0, CPOL_SC1);
-      const double2 od = __builtin_bit_cast(double2, o);
-      v0 += od.x;
-      v1 += od.y;
-    }
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(v0, v1)), ry,
-                                           off, 0, CPOL_SC1);
   } else if (a == W_ATOMIC) {
     atomic_add_f64(dst, v0);
     atomic_add_f64(dst + 1, v1);
@@ -566,9 +404,6 @@ __device__ __forceinline__ void store_row(double* L, int i, const double (&t)[N]
 #endif
 #ifndef SEM_NODAL_EARLY_U
 #define SEM_NODAL_EARLY_U 0
-#endif
-#ifndef SEM_RMW_ATOMIC
-#define SEM_RMW_ATOMIC 0
 #endif
 template <int N, bool PAD = true>
 struct Tile {
@@ -678,11 +513,7 @@ __device__ __forceinline__ void poisson_group_stored(const MapRef& mref,
   load_map<N, M16>(mref, g, lane, in_wave, raw);
 #pragma unroll
   for (int r = 0; r < N; ++r) {
-#ifdef SEM_DIAG_NO_U
-    uc[r] = (double)(raw[r] & 7u);  // timing-only: no u gather
-#else
     uc[r] = u[raw[r] & GID_MASK];
-#endif
   }
   // column j: d0[m][j] = sum_r D[m][r] u[r][j]     (TensorProduct.deriv dim 0)
   double d0[N];
@@ -698,13 +529,9 @@ __device__ __forceinline__ void poisson_group_stored(const MapRef& mref,
 #pragma unroll
     for (int m = 0; m < N; ++m) {
       const double d1 = L[m * RS + j];
-#if defined(SEM_DIAG_NO_G)
-      const double g00 = 1.0 + m, g01 = 0.25 * j, g11 = 2.0;  // timing-only
-#else
       const double g00 = gp[(0 * N + m) * LW];
       const double g01 = gp[(1 * N + m) * LW];
       const double g11 = gp[(2 * N + m) * LW];
-#endif
       w0[m] = fma(g00, d0[m], g01 * d1);
       L[m * RS + j] = fma(g01, d0[m], g11 * d1);  // w1, same lane's slot
     }
@@ -755,11 +582,7 @@ __device__ __forceinline__ void gather_x(const double2* __restrict__ XG, const u
                                          int j, double2 (&xc)[N]) {
 #pragma unroll
   for (int r = 0; r < N; ++r) {
-#ifdef SEM_DIAG_NO_X
-    xc[r] = make_double2(0.01 * (raw[r] & 15u) + j, 0.02 * r + (raw[r] & 3u));  // timing-only
-#else
     xc[r] = XG[raw[r] & GID_MASK];
-#endif
   }
 }
 
@@ -768,11 +591,7 @@ __device__ __forceinline__ void gather_u(const double* __restrict__ u, const uin
                                          double (&uc)[N]) {
 #pragma unroll
   for (int r = 0; r < N; ++r) {
-#ifdef SEM_DIAG_NO_U
-    uc[r] = (double)(raw[r] & 7u);  // timing-only: no u gather
-#else
     uc[r] = u[raw[r] & GID_MASK];
-#endif
   }
 }
 
@@ -897,14 +716,23 @@ __device__ __forceinline__ void poisson_group_nodal(const MapRef& mref,
 // Scatter of one group's column values through the coded map, with the
 // in-group merge (next lane) and the chain carry (previous group) applied.
 // ncomp values per node (1: Poisson, 2: axisymmetric block).
-template <int N, int NC, bool PRE = false, int CW = ChainWaves<N>::value, bool DF = false,
-          bool SEAM = false>
+template <int N, int NC, bool PRE = false, int CW = ChainWaves<N>::value, bool SEAM = false>
 __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_t (&raw)[N],
                                            double (&v)[NC][N], int lane, int wave, int rd,
                                            bool in_wave, double (*carry)[CW][NC][N],
-                                           int accumulate, const double* prev = nullptr,
+                                           double (&rowc)[NC], int accumulate,
+                                           const double* prev = nullptr,
                                            const SeamOut& so = SeamOut()) {
   constexpr int LW = Tile<N>::LW;
+  // row carry between rounds (block layout): before any merge, row 0 takes
+  // the row n-1 value this lane held back in the previous round
+  const bool rc_out = (raw[N - 1] >> CODE_SHIFT) == W_ROWCARRY;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const double out = rc_out ? v[c][N - 1] : 0.0;
+    v[c][0] += rowc[c];
+    rowc[c] = out;
+  }
 #pragma unroll
   for (int c = 0; c < NC; ++c)
 #pragma unroll
@@ -912,7 +740,6 @@ __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_
       const double vn = __shfl_down(v[c][p], 1, WAVE);
       if ((raw[p] >> CODE_SHIFT) & W_MERGE) v[c][p] += vn;
     }
-#ifndef SEM_DIAG_NO_SYNC
   // hand the last lane's column to the next group of the chain
   if (lane == LW - 1) {
 #pragma unroll
@@ -931,20 +758,15 @@ __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_
         for (int c = 0; c < NC; ++c) v[c][p] += src[c * N + p];
       }
   }
-#endif
   if (in_wave) {
 #pragma unroll
     for (int p = 0; p < N; ++p) {
       if constexpr (SEAM && NC == 1)
         emit1_seam(y, raw[p], v[0][p], accumulate, so);
       else if constexpr (PRE)
-        emit1p<DF>(y, raw[p], v[0][p], prev[p]);
-      else if (DF && NC == 1)
-        emit1_df(y, raw[p], v[0][p], accumulate);
+        emit1p(y, raw[p], v[0][p], prev[p]);
       else if (NC == 1)
         emit1(y, raw[p], v[0][p], accumulate);
-      else if (DF)
-        emit2_df(y, raw[p], v[0][p], v[NC - 1][p], accumulate);
       else if (SEAM && ((raw[p] >> CODE_SHIFT) & 3u) == W_ATOMIC)  // seam slot (2 DOFs)
         reinterpret_cast<double2*>(so.base)[raw[p] & GID_MASK] =
             make_double2(v[0][p], v[NC - 1][p]);
@@ -952,10 +774,8 @@ __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_
         emit2(y, raw[p], v[0][p], v[NC - 1][p], accumulate);
     }
   }
-#ifndef SEM_DIAG_NO_SYNC
   // this round's stores and carry reads complete before the next round
   __syncthreads();
-#endif
 }
 
 // Workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8 share
@@ -995,19 +815,18 @@ struct SeamPlan {
   int64_t n_node;
 };
 
-template <int N, bool NODAL, bool M16, bool DF = false, bool SEAM = false>
+template <int N, bool NODAL, bool M16, bool SEAM = false>
 __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODAL>::value))
     k_poisson_apply(const MapRef mref, const double* __restrict__ GP,
                     const double2* __restrict__ XG, const double* __restrict__ u,
                     double* __restrict__ y, int64_t c0, int64_t c1, int rounds, int accumulate,
-                    const DEO<N> D, const WVec<N> w, const DFPlan df, const SeamPlan sp) {
+                    const DEO<N> D, const WVec<N> w, const SeamPlan sp) {
   using T = Tile<N, NODAL ? SEM_TILE_PAD_NODAL : SEM_TILE_PAD_STORED>;
   constexpr int NT = NODAL ? 2 : 1;  // tiles per element slot
   __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * T::ES * NT];
   constexpr int CW = ChainWaves<N>::value;
   __shared__ double carry[2][CW][1][N];
-  __shared__ DFShared sdf;
-  const int64_t chain = DF ? df_take(df, c0, c1, sdf) : c0 + xcd_block(blockIdx.x, gridDim.x);
+  const int64_t chain = c0 + xcd_block(blockIdx.x, gridDim.x);
   if (chain >= c1) return;  // uniform over the workgroup
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);  // provably uniform
   const int lane = threadIdx.x % WAVE;
@@ -1020,12 +839,12 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
   double* L = lds + T::slot(wave, k, in_wave) * T::ES;
   double* LB = L + (NT - 1) * T::TILE_SLOTS * T::ES;
   const double wj = pick<N>(w, j);
+  double rowc[1] = {0.0};
   for (int rd = 0; rd < rounds; ++rd) {
     const int64_t g = (chain * rounds + rd) * CW + wave;
     uint32_t raw[N];
     double v[1][N], prev[N];
-    using Pre = typename std::conditional<DF, DFWait,
-                                          typename std::conditional<SEAM, NoPrefetch, NoWait>::type>::type;
+    using Pre = typename std::conditional<SEAM, NoPrefetch, NoWait>::type;
     const Pre pre{};
     constexpr bool PRE = RmwPrefetch<N>::value > 0 && Pre::prefetch;
     if constexpr (NODAL)
@@ -1034,16 +853,11 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
     else
       poisson_group_stored<N, M16>(mref, GP, u, g, lane, j, in_wave, L, D, raw, v[0], y,
                                    accumulate, prev, pre);
-#ifdef SEM_DIAG_NO_STORE
-    if (in_wave && v[0][0] == 1234.5678) y[0] = v[0][1];  // timing-only
-#else
     SeamOut so;
     if constexpr (SEAM) so.base = sp.buf + sp.colour[chain] * sp.n_node;
-    chain_emit<N, 1, PRE, CW, DF, SEAM>(y, raw, v, lane, wave, rd, in_wave, carry, accumulate,
+    chain_emit<N, 1, PRE, CW, SEAM>(y, raw, v, lane, wave, rd, in_wave, carry, rowc, accumulate,
                                         prev, so);
-#endif
   }
-  if constexpr (DF) df_publish(df, c0, sdf);
 }
 
 // second launch of the seam plan: y[gid] (+)= the colour slots, in colour
@@ -1109,14 +923,6 @@ __global__ void k_seam_sum(double* __restrict__ y, const uint32_t* __restrict__ 
         first = false;
       }
     y[g] = s;
-  }
-}
-
-// before every one-launch action: ticket counter to 0, next epoch
-__global__ void k_df_begin(uint32_t* state) {
-  if (threadIdx.x == 0) {
-    __hip_atomic_exchange(state, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(state + DF_EPOCH, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1442,17 +1248,16 @@ __device__ __forceinline__ void axisym_group_nodal(const MapRef& mref,
   wave_sync();
 }
 
-template <int N, bool M16, bool DF = false, bool SEAM = false>
+template <int N, bool M16, bool SEAM = false>
 __global__ void __launch_bounds__(ChainWaves<N>::block, SEM_AXI_MIN_WAVES)
     k_axisym_nodal(const MapRef mref, const double2* __restrict__ XG, const double* __restrict__ u,
                    double* __restrict__ y, int64_t c0, int64_t c1, int rounds, int accumulate,
-                   const DEO<N> D, const WVec<N> w, const DFPlan df, const SeamPlan sp) {
+                   const DEO<N> D, const WVec<N> w, const SeamPlan sp) {
   using T = Tile<N>;
   __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * 2 * T::ES];
   constexpr int CW = ChainWaves<N>::value;
   __shared__ double carry[2][CW][2][N];
-  __shared__ DFShared sdf;
-  const int64_t chain = DF ? df_take(df, c0, c1, sdf) : c0 + blockIdx.x;
+  const int64_t chain = c0 + blockIdx.x;
   if (chain >= c1) return;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   const int lane = threadIdx.x % WAVE;
@@ -1462,6 +1267,7 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, SEM_AXI_MIN_WAVES)
   const double wj = pick<N>(w, j);
   double* LP = lds + T::slot(wave, k, in_wave) * T::ES;
   double* LO = LP + T::TILE_SLOTS * T::ES;
+  double rowc[2] = {0.0, 0.0};
   for (int rd = 0; rd < rounds; ++rd) {
     const int64_t g = (chain * rounds + rd) * CW + wave;
     uint32_t raw[N];
@@ -1470,24 +1276,22 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, SEM_AXI_MIN_WAVES)
                                v[1]);
     SeamOut so;
     if constexpr (SEAM) so.base = sp.buf + sp.colour[chain] * sp.n_node * 2;
-    chain_emit<N, 2, false, CW, DF, SEAM>(y, raw, v, lane, wave, rd, in_wave, carry, accumulate,
+    chain_emit<N, 2, false, CW, SEAM>(y, raw, v, lane, wave, rd, in_wave, carry, rowc, accumulate,
                                           nullptr, so);
   }
-  if constexpr (DF) df_publish(df, c0, sdf);
 }
 
-template <int N, int MODE, bool DF = false, bool SEAM = false>
+template <int N, int MODE, bool SEAM = false>
 __global__ void __launch_bounds__(ChainWaves<N>::block)
     k_axisym_apply(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
                    const double* __restrict__ u, double* __restrict__ y, int64_t c0, int64_t c1,
                    int rounds, int accumulate, const DEO<N> D, const WVec<N> w, const AxiNS ns,
-                   const DFPlan df, const SeamPlan sp) {
+                   const SeamPlan sp) {
   using T = Tile<N>;
   __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * 2 * T::ES];
   constexpr int CW = ChainWaves<N>::value;
   __shared__ double carry[2][CW][2][N];
-  __shared__ DFShared sdf;
-  const int64_t chain = DF ? df_take(df, c0, c1, sdf) : c0 + blockIdx.x;
+  const int64_t chain = c0 + blockIdx.x;
   if (chain >= c1) return;
   const int wave = threadIdx.x / WAVE;
   const int lane = threadIdx.x % WAVE;
@@ -1497,6 +1301,7 @@ __global__ void __launch_bounds__(ChainWaves<N>::block)
   const double wj = pick<N>(w, j);
   double* LP = lds + T::slot(wave, k, in_wave) * T::ES;  // psi tile plane
   double* LO = LP + T::TILE_SLOTS * T::ES;                // omega tile plane
+  double rowc[2] = {0.0, 0.0};
   for (int rd = 0; rd < rounds; ++rd) {
     const int64_t g = (chain * rounds + rd) * CW + wave;
     uint32_t raw[N];
@@ -1505,10 +1310,9 @@ __global__ void __launch_bounds__(ChainWaves<N>::block)
                           v[1]);
     SeamOut so;
     if constexpr (SEAM) so.base = sp.buf + sp.colour[chain] * sp.n_node * 2;
-    chain_emit<N, 2, false, CW, DF, SEAM>(y, raw, v, lane, wave, rd, in_wave, carry, accumulate,
+    chain_emit<N, 2, false, CW, SEAM>(y, raw, v, lane, wave, rd, in_wave, carry, rowc, accumulate,
                                           nullptr, so);
   }
-  if constexpr (DF) df_publish(df, c0, sdf);
 }
 
 // ---------------------------------------------------------------------------
@@ -1709,6 +1513,34 @@ struct GeomShape {
   static constexpr int THREADS = ((EPB * NN + 63) / 64) * 64;
 };
 
+// Error-free transformations for the compensated equispaced->GLL transform:
+// a*b = p + e exactly, a + b = s + e exactly (round to nearest, no fast-math).
+__device__ __forceinline__ void two_prod(double a, double b, double& p, double& e) {
+  p = a * b;
+  e = fma(a, b, -p);
+}
+__device__ __forceinline__ void two_sum(double a, double b, double& s, double& e) {
+  s = a + b;
+  const double bb = s - a;
+  e = (a - (s - bb)) + (b - bb);
+}
+// s_hi + s_lo ~= s_hi_in + sum_i a[i*sa] * (bh[i*sb] + bl[i*sb]) to about twice
+// the working precision (Ogita-Rump-Oishi Dot2; the lo parts enter plainly).
+template <int N>
+__device__ __forceinline__ void dot2(const double* a, int sa, const double* bh, const double* bl,
+                                     int sb, double& hi, double& lo) {
+  double s = 0.0, c = 0.0;
+  for (int i = 0; i < N; ++i) {
+    double p, ep, es;
+    two_prod(a[i * sa], bh[i * sb], p, ep);
+    two_sum(s, p, s, es);
+    c += ep + es;
+    if (bl) c = fma(a[i * sa], bl[i * sb], c);
+  }
+  hi = s + c;
+  lo = c - (hi - s);
+}
+
 template <int N>
 __global__ void __launch_bounds__(GeomShape<N>::THREADS)
     k_geometry(const double* __restrict__ nodes, int64_t n_node, const uint32_t* __restrict__ e2n,
@@ -1723,7 +1555,7 @@ __global__ void __launch_bounds__(GeomShape<N>::THREADS)
   constexpr int EPB = S::EPB;
   const int LW = epw * N;  // packed row: the epw elements of a group (1 for the MFMA kernel)
   __shared__ double sV[NN], sD[NN], sw[N];
-  __shared__ double sx[EPB][2][NN], st[EPB][2][NN];
+  __shared__ double sx[EPB][2][NN], st[EPB][2][NN], stl[EPB][2][NN];
   const int tid = threadIdx.x;
   for (int i = tid; i < NN; i += blockDim.x) {
     sV[i] = gVinv[i];
@@ -1753,14 +1585,22 @@ __global__ void __launch_bounds__(GeomShape<N>::THREADS)
   // evaluated on coordinates relative to the element's node (0,0): the map
   // is translation invariant (V_eq reproduces constants) and J = D x_phys
   // then no longer cancels the O(1) offset against O(h) variations.
+  // Both passes are compensated dot products (dot2, the intermediate kept as
+  // hi + lo): Vinv has entries up to ~170 at p = 16 (cond(V_eq) ~ 1e5), and
+  // J = D x_phys amplifies the rounding of plain float64 sums by ~n^2/4;
+  // measured on CPU emulation at p = 16: 6.8e-11 -> 1.2e-11 rel-L2 of the
+  // action against the extended-precision oracle.
   double x0[2] = {0.0, 0.0};
   if (act && !XGin) {
     x0[0] = sx[el][0][0];
     x0[1] = sx[el][1][0];
     for (int c = 0; c < 2; ++c) {
-      double a = 0.0;
-      for (int i = 0; i < N; ++i) a = fma(sV[m * N + i], sx[el][c][i * N + nq] - x0[c], a);
-      st[el][c][node] = a;
+      double xr[N];
+      for (int i = 0; i < N; ++i) xr[i] = sx[el][c][i * N + nq] - x0[c];
+      double hi, lo;
+      dot2<N>(&sV[m * N], 1, xr, nullptr, 1, hi, lo);
+      st[el][c][node] = hi;
+      stl[el][c][node] = lo;
     }
   }
   __syncthreads();
@@ -1772,9 +1612,9 @@ __global__ void __launch_bounds__(GeomShape<N>::THREADS)
     xp[1] = sx[el][1][node] - x0[1];
   } else if (act) {
     for (int c = 0; c < 2; ++c) {
-      double a = 0.0;
-      for (int jj = 0; jj < N; ++jj) a = fma(sV[nq * N + jj], st[el][c][m * N + jj], a);
-      xp[c] = a;
+      double hi, lo;
+      dot2<N>(&sV[nq * N], 1, &st[el][c][m * N], &stl[el][c][m * N], 1, hi, lo);
+      xp[c] = hi;
     }
   }
   __syncthreads();

@@ -1,0 +1,173 @@
+// Per-order launch unit of libsem_hip.so: the kernel instantiations of
+// sem_kernels.h for the orders n in [SEM_N_LO, SEM_N_HI] (the build compiles
+// this file once per range, in parallel; spectralelementmethod_amd/_build.py).
+#include "sem_ctx.h"
+
+#ifndef SEM_N_LO
+#define SEM_N_LO 2
+#endif
+#ifndef SEM_N_HI
+#define SEM_N_HI 17
+#endif
+
+namespace semd {
+
+// one chain-kernel launch: a colour class, or every chain of the seam plan
+template <int N, bool SEAM>
+void launch_chains(sem_ctx* c, int op_kind, bool nodal, const double* u, double* y, int acc,
+                   bool lin, int64_t c0, int64_t c1, const DEO<N>& D, const WVec<N>& w,
+                   hipStream_t st) {
+  const dim3 g((unsigned)(c1 - c0)), b(ChainWaves<N>::block);
+  const MapRef mr{c->d_mapP, c->d_map16, c->d_mbase};
+  const int R = c->rounds;
+  const SeamPlan sp{c->d_ccol, c->d_seam_buf, c->n_node};
+  if (op_kind == SEM_OP_POISSON) {
+    const double* GP = nodal ? nullptr : c->d_GP[0];
+    const double2* XG = nodal ? c->d_XG : nullptr;
+    if (nodal && c->map16)
+      hipLaunchKernelGGL((k_poisson_apply<N, true, true, SEAM>), g, b, 0, st, mr, GP, XG, u, y, c0,
+                         c1, R, acc, D, w, sp);
+    else if (nodal)
+      hipLaunchKernelGGL((k_poisson_apply<N, true, false, SEAM>), g, b, 0, st, mr, GP, XG, u, y, c0,
+                         c1, R, acc, D, w, sp);
+    else if (c->map16)
+      hipLaunchKernelGGL((k_poisson_apply<N, false, true, SEAM>), g, b, 0, st, mr, GP, XG, u, y, c0,
+                         c1, R, acc, D, w, sp);
+    else
+      hipLaunchKernelGGL((k_poisson_apply<N, false, false, SEAM>), g, b, 0, st, mr, GP, XG, u, y,
+                         c0, c1, R, acc, D, w, sp);
+  } else if (op_kind == SEM_OP_AXISYM_STOKES && nodal) {
+    if (c->map16)
+      hipLaunchKernelGGL((k_axisym_nodal<N, true, SEAM>), g, b, 0, st, mr, c->d_XG, u, y, c0, c1,
+                         R, acc, D, w, sp);
+    else
+      hipLaunchKernelGGL((k_axisym_nodal<N, false, SEAM>), g, b, 0, st, mr, c->d_XG, u, y, c0, c1,
+                         R, acc, D, w, sp);
+  } else if (op_kind == SEM_OP_AXISYM_STOKES) {
+    hipLaunchKernelGGL((k_axisym_apply<N, 0, SEAM>), g, b, 0, st, c->d_mapP, c->d_GP[1], u, y, c0,
+                       c1, R, acc, D, w, AxiNS(), sp);
+  } else {
+    AxiNS ns;
+    ns.re = c->reynolds;
+    ns.lin = (op_kind == SEM_OP_AXISYM_NS_JVP || lin) ? c->d_lin : nullptr;
+    if (op_kind == SEM_OP_AXISYM_NS)
+      hipLaunchKernelGGL((k_axisym_apply<N, 1, SEAM>), g, b, 0, st, c->d_mapP, c->d_GP[2], u, y,
+                         c0, c1, R, acc, D, w, ns, sp);
+    else
+      hipLaunchKernelGGL((k_axisym_apply<N, 2, SEAM>), g, b, 0, st, c->d_mapP, c->d_GP[2], u, y,
+                         c0, c1, R, acc, D, w, ns, sp);
+  }
+}
+
+template <int N>
+int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc, bool lin,
+                   hipStream_t st) {
+  const DEO<N> D = make_deo<N>(c);
+  WVec<N> w;
+  std::memcpy(w.v, c->hw, sizeof(w.v));
+  const bool nodal = use_nodal(c, op_kind);
+  if (c->seam) {  // one launch + the seam sums (SeamPlan)
+    launch_chains<N, true>(c, op_kind, nodal, u, y, acc, lin, c->colour_start.front(),
+                           c->colour_start.back(), D, w, st);
+    return launch_seam_sum(c, y, acc, st);
+  }
+  const size_t nc = c->colour_start.size() - 1;
+  for (size_t k = 0; k < nc; ++k) {
+    const int64_t c0 = c->colour_start[k], c1 = c->colour_start[k + 1];
+    if (c1 <= c0) continue;
+    if (op_kind == SEM_OP_POISSON && c->mfma) {
+      if constexpr (N <= 16) {
+        constexpr int per_block = MFMA_EPB * (16 / N) * (16 / N);
+        const dim3 g((unsigned)((c1 - c0 + per_block - 1) / per_block));
+        if (nodal)
+          hipLaunchKernelGGL((k_poisson_mfma<N, true>), g, dim3(BLOCK), 0, st, c->d_mapP, nullptr,
+                             c->d_XG, u, y, c->d_D, w, c0, c1, acc);
+        else
+          hipLaunchKernelGGL((k_poisson_mfma<N, false>), g, dim3(BLOCK), 0, st, c->d_mapP,
+                             c->d_GP[0], nullptr, u, y, c->d_D, w, c0, c1, acc);
+      } else {
+        return sem::fail(SEM_E_NOTIMPL, "the MFMA kernel needs n <= 16");
+      }
+    } else {
+      launch_chains<N, false>(c, op_kind, nodal, u, y, acc, lin, c0, c1, D, w, st);
+    }
+  }
+  return SEM_OK;
+}
+
+// nodes -> factors/fields (XGin null), or XGin (x_phys per node) -> factors
+template <int N>
+int launch_geom_n(sem_ctx* c, const double* nodes, int op_kind, double* GP, double* xph,
+                  double* J, double* iJ, double* dJ, double* dJW, double2* XG,
+                  const double2* XGin, hipStream_t st) {
+  using Sh = GeomShape<N>;
+  const int grid = (int)((c->n_elem + Sh::EPB - 1) / Sh::EPB);
+  hipLaunchKernelGGL((k_geometry<N>), dim3(grid), dim3(Sh::THREADS), 0, st, nodes, c->n_node,
+                     c->d_e2n, c->n_elem, c->d_Vinv, c->d_D, c->d_w, op_kind, c->epw, c->d_epos, GP,
+                     xph, J, iJ, dJ, dJW, XG, XG ? c->d_owner : nullptr, XGin, c->d_bad);
+  return SEM_OK;
+}
+
+template <int N>
+int upload_deo(sem_ctx* c) {
+  const DEOData<N> d = make_deo_data<N>(c->hD);
+  HIP_TRY(hipMemcpy(c->d_deo, &d, sizeof(d), hipMemcpyHostToDevice));
+  return SEM_OK;
+}
+
+#define SEM_INSTANTIATE(N)                                                                     \
+  template int launch_apply_n<N>(sem_ctx*, int, const double*, double*, int, bool, hipStream_t); \
+  template int launch_geom_n<N>(sem_ctx*, const double*, int, double*, double*, double*, double*, \
+                                double*, double*, double2*, const double2*, hipStream_t);        \
+  template int upload_deo<N>(sem_ctx*);
+
+#if SEM_N_LO <= 2 && 2 <= SEM_N_HI
+SEM_INSTANTIATE(2)
+#endif
+#if SEM_N_LO <= 3 && 3 <= SEM_N_HI
+SEM_INSTANTIATE(3)
+#endif
+#if SEM_N_LO <= 4 && 4 <= SEM_N_HI
+SEM_INSTANTIATE(4)
+#endif
+#if SEM_N_LO <= 5 && 5 <= SEM_N_HI
+SEM_INSTANTIATE(5)
+#endif
+#if SEM_N_LO <= 6 && 6 <= SEM_N_HI
+SEM_INSTANTIATE(6)
+#endif
+#if SEM_N_LO <= 7 && 7 <= SEM_N_HI
+SEM_INSTANTIATE(7)
+#endif
+#if SEM_N_LO <= 8 && 8 <= SEM_N_HI
+SEM_INSTANTIATE(8)
+#endif
+#if SEM_N_LO <= 9 && 9 <= SEM_N_HI
+SEM_INSTANTIATE(9)
+#endif
+#if SEM_N_LO <= 10 && 10 <= SEM_N_HI
+SEM_INSTANTIATE(10)
+#endif
+#if SEM_N_LO <= 11 && 11 <= SEM_N_HI
+SEM_INSTANTIATE(11)
+#endif
+#if SEM_N_LO <= 12 && 12 <= SEM_N_HI
+SEM_INSTANTIATE(12)
+#endif
+#if SEM_N_LO <= 13 && 13 <= SEM_N_HI
+SEM_INSTANTIATE(13)
+#endif
+#if SEM_N_LO <= 14 && 14 <= SEM_N_HI
+SEM_INSTANTIATE(14)
+#endif
+#if SEM_N_LO <= 15 && 15 <= SEM_N_HI
+SEM_INSTANTIATE(15)
+#endif
+#if SEM_N_LO <= 16 && 16 <= SEM_N_HI
+SEM_INSTANTIATE(16)
+#endif
+#if SEM_N_LO <= 17 && 17 <= SEM_N_HI
+SEM_INSTANTIATE(17)
+#endif
+
+}  // namespace semd

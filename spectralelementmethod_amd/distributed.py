@@ -565,6 +565,22 @@ class OverlappedOperator(object):
     def plan_info(self):
         return (self.interior or self.iface).plan_info() if self.dd else self.ops[0].plan_info()
 
+    def dd_info(self):
+        """The decomposition's sem_dd_info as a dict (None on one rank)."""
+        if not self.dd:
+            return None
+        v = (C.c_int64 * 9)()
+        _lib.check(self._lib.sem_dd_info(self.dd, v, 9))
+        return dict(ndof=v[0], iface_dofs=v[1], peers=v[2], exchanged=v[3],
+                    transport=("none", "rccl", "callbacks")[v[4]], interior=bool(v[5]),
+                    graphs=bool(v[6]), captures=v[7], replays=v[8])
+
+    def set_graphs(self, enable):
+        """Captured step on / off (sem_dd_set_graphs)."""
+        if self.dd:
+            _lib.check(self._lib.sem_dd_set_graphs(self.dd, 1 if enable else 0))
+        return self
+
     def step(self, u, y, events=None):
         """y = K u on this rank's DOFs, shared DOFs summed over all ranks.
         ``events`` (start, end) bracket the step on the caller's stream."""
@@ -601,6 +617,10 @@ class OverlappedOperator(object):
         """Jacobi-PCG for K x = rhs on this rank's DOFs (dirichlet: bool mask;
         x holds the Dirichlet values and the initial guess, updated in place).
         Returns (x, iterations executed, final relative residual)."""
+        if self.dd and self.world > 1 and self.plan.not_owned is None:
+            # every rank would count its copies of the shared DOFs in the
+            # global dot products: a wrong inner product, silently
+            raise ValueError("pcg_solve on several ranks needs the ownership mask (owned=...)")
         mask = torch.as_tensor(dirichlet, dtype=torch.bool).to(self.device).to(torch.uint8)
         its, rel = C.c_int(0), C.c_double(0.0)
         sp = _lib.stream_ptr(torch.cuda.current_stream(self.device))

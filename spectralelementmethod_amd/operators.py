@@ -201,12 +201,12 @@ class SEMOperator(object):
                     kernel="mfma" if v[17] == _lib.KERNEL_MFMA else "column",
                     map_entry_bytes=v[18],
                     geometry="nodal" if v[19] == _lib.GEOM_NODAL else "stored",
-                    plan=("chains", "element-coloured", "element", "chains-one-launch",
-                          "chains-seams")[v[20]],
+                    plan={0: "chains", 1: "element-coloured", 2: "element",
+                          4: "chains-seams"}[v[20]],
                     geometry_axisym=(None if self.dpn != 2 else
                                      "nodal" if v[21] == _lib.GEOM_NODAL else "stored"),
-                    dependencies=v[22] if v[20] == 3 else 0, lag=v[23], wait_timeouts=v[24],
-                    seam_nodes=v[22] if v[20] == 4 else 0)
+                    seam_nodes=v[22] if v[20] == 4 else 0, blocks=bool(v[23]),
+                    row_carries=v[24])
 
     # ------------------------------------------------------------------
     def compute_geometry(self, kind=POISSON, stream=None):

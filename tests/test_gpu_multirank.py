@@ -315,3 +315,87 @@ def test_overlapped_axisym_two_dofs_per_node(gpu):
     for rank, err, nbytes in res:
         assert err < 1e-13, (rank, err)
         assert nbytes > 0
+
+
+def _graph_worker(rank, world, port, q):
+    """One rank's step eager and as captured graphs (sem_dd_set_graphs):
+    bitwise equal actions (same kernels, same order), equal PCG solves, and
+    the host-enqueue time per step of both."""
+    import sys
+    import time
+    for pth in (ROOT, os.path.join(ROOT, "oracle")):
+        if pth not in sys.path:
+            sys.path.insert(0, pth)
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from spectralelementmethod_amd.distributed import OverlappedOperator, StripPartition
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        p = 8
+        part = StripPartition(32, 24, p, world, rank)
+        nodes, e2n = part.local_mesh(0.05)
+        op = OverlappedOperator(p, nodes, e2n, part.neighbors, 1, dev, owned=part.owned,
+                                transport="torch", world=world, rank=rank)
+        g = torch.Generator(device=dev).manual_seed(5 + rank)
+        u = torch.randn(op.ndof, dtype=torch.float64, device=dev, generator=g)
+        out, enq = {}, {}
+        for mode in (False, True):
+            op.set_graphs(mode)
+            y = torch.full_like(u, 3.0)
+            op.step(u, y)  # (re)capture
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(10):
+                op.step(u, y)
+            enq[mode] = (time.perf_counter() - t0) / 10
+            torch.cuda.synchronize()
+            out[mode] = y.clone()
+        info = op.dd_info()
+        xs, on = _manufactured(nodes, dev)
+        b = op.apply(xs)
+        sol = {}
+        for mode in (False, True):
+            op.set_graphs(mode)
+            x = torch.where(on, xs, torch.zeros_like(xs))
+            x, its, rel = op.pcg_solve(b, x, on, rtol=1e-11)
+            sol[mode] = (x, its)
+        # the Jacobi diagonal is summed with atomics (setup, sem_diag): the two
+        # solves differ at rounding level, not in their iteration count
+        dx = ((sol[False][0] - sol[True][0]).norm() / sol[True][0].norm()).item()
+        q.put((rank, torch.equal(out[False], out[True]), info, dx, sol[False][1], sol[True][1],
+               enq[False] * 1e6, enq[True] * 1e6))
+        op.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_captured_step_equals_eager(gpu):
+    """sem_dd_apply through its captured graphs (the default) equals the
+    eager enqueue bit for bit on 2 ranks of one device (torch transport
+    between the graph segments); the PCG over the decomposition agrees to
+    rounding (its Jacobi diagonal is an atomic sum)."""
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_graph_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    try:
+        res = [q.get(timeout=150) for _ in range(world)]
+    finally:
+        for pr in procs:
+            pr.join(timeout=60)
+    for pr in procs:
+        assert pr.exitcode == 0
+    for rank, same, info, dx, its0, its1, us_eager, us_graph in res:
+        assert same, rank
+        assert info["graphs"] and info["replays"] >= 10 and info["captures"] >= 1, info
+        assert dx < 1e-12 and abs(its0 - its1) <= 16, (rank, dx, its0, its1)
+        print("rank %d host enqueue per step: eager %.1f us, graphs %.1f us (torch-host "
+              "transport included)" % (rank, us_eager, us_graph))

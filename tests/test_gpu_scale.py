@@ -13,6 +13,10 @@ relative L2.
   geometry (element-relative coordinates) is checked against the
   extended-precision oracle on the golden meshes instead
   (test_gpu_parity.py);
+* config 4 above p = 10 on the PRODUCTION path (device geometry from the mesh
+  nodes, no installed factors) at full size: a block of 2 element columns x
+  all rows against the extended-precision oracle at 1e-10, and no less
+  accurate than the reference's float64 algorithm on the same block;
 * config 5: the axisymmetric Stokes block on a 128 x 128 curved annulus, p = 6,
   with the factors re-derived per node from x_phys (NODAL) and streamed.
 
@@ -102,3 +106,39 @@ def test_config5_axisym_vs_oracle(gpu, gll, geometry):
     assert op.plan_info()["geometry_axisym"] == geometry
     assert rel_l2(y[0::2], ref[0::2]) < TOL
     assert rel_l2(y[1::2], ref[1::2]) < TOL
+
+
+CFG4_EXT = [(12, 263), (14, 227), (16, 198)]
+
+
+@pytest.mark.parametrize("geometry", ["nodal", "stored"])
+@pytest.mark.parametrize("p,nex", CFG4_EXT)
+def test_config4_device_geometry_vs_extended(gpu, gll, p, nex, geometry):
+    """p > 10 at ~1e7 DOF through sem_geom_from_nodes (the compensated
+    equispaced->GLL transform of k_geometry): the inner nodes of
+    element columns [nex/2 - 1, nex/2 + 1) x all rows against
+    poisson_apply_extended (x87 extended precision from the same float64
+    inputs) at the north-star 1e-10, and at least as accurate as the
+    reference's own float64 algorithm there (sem/basis_functions.py:599-624)."""
+    import sem_oracle
+    from spectralelementmethod_amd import meshgen
+    from spectralelementmethod_amd.operators import SEMOperator
+    nodes, e2n = meshgen.structured_square(nex, nex, p, warp=0.05)
+    assert 0.98e7 < nodes.shape[1] < 1.02e7
+    u = np.random.default_rng(p).standard_normal(nodes.shape[1])
+    op = SEMOperator(p, e2n, nodes, device=gpu, geometry=geometry)
+    assert op.plan_info()["geometry"] == geometry
+    y = op.apply(torch.from_numpy(u).to(gpu)).cpu().numpy()
+    op.close()
+    c0 = nex // 2 - 1
+    nb, eb, off = meshgen.structured_strip(nex, nex, p, c0, c0 + 2, 0.05)
+    loc = off + np.arange(nb.shape[1])
+    Ny = nex * p + 1
+    inner = np.arange(Ny, nb.shape[1] - Ny)  # the block's outer node lines get outside terms
+    half = gll["half_%d" % p]
+    ext = np.asarray(sem_oracle.poisson_apply_extended(nb, eb, half, u[loc]), dtype=np.float64)
+    ref = sem_oracle.PoissonProblem(nb, eb, half, batched_geometry=True).apply(u[loc])
+    e_gpu = rel_l2(y[loc[inner]], ext[inner])
+    e_ref = rel_l2(ref[inner], ext[inner])
+    assert e_gpu < TOL, (p, geometry, e_gpu, e_ref)
+    assert e_gpu <= e_ref, (p, geometry, e_gpu, e_ref)
