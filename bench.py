@@ -50,6 +50,9 @@ DEFAULT_TRAFFIC = {"stored": "pmc_traffic_stored_p8_1024x1024.json",
                    "nodal": "pmc_traffic_nodal_p8_1024x1024.json"}
 
 
+JSON_OUT = sys.stdout  # the driver's JSON line (rank 0)
+
+
 def log(msg):
     print("[bench] " + msg, file=sys.stderr, flush=True)
 
@@ -371,6 +374,11 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
+        # keep stdout for the one JSON line: gloo / RCCL print connection
+        # banners on file descriptor 1 from C++ (they go to stderr instead)
+        global JSON_OUT
+        JSON_OUT = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
         import datetime
         pg_timeout = datetime.timedelta(seconds=args.deadline)
         if args.rehearse_one_gpu:
@@ -571,7 +579,7 @@ def main():
             "gpu_setup_sec_per_elem": t_setup / max(1, n_elem_local),
         }
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=JSON_OUT, flush=True)
     op.close()
     if world > 1:
         dist.destroy_process_group()
@@ -661,7 +669,7 @@ def bench_pcg(args, op, part, nodes, dev, world, rank, ndof_global, t_setup):
                 "check_every": 16, "gpu_setup_sec": t_setup},
     }
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=JSON_OUT, flush=True)
     op.close()
     if world > 1:
         dist.destroy_process_group()

@@ -47,7 +47,11 @@ inline int block_rounds_auto(int n, int dpn) {
   (void)dpn;
   return 4;
 }
-inline bool seam_auto(int n, int64_t chains_per_colour, int dpn = 1) {
+inline bool seam_auto(int n, int64_t chains_per_colour, int dpn = 1, bool blocks = false) {
+  // block layout: the seams are a few % of the nodes (every R-th node row and
+  // every 4*EPW-th column) -- 1024^2 p = 8: R = 4 seams 0.671, colours 0.692,
+  // consecutive groups 0.684 ms (profiles/r03/blocks_ab.txt)
+  if (blocks && dpn == 1) return true;
   if (dpn == 2) return chains_per_colour <= 512;
   return n >= 11 || chains_per_colour <= 1024 || (n >= 9 && chains_per_colour <= 2400);
 }

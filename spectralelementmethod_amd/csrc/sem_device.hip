@@ -406,7 +406,7 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
   if (seam == 2) {  // AUTO (seam_auto): high orders, or colour classes below ~1 generation
     std::vector<int64_t> per(MAX_COLOURS + 1, 0);
     for (int64_t ch = 0; ch < n_chains; ++ch) per[colour[ch]]++;
-    seam = seam_auto(n, *std::max_element(per.begin(), per.end()), seam_dpn) ? 1 : 0;
+    seam = seam_auto(n, *std::max_element(per.begin(), per.end()), seam_dpn, P.blocks) ? 1 : 0;
   }
   P.seam = seam == 1 && conforming;
   for (int64_t ch = 0; ch < n_chains && P.seam; ++ch)

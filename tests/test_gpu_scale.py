@@ -140,5 +140,8 @@ def test_config4_device_geometry_vs_extended(gpu, gll, p, nex, geometry):
     ref = sem_oracle.PoissonProblem(nb, eb, half, batched_geometry=True).apply(u[loc])
     e_gpu = rel_l2(y[loc[inner]], ext[inner])
     e_ref = rel_l2(ref[inner], ext[inner])
+    print("p=%d %dx%d %s: device vs extended %.2e, reference float64 vs extended %.2e, "
+          "device vs reference float64 %.2e" % (p, nex, nex, geometry, e_gpu, e_ref,
+                                                  rel_l2(y[loc[inner]], ref[inner])))
     assert e_gpu < TOL, (p, geometry, e_gpu, e_ref)
     assert e_gpu <= e_ref, (p, geometry, e_gpu, e_ref)
