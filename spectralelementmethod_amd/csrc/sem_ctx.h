@@ -40,12 +40,16 @@ constexpr int MAX_COLOURS = 8;  // + one trailing all-atomic class
 // axisym_seams): 128^2 (cpc 114) 0.0441 -> 0.0236, 512^2 (cpc 1,820) 0.227
 // -> 0.274 (the nodal kernel's seam instantiation runs 1 wave per SIMD
 // instead of 2).
-// AUTO rounds of the block layout (sem_device.hip groups_blocks): a chain is
-// R stacked lines x 4 groups; 0 = consecutive groups
-inline int block_rounds_auto(int n, int dpn) {
+// AUTO of the block layout (sem_device.hip groups_blocks, 4 rounds): only
+// where the mesh still has this many chains with it.  Measured on MI355X,
+// ms per action, consecutive groups -> blocks (profiles/r03/sweep): the
+// axisymmetric Stokes block at 512^2, p = 6 (1,920 block chains) 0.302 ->
+// 0.257; Poisson p = 8 1024^2 (9,472) 0.684 -> 0.671, 395^2 (1,481) 0.106
+// -> 0.107, p = 6 527^2 (1,980) 0.118 -> 0.122, p = 12 263^2 0.132 ->
+// 0.151, p = 16 198^2 0.139 -> 0.188, 256^2 p = 8 0.046 -> 0.056.
+inline int64_t block_min_chains(int n, int dpn) {
   (void)n;
-  (void)dpn;
-  return 4;
+  return dpn == 2 ? 1024 : 4096;
 }
 inline bool seam_auto(int n, int64_t chains_per_colour, int dpn = 1, bool blocks = false) {
   // block layout: the seams are a few % of the nodes (every R-th node row and

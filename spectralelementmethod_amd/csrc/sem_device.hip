@@ -251,6 +251,7 @@ struct Plan {
   int64_t n_slots = 0;
   bool conforming = true;
   bool blocks = false;     // block layout (groups_blocks)
+  int block_rounds = 0;
   int64_t row_carries = 0;  // entries carried to the next round in registers
   // seam plan: chains in element order, one launch; nodes written by several
   // chains go through per-colour slots summed by k_seam_sum
@@ -336,8 +337,18 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
   const int epw = WAVE / n, lw = epw * n, nn = n * n;
   const int CW = chain_waves_of(n);  // groups of a chain that run concurrently
   std::vector<int64_t> gel;          // [group][lane element] -> element or -1
+  // block_rounds < 0: AUTO -- 4 rounds when the mesh then still has enough
+  // chains to fill the chip many times over (block_min_chains); fewer chains
+  // leave a tail of lone workgroups that costs more than the carried rows save
+  const bool block_auto = block_rounds < 0;
+  if (block_auto) block_rounds = 4;
   P.blocks = block_rounds >= 2 && groups_blocks(e2n, n_elem, n, epw, CW, block_rounds, gel);
-  if (P.blocks) rounds = block_rounds;
+  if (P.blocks && block_auto &&
+      (int64_t)gel.size() / ((int64_t)epw * CW * block_rounds) < block_min_chains(n, seam_dpn)) {
+    P.blocks = false;
+    gel.clear();
+  }
+  if (P.blocks) rounds = P.block_rounds = block_rounds;
   const int CH = CW * rounds;
   if (!P.blocks) groups_consecutive(n_elem, epw, CH, gel);
   const int64_t n_groups = (int64_t)gel.size() / epw;
@@ -1055,8 +1066,8 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
   const bool mfma = want_mfma(c);
   // block layout (groups_blocks): rounds stacked along the lines, the node
   // row between rounds carried in registers; SEM_BLOCK_ROUNDS=R forces R
-  // (0 or 1: off), default block_rounds_auto
-  int brounds = block_rounds_auto(n, c->dpn);
+  // (0 or 1: off), default AUTO (build_plan, block_min_chains)
+  int brounds = -1;  // AUTO (build_plan)
   if (const char* s = std::getenv("SEM_BLOCK_ROUNDS")) brounds = std::atoi(s);
   // seam plan: one launch + seam sums; SEM_SEAM=1 / 0 forces / forbids it;
   // default AUTO (seam_auto, per dofs per node)
@@ -1072,7 +1083,7 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
     rc = build_plan(h, c->n_elem, c->n_node, n, rounds, state, P, 0, c->dpn, brounds);
   }
   if (rc) return rc;
-  if (P.blocks) rounds = brounds;
+  if (P.blocks) rounds = P.block_rounds;
   // element-coloured fallback for orders that defeat the chain patterns
   // (SEM_PLAN=1 forces it, SEM_PLAN=0 forbids it)
   const char* penv = std::getenv("SEM_PLAN");

@@ -134,15 +134,59 @@ struct DEO<N, false> {
   __device__ __forceinline__ const DEOData<N>* row() const { return &d; }
 };
 
+// SEM_D_LDS (default): each workgroup copies the even-odd D into LDS once
+// and the contractions read it with broadcast ds_reads.  Through scalar loads
+// the 144 (n = 17) coefficients compete with the kernel's pointers for ~100
+// SGPRs: the compiler then loads ONE coefficient at a time and waits for each
+// (s_load_dwordx2 + s_waitcnt lgkmcnt(0) before every second FMA of a row).
+#ifndef SEM_D_LDS
+#define SEM_D_LDS 1
+#endif
+template <int N>
+using LDEOData = const __attribute__((address_space(3))) DEOData<N>;
+
 template <int N>
 struct DEO<N, true> {
-  const DEOData<N>* p;  // device copy (constant during the launch)
+  const DEOData<N>* p;       // device copy (constant during the launch)
+  LDEOData<N>* l = nullptr;  // the workgroup's LDS copy (deo_to_lds)
+#if SEM_D_LDS
+  __device__ __forceinline__ LDEOData<N>* row() const {
+    LDEOData<N>* q = l;
+    asm volatile("" : "+v"(q));
+    return q;
+  }
+#else
   __device__ __forceinline__ CDEOData<N>* row() const {
     CDEOData<N>* q = (CDEOData<N>*)(p);
     asm volatile("" : "+s"(q));
     return q;
   }
+#endif
 };
+
+// LDS staging of D (n >= SEM_D_SCALAR_LOAD_N; a workgroup-uniform call after
+// any early exit): returns the DEO the contractions use
+template <int N>
+struct DeoLds {
+  static constexpr bool on = N >= SEM_D_SCALAR_LOAD_N && SEM_D_LDS;
+  DEOData<on ? N : 2> d;
+};
+template <int N>
+__device__ __forceinline__ DEO<N> deo_to_lds(const DEO<N>& D, DeoLds<N>& s) {
+  if constexpr (DeoLds<N>::on) {
+    const double* src = reinterpret_cast<const double*>(D.p);
+    double* dst = reinterpret_cast<double*>(&s.d);
+    for (int i = threadIdx.x; i < (int)(sizeof(DEOData<N>) / sizeof(double)); i += blockDim.x)
+      dst[i] = src[i];
+    __syncthreads();
+    DEO<N> r = D;
+    r.l = (LDEOData<N>*)(&s.d);
+    return r;
+  } else {
+    (void)s;
+    return D;
+  }
+}
 
 // v = D x
 template <int N>
@@ -207,6 +251,41 @@ __device__ __forceinline__ void deo_apply_t(const DEO<N>& D, const double (&x)[N
 #pragma unroll
     for (int m = 0; m < H; ++m) a = fma(E->cc[m], o[m], a);
     v[H] = a;
+  }
+}
+
+// out[m] (m = 0..N-1) = (TR ? D^T x : D x), written to out[m * stride] pair by
+// pair as the even-odd sums complete (a row pass stores into the lane's own
+// LDS row): only e, o and one output pair are live, not the whole output
+// column -- the register peak of the high-order column kernels
+template <int N, bool TR>
+__device__ __forceinline__ void deo_apply_to(const DEO<N>& D, const double (&x)[N], double* out) {
+  constexpr int H = N / 2;
+  double e[H], o[H];
+#pragma unroll
+  for (int r = 0; r < H; ++r) {
+    e[r] = x[r] + x[N - 1 - r];
+    o[r] = x[r] - x[N - 1 - r];
+  }
+#pragma unroll
+  for (int m = 0; m < H; ++m) {
+    const auto E = D.row();
+    double sp = 0.0, tp = 0.0;
+    if constexpr (DEOData<N>::C) tp = (TR ? E->rr[m] : E->cc[m]) * x[H];
+#pragma unroll
+    for (int r = 0; r < H; ++r) {
+      sp = fma(TR ? E->Q[r * H + m] : E->P[m * H + r], o[r], sp);
+      tp = fma(TR ? E->P[r * H + m] : E->Q[m * H + r], e[r], tp);
+    }
+    out[m] = sp + tp;
+    out[N - 1 - m] = sp - tp;
+  }
+  if constexpr (DEOData<N>::C) {
+    const auto E = D.row();
+    double a = 0.0;
+#pragma unroll
+    for (int r = 0; r < H; ++r) a = fma(TR ? E->cc[r] : E->rr[r], o[r], a);
+    out[H] = a;
   }
 }
 
@@ -422,18 +501,28 @@ struct Tile {
 // the wave and synchronised) is contracted with D (or D^T when TR) and
 // written back, so the tile again holds the result in column layout.  REL
 // differentiates relative to the row's first entry (see poisson_group_nodal).
+#ifndef SEM_ROW_STORE_PAIRS_N
+#define SEM_ROW_STORE_PAIRS_N 17  // orders from which row passes store output pairs directly
+#endif
 template <int N, int RS, bool TR, bool REL>
 __device__ __forceinline__ void row_pass(double* L, int j, const DEO<N>& D) {
-  double r[RS], x[N], t[N];
+  double r[RS], x[N];
   load_row<N, RS>(L, j, r);
 #pragma unroll
   for (int q = 0; q < N; ++q) x[q] = REL ? r[q] - r[0] : r[q];
-  if constexpr (TR)
-    deo_apply_t<N>(D, x, t);
-  else
-    deo_apply<N>(D, x, t);
-  wave_sync();
-  store_row<N, RS>(L, j, t);
+  if constexpr (N >= SEM_ROW_STORE_PAIRS_N) {
+    // the lane rewrites only its own row: no ordering point needed between
+    // its loads and its stores (the compiler orders them by address)
+    deo_apply_to<N, TR>(D, x, L + j * RS);
+  } else {
+    double t[N];
+    if constexpr (TR)
+      deo_apply_t<N>(D, x, t);
+    else
+      deo_apply<N>(D, x, t);
+    wave_sync();
+    store_row<N, RS>(L, j, t);
+  }
   wave_sync();
 }
 
@@ -820,14 +909,16 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
     k_poisson_apply(const MapRef mref, const double* __restrict__ GP,
                     const double2* __restrict__ XG, const double* __restrict__ u,
                     double* __restrict__ y, int64_t c0, int64_t c1, int rounds, int accumulate,
-                    const DEO<N> D, const WVec<N> w, const SeamPlan sp) {
+                    const DEO<N> D0, const WVec<N> w, const SeamPlan sp) {
   using T = Tile<N, NODAL ? SEM_TILE_PAD_NODAL : SEM_TILE_PAD_STORED>;
   constexpr int NT = NODAL ? 2 : 1;  // tiles per element slot
   __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * T::ES * NT];
   constexpr int CW = ChainWaves<N>::value;
   __shared__ double carry[2][CW][1][N];
+  __shared__ DeoLds<N> sdeo;
   const int64_t chain = c0 + xcd_block(blockIdx.x, gridDim.x);
   if (chain >= c1) return;  // uniform over the workgroup
+  const DEO<N> Dk = deo_to_lds<N>(D0, sdeo);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);  // provably uniform
   const int lane = threadIdx.x % WAVE;
   const int k = lane / N;
@@ -848,10 +939,10 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
     const Pre pre{};
     constexpr bool PRE = RmwPrefetch<N>::value > 0 && Pre::prefetch;
     if constexpr (NODAL)
-      poisson_group_nodal<N, M16>(mref, XG, u, g, lane, j, in_wave, L, LB, D, w, wj, raw, v[0],
+      poisson_group_nodal<N, M16>(mref, XG, u, g, lane, j, in_wave, L, LB, Dk, w, wj, raw, v[0],
                                   y, accumulate, prev, pre);
     else
-      poisson_group_stored<N, M16>(mref, GP, u, g, lane, j, in_wave, L, D, raw, v[0], y,
+      poisson_group_stored<N, M16>(mref, GP, u, g, lane, j, in_wave, L, Dk, raw, v[0], y,
                                    accumulate, prev, pre);
     SeamOut so;
     if constexpr (SEAM) so.base = sp.buf + sp.colour[chain] * sp.n_node;
@@ -1252,13 +1343,15 @@ template <int N, bool M16, bool SEAM = false>
 __global__ void __launch_bounds__(ChainWaves<N>::block, SEM_AXI_MIN_WAVES)
     k_axisym_nodal(const MapRef mref, const double2* __restrict__ XG, const double* __restrict__ u,
                    double* __restrict__ y, int64_t c0, int64_t c1, int rounds, int accumulate,
-                   const DEO<N> D, const WVec<N> w, const SeamPlan sp) {
+                   const DEO<N> D0, const WVec<N> w, const SeamPlan sp) {
   using T = Tile<N>;
   __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * 2 * T::ES];
   constexpr int CW = ChainWaves<N>::value;
   __shared__ double carry[2][CW][2][N];
+  __shared__ DeoLds<N> sdeo;
   const int64_t chain = c0 + blockIdx.x;
   if (chain >= c1) return;
+  const DEO<N> D = deo_to_lds<N>(D0, sdeo);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   const int lane = threadIdx.x % WAVE;
   const int k = lane / N;
@@ -1285,14 +1378,16 @@ template <int N, int MODE, bool SEAM = false>
 __global__ void __launch_bounds__(ChainWaves<N>::block)
     k_axisym_apply(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
                    const double* __restrict__ u, double* __restrict__ y, int64_t c0, int64_t c1,
-                   int rounds, int accumulate, const DEO<N> D, const WVec<N> w, const AxiNS ns,
+                   int rounds, int accumulate, const DEO<N> D0, const WVec<N> w, const AxiNS ns,
                    const SeamPlan sp) {
   using T = Tile<N>;
   __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * 2 * T::ES];
   constexpr int CW = ChainWaves<N>::value;
   __shared__ double carry[2][CW][2][N];
+  __shared__ DeoLds<N> sdeo;
   const int64_t chain = c0 + blockIdx.x;
   if (chain >= c1) return;
+  const DEO<N> D = deo_to_lds<N>(D0, sdeo);
   const int wave = threadIdx.x / WAVE;
   const int lane = threadIdx.x % WAVE;
   const int k = lane / N;
