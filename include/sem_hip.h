@@ -381,7 +381,10 @@ int sem_copy_async(void* dst, const void* src, int64_t nbytes, void* stream);
 
 /* info[0] ndof_local, [1] n_iface_dofs, [2] peers, [3] exchanged values per
  * direction, [4] transport (0 none, 1 RCCL, 2 callbacks), [5] has interior,
- * [6] captured step on (sem_dd_set_graphs), [7] captures, [8] replays. */
+ * [6] captured step on (sem_dd_set_graphs), [7] captures, [8] replays,
+ * [9] sem_dd_apply calls, [10] host nanoseconds spent in them, [11] of which
+ * inside the transport call (a caller transport that synchronises with the
+ * device makes [11] the device time up to the exchange). */
 int sem_dd_info(sem_dd* dd, int64_t* info, int n_info);
 
 /* Captured step (default on; SEM_DD_GRAPH=0 in the environment turns it

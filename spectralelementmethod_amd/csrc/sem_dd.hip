@@ -26,6 +26,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -322,6 +323,8 @@ struct sem_dd {
   const double* g_u = nullptr;
   double* g_y = nullptr;
   int64_t n_captures = 0, n_replays = 0;
+  // host time spent enqueueing sem_dd_apply, and inside the transport call
+  int64_t host_steps = 0, host_ns = 0, host_ns_transport = 0;
 };
 
 namespace {
@@ -360,7 +363,18 @@ int dd_begin(sem_dd* d, int op_kind, bool diag, const double* u, double* y, hipS
   return dd_main(d, op_kind, diag, u, y, st);
 }
 
+int dd_exchange_impl(sem_dd* d);
+
+// the transport call, timed on the host (sem_dd_info [10])
 int dd_exchange(sem_dd* d) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = dd_exchange_impl(d);
+  d->host_ns_transport += std::chrono::duration_cast<std::chrono::nanoseconds>(
+                              std::chrono::steady_clock::now() - t0).count();
+  return rc;
+}
+
+int dd_exchange_impl(sem_dd* d) {
   const int np = (int)d->peer.size();
   if (!np) return SEM_OK;
   if (d->comm) {
@@ -796,10 +810,11 @@ int sem_dd_set_transport(sem_dd* d, sem_exchange_fn xfn, sem_allreduce_fn rfn, v
 
 int sem_dd_info(sem_dd* d, int64_t* info, int n_info) {
   if (!d || !info || n_info < 1) return fail(SEM_E_INVALID, "bad arguments");
-  const int64_t v[9] = {d->ndof, d->nc, (int64_t)d->peer.size(), n_exchanged(d),
-                        d->comm ? 1 : (d->xfn ? 2 : 0), d->interior ? 1 : 0,
-                        d->graphs ? 1 : 0, d->n_captures, d->n_replays};
-  for (int i = 0; i < n_info && i < 9; ++i) info[i] = v[i];
+  const int64_t v[12] = {d->ndof, d->nc, (int64_t)d->peer.size(), n_exchanged(d),
+                         d->comm ? 1 : (d->xfn ? 2 : 0), d->interior ? 1 : 0,
+                         d->graphs ? 1 : 0, d->n_captures, d->n_replays,
+                         d->host_steps, d->host_ns, d->host_ns_transport};
+  for (int i = 0; i < n_info && i < 12; ++i) info[i] = v[i];
   return SEM_OK;
 }
 
@@ -816,10 +831,21 @@ int sem_dd_apply(sem_dd* d, int op_kind, const double* d_u, double* d_y, void* s
   if (!d || !d_u || !d_y) return fail(SEM_E_INVALID, "null argument");
   if (d_u == d_y) return fail(SEM_E_INVALID, "sem_dd_apply: u and y must not alias");
   DeviceGuard g(d->device);
-  if (d->graphs) return dd_apply_graphs(d, op_kind, d_u, d_y, S(stream));
-  SEM_TRY(dd_begin(d, op_kind, false, d_u, d_y, S(stream)));
-  SEM_TRY(dd_exchange(d));
-  return dd_finish(d, d_y, S(stream));
+  const auto t0 = std::chrono::steady_clock::now();
+  const int64_t tr0 = d->host_ns_transport;
+  int rc;
+  if (d->graphs) {
+    rc = dd_apply_graphs(d, op_kind, d_u, d_y, S(stream));
+  } else {
+    SEM_TRY(dd_begin(d, op_kind, false, d_u, d_y, S(stream)));
+    SEM_TRY(dd_exchange(d));
+    rc = dd_finish(d, d_y, S(stream));
+  }
+  (void)tr0;
+  d->host_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(
+                    std::chrono::steady_clock::now() - t0).count();
+  d->host_steps++;
+  return rc;
 }
 
 int sem_dd_diag(sem_dd* d, int op_kind, double* d_diag, void* stream) {

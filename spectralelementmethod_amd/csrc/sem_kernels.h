@@ -1339,13 +1339,137 @@ __device__ __forceinline__ void axisym_group_nodal(const MapRef& mref,
   wave_sync();
 }
 
+// The same group, fields first (round 3): psi / omega are gathered and
+// differentiated before the geometry, d1 of both fields waits in the two
+// field tiles while the geometry runs through a third tile plane (x, then
+// y), so the Jacobian arrays never coexist with the row-pass temporaries of
+// the fields -- the live set drops from 256 VGPRs (one or two waves per SIMD)
+// to the three-wave range.  Same arithmetic, same order per node as
+// axisym_group_nodal.
+#ifndef SEM_AXI_FIELDS_FIRST
+#define SEM_AXI_FIELDS_FIRST 1
+#endif
+template <int N, bool M16>
+__device__ __forceinline__ void axisym_group_nodal3(const MapRef& mref,
+                                                    const double2* __restrict__ XG,
+                                                    const double* __restrict__ u, int64_t g,
+                                                    int lane, int j, bool in_wave, double* LP,
+                                                    double* LO, double* LG, const DEO<N>& D,
+                                                    const WVec<N>& w, double wj,
+                                                    uint32_t (&raw)[N], double (&vo)[N],
+                                                    double (&vp)[N]) {
+  constexpr int RS = Tile<N>::RS;
+  load_map<N, M16>(mref, g, lane, in_wave, raw);
+  const double2* u2 = reinterpret_cast<const double2*>(u);
+  double om[N], d0p[N], d0o[N];
+  {
+    double ps[N];
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      const double2 val = u2[raw[r] & GID_MASK];
+      ps[r] = val.x;
+      om[r] = val.y;
+    }
+    deo_apply<N>(D, ps, d0p);
+    deo_apply<N>(D, om, d0o);
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      LP[r * RS + j] = ps[r];
+      LO[r * RS + j] = om[r];
+    }
+  }
+  wave_sync();
+  row_pass<N, RS, false, false>(LP, j, D);  // d1 psi
+  row_pass<N, RS, false, false>(LO, j, D);  // d1 omega
+  // geometry: J along the column in registers, along the row through LG
+  double jr0[N], jr1[N], js0[N], js1[N], rho[N];
+  {
+    double2 xc[N];
+    gather_x<N>(XG, raw, j, xc);
+    double ta[N], tb[N];
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      ta[r] = xc[r].x - xc[0].x;
+      tb[r] = xc[r].y - xc[0].y;
+      rho[r] = xc[r].x;
+      LG[r * RS + j] = xc[r].x;
+    }
+    deo_apply<N>(D, ta, jr0);
+    deo_apply<N>(D, tb, jr1);
+    wave_sync();
+    row_pass<N, RS, false, true>(LG, j, D);
+#pragma unroll
+    for (int m = 0; m < N; ++m) js0[m] = LG[m * RS + j];
+    wave_sync();
+#pragma unroll
+    for (int r = 0; r < N; ++r) LG[r * RS + j] = xc[r].y;
+  }
+  wave_sync();
+  row_pass<N, RS, false, true>(LG, j, D);
+#pragma unroll
+  for (int m = 0; m < N; ++m) js1[m] = LG[m * RS + j];
+  // pointwise (squirmer-axisymmetric.py:193-227), as axisym_group_nodal
+#pragma unroll
+  for (int m = 0; m < N; ++m) {
+    const double d1p = LP[m * RS + j];
+    const double d1o = LO[m * RS + j];
+    const double det = jr0[m] * js1[m] - js0[m] * jr1[m];
+    const double wm = w.v[m];
+    const double rs = rho[m] * (wm * (wj * fast_rcp(det)));
+    const double g00 = rs * fma(js1[m], js1[m], js0[m] * js0[m]);
+    const double g01 = -rs * fma(js1[m], jr1[m], js0[m] * jr0[m]);
+    const double g11 = rs * fma(jr1[m], jr1[m], jr0[m] * jr0[m]);
+    const double W = wm * (wj * det);
+    const double b0 = 2.0 * wm * (wj * js1[m]);
+    const double b1 = -2.0 * wm * (wj * jr1[m]);
+    const double c = W * fast_rcp(rho[m]);
+    const double mm = rho[m] * rho[m] * W;
+    LP[m * RS + j] = fma(g01, d0p[m], g11 * d1p);
+    LO[m * RS + j] = fma(g01, d0o[m], g11 * d1o);
+    vp[m] = fma(b0, d0p[m], fma(b1, d1p, -mm * om[m]));
+    vo[m] = c * om[m];
+    d0p[m] = fma(g00, d0p[m], g01 * d1p);
+    d0o[m] = fma(g00, d0o[m], g01 * d1o);
+  }
+  {
+    double t[N];
+    deo_apply_t<N>(D, d0p, t);
+#pragma unroll
+    for (int p = 0; p < N; ++p) vp[p] += t[p];
+    deo_apply_t<N>(D, d0o, t);
+#pragma unroll
+    for (int p = 0; p < N; ++p) vo[p] += t[p];
+  }
+  wave_sync();
+  row_pass<N, RS, true, false>(LP, j, D);
+  row_pass<N, RS, true, false>(LO, j, D);
+#pragma unroll
+  for (int p = 0; p < N; ++p) {
+    vo[p] += LO[p * RS + j];
+    vp[p] += LP[p * RS + j];
+  }
+  wave_sync();
+}
+
+// fields first up to n = 8 (three tile planes at three workgroups per CU:
+// 151 KB of LDS at n = 7); above, the LDS of a third plane would cost more
+// occupancy than the registers gain
+template <int N>
+struct AxiNodal {
+  static constexpr bool fields_first = SEM_AXI_FIELDS_FIRST && N <= 8;
+  static constexpr int planes = fields_first ? 3 : 2;
+  static constexpr int waves = fields_first ? (SEM_AXI_MIN_WAVES > 1 ? SEM_AXI_MIN_WAVES : 3)
+                                            : SEM_AXI_MIN_WAVES;
+};
+
 template <int N, bool M16, bool SEAM = false>
-__global__ void __launch_bounds__(ChainWaves<N>::block, SEM_AXI_MIN_WAVES)
+__global__ void __launch_bounds__(ChainWaves<N>::block, AxiNodal<N>::waves)
     k_axisym_nodal(const MapRef mref, const double2* __restrict__ XG, const double* __restrict__ u,
                    double* __restrict__ y, int64_t c0, int64_t c1, int rounds, int accumulate,
                    const DEO<N> D0, const WVec<N> w, const SeamPlan sp) {
   using T = Tile<N>;
-  __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * 2 * T::ES];
+  constexpr int NPL = AxiNodal<N>::planes;  // tile planes
+  __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * NPL * T::ES];
   constexpr int CW = ChainWaves<N>::value;
   __shared__ double carry[2][CW][2][N];
   __shared__ DeoLds<N> sdeo;
@@ -1365,8 +1489,12 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, SEM_AXI_MIN_WAVES)
     const int64_t g = (chain * rounds + rd) * CW + wave;
     uint32_t raw[N];
     double v[2][N];  // [0] omega row (y[2k]), [1] psi row (y[2k+1])
-    axisym_group_nodal<N, M16>(mref, XG, u, g, lane, j, in_wave, LP, LO, D, w, wj, raw, v[0],
-                               v[1]);
+    if constexpr (AxiNodal<N>::fields_first)
+      axisym_group_nodal3<N, M16>(mref, XG, u, g, lane, j, in_wave, LP, LO,
+                                  LO + T::TILE_SLOTS * T::ES, D, w, wj, raw, v[0], v[1]);
+    else
+      axisym_group_nodal<N, M16>(mref, XG, u, g, lane, j, in_wave, LP, LO, D, w, wj, raw, v[0],
+                                 v[1]);
     SeamOut so;
     if constexpr (SEAM) so.base = sp.buf + sp.colour[chain] * sp.n_node * 2;
     chain_emit<N, 2, false, CW, SEAM>(y, raw, v, lane, wave, rd, in_wave, carry, rowc, accumulate,

@@ -569,11 +569,15 @@ class OverlappedOperator(object):
         """The decomposition's sem_dd_info as a dict (None on one rank)."""
         if not self.dd:
             return None
-        v = (C.c_int64 * 9)()
-        _lib.check(self._lib.sem_dd_info(self.dd, v, 9))
+        v = (C.c_int64 * 12)()
+        _lib.check(self._lib.sem_dd_info(self.dd, v, 12))
+        steps = max(1, v[9])
         return dict(ndof=v[0], iface_dofs=v[1], peers=v[2], exchanged=v[3],
                     transport=("none", "rccl", "callbacks")[v[4]], interior=bool(v[5]),
-                    graphs=bool(v[6]), captures=v[7], replays=v[8])
+                    graphs=bool(v[6]), captures=v[7], replays=v[8], applies=v[9],
+                    host_ns=v[10], host_ns_transport=v[11],
+                    host_us_per_apply=v[10] / steps / 1e3,
+                    host_us_per_apply_excl_transport=(v[10] - v[11]) / steps / 1e3)
 
     def set_graphs(self, enable):
         """Captured step on / off (sem_dd_set_graphs)."""

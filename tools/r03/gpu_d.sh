@@ -22,7 +22,12 @@ for cfg in "10 316" "12 263" "14 227" "16 198"; do
   run p$1_sgpr_$rep SEM_LIB_PATH=$PWD/build_variants/lib_dsgpr.so --p $1 --nex $2 --ney $2 --steps 50
 done
 done
-run cfg5_auto SEM_X=1 --op axisym_stokes --p 6 --nex 512 --ney 512 --steps 50
+for rep in 1 2; do
+run cfg5_fields_first_$rep SEM_X=1 --op axisym_stokes --p 6 --nex 512 --ney 512 --steps 50
+run cfg5_two_planes_$rep SEM_LIB_PATH=$PWD/build_variants/lib_axi2plane.so --op axisym_stokes --p 6 --nex 512 --ney 512 --steps 50
+done
+timeout -k 10 200 python -u -m pytest tests/test_gpu_multirank.py::test_captured_step_equals_eager -s -q --timeout 170 --timeout-method thread -p no:cacheprovider > $O/captured.log 2>&1; rc=$?; echo "captured rc=$rc"; grep -E "enqueue|passed|failed" $O/captured.log
+fatal $rc captured
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/pcg_trace -o run -- python bench.py --op pcg --steps 30 --warmup 3 > $O/pcg_trace.log 2>&1; rc=$?; echo "pcg trace rc=$rc"
 fatal $rc pcgtrace
 head -12 $O/pcg_trace/run_kernel_stats.csv | cut -c1-200
