@@ -120,6 +120,13 @@ __global__ void k_cg_flags(const uint8_t* __restrict__ dir, const uint8_t* __res
     f[t] = (dir[t] ? F_DIR : 0) | ((notown && notown[t]) ? F_NOTOWN : 0);
 }
 
+// diag -> 1 / diag in place (once per solve: the Jacobi preconditioner is
+// then a multiply in the update pass, not an fp64 division per DOF)
+__global__ void k_cg_invert(double* __restrict__ d, int64_t n) {
+  for (int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x; t < n; t += (int64_t)gridDim.x * BLK)
+    d[t] = 1.0 / d[t];
+}
+
 // r = b - K x on free DOFs (r holds K x on entry), z = r / diag, p = z;
 // partial sums of r.z and r.r over owned DOFs
 __global__ void __launch_bounds__(BLK)
@@ -130,7 +137,7 @@ __global__ void __launch_bounds__(BLK)
   for (int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x; t < n; t += (int64_t)gridDim.x * BLK) {
     const uint8_t ft = f[t];
     const double rt = (ft & F_DIR) ? 0.0 : b[t] - r[t];
-    const double zt = (ft & F_DIR) ? 0.0 : rt / diag[t];
+    const double zt = (ft & F_DIR) ? 0.0 : rt * diag[t];  // diag holds 1 / diag
     r[t] = rt;
     z[t] = zt;
     p[t] = zt;
@@ -199,7 +206,7 @@ __global__ void __launch_bounds__(BLK)
       if (t >= n) continue;
       x[t] = fma(alpha, pv[u], xv[u]);
       const double rt = (fv[u] & F_DIR) ? 0.0 : fma(-alpha, qv[u], rv[u]);
-      const double zt = (fv[u] & F_DIR) ? 0.0 : rt / dv[u];
+      const double zt = (fv[u] & F_DIR) ? 0.0 : rt * dv[u];  // dv = 1 / diag
       r[t] = rt;
       z[t] = zt;
       if (!(fv[u] & F_NOTOWN)) {
@@ -586,6 +593,7 @@ int pcg_run(const PcgOp& op, int kind, const double* b, double* x, const uint8_t
   const bool multi = op.dd && op.dd->world > 1;  // dots need an all-reduce
   hipLaunchKernelGGL(k_cg_flags, dim3(grid_for(n)), dim3(BLK), 0, st, dir, notown, n, s.flags);
   SEM_TRY(op.diag(kind, dg, st));
+  hipLaunchKernelGGL(k_cg_invert, dim3(grid_for(n)), dim3(BLK), 0, st, dg, n);
   SEM_TRY(op.apply(kind, x, r, st));
   hipLaunchKernelGGL(k_cg_start, dim3(gb), dim3(BLK), 0, st, b, r, dg, s.flags, n, z, p, partial);
   hipLaunchKernelGGL(k_cg_finish, dim3(1), dim3(BLK), 0, st, partial, gb, 2, T[0], nullptr);

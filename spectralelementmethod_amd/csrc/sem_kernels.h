@@ -119,6 +119,11 @@ struct DEOData {
 // v_readlane per FMA operand); instead each contraction row re-reads its
 // 2H values with scalar loads from a device copy: the pointer is laundered
 // through an empty asm per row so the loads are neither hoisted nor CSE'd.
+// (Round 3 tried a per-workgroup LDS copy read with broadcast ds_reads: no
+// SGPR pressure, but every wave-wide read returns 64 copies of a value
+// through the CU's LDS port -- slower at every order, p = 10 / 12 / 14 / 16:
+// 0.131 / 0.137 / 0.153 / 0.158 against 0.122 / 0.131 / 0.138 / 0.138 ms,
+// profiles/r03/high_order_d.)
 #ifndef SEM_D_SCALAR_LOAD_N
 #define SEM_D_SCALAR_LOAD_N 10
 #endif
@@ -134,59 +139,15 @@ struct DEO<N, false> {
   __device__ __forceinline__ const DEOData<N>* row() const { return &d; }
 };
 
-// SEM_D_LDS (default): each workgroup copies the even-odd D into LDS once
-// and the contractions read it with broadcast ds_reads.  Through scalar loads
-// the 144 (n = 17) coefficients compete with the kernel's pointers for ~100
-// SGPRs: the compiler then loads ONE coefficient at a time and waits for each
-// (s_load_dwordx2 + s_waitcnt lgkmcnt(0) before every second FMA of a row).
-#ifndef SEM_D_LDS
-#define SEM_D_LDS 1
-#endif
-template <int N>
-using LDEOData = const __attribute__((address_space(3))) DEOData<N>;
-
 template <int N>
 struct DEO<N, true> {
-  const DEOData<N>* p;       // device copy (constant during the launch)
-  LDEOData<N>* l = nullptr;  // the workgroup's LDS copy (deo_to_lds)
-#if SEM_D_LDS
-  __device__ __forceinline__ LDEOData<N>* row() const {
-    LDEOData<N>* q = l;
-    asm volatile("" : "+v"(q));
-    return q;
-  }
-#else
+  const DEOData<N>* p;  // device copy (constant during the launch)
   __device__ __forceinline__ CDEOData<N>* row() const {
     CDEOData<N>* q = (CDEOData<N>*)(p);
     asm volatile("" : "+s"(q));
     return q;
   }
-#endif
 };
-
-// LDS staging of D (n >= SEM_D_SCALAR_LOAD_N; a workgroup-uniform call after
-// any early exit): returns the DEO the contractions use
-template <int N>
-struct DeoLds {
-  static constexpr bool on = N >= SEM_D_SCALAR_LOAD_N && SEM_D_LDS;
-  DEOData<on ? N : 2> d;
-};
-template <int N>
-__device__ __forceinline__ DEO<N> deo_to_lds(const DEO<N>& D, DeoLds<N>& s) {
-  if constexpr (DeoLds<N>::on) {
-    const double* src = reinterpret_cast<const double*>(D.p);
-    double* dst = reinterpret_cast<double*>(&s.d);
-    for (int i = threadIdx.x; i < (int)(sizeof(DEOData<N>) / sizeof(double)); i += blockDim.x)
-      dst[i] = src[i];
-    __syncthreads();
-    DEO<N> r = D;
-    r.l = (LDEOData<N>*)(&s.d);
-    return r;
-  } else {
-    (void)s;
-    return D;
-  }
-}
 
 // v = D x
 template <int N>
@@ -909,16 +870,14 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
     k_poisson_apply(const MapRef mref, const double* __restrict__ GP,
                     const double2* __restrict__ XG, const double* __restrict__ u,
                     double* __restrict__ y, int64_t c0, int64_t c1, int rounds, int accumulate,
-                    const DEO<N> D0, const WVec<N> w, const SeamPlan sp) {
+                    const DEO<N> D, const WVec<N> w, const SeamPlan sp) {
   using T = Tile<N, NODAL ? SEM_TILE_PAD_NODAL : SEM_TILE_PAD_STORED>;
   constexpr int NT = NODAL ? 2 : 1;  // tiles per element slot
   __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * T::ES * NT];
   constexpr int CW = ChainWaves<N>::value;
   __shared__ double carry[2][CW][1][N];
-  __shared__ DeoLds<N> sdeo;
   const int64_t chain = c0 + xcd_block(blockIdx.x, gridDim.x);
   if (chain >= c1) return;  // uniform over the workgroup
-  const DEO<N> Dk = deo_to_lds<N>(D0, sdeo);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);  // provably uniform
   const int lane = threadIdx.x % WAVE;
   const int k = lane / N;
@@ -939,10 +898,10 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
     const Pre pre{};
     constexpr bool PRE = RmwPrefetch<N>::value > 0 && Pre::prefetch;
     if constexpr (NODAL)
-      poisson_group_nodal<N, M16>(mref, XG, u, g, lane, j, in_wave, L, LB, Dk, w, wj, raw, v[0],
+      poisson_group_nodal<N, M16>(mref, XG, u, g, lane, j, in_wave, L, LB, D, w, wj, raw, v[0],
                                   y, accumulate, prev, pre);
     else
-      poisson_group_stored<N, M16>(mref, GP, u, g, lane, j, in_wave, L, Dk, raw, v[0], y,
+      poisson_group_stored<N, M16>(mref, GP, u, g, lane, j, in_wave, L, D, raw, v[0], y,
                                    accumulate, prev, pre);
     SeamOut so;
     if constexpr (SEAM) so.base = sp.buf + sp.colour[chain] * sp.n_node;
@@ -1466,16 +1425,14 @@ template <int N, bool M16, bool SEAM = false>
 __global__ void __launch_bounds__(ChainWaves<N>::block, AxiNodal<N>::waves)
     k_axisym_nodal(const MapRef mref, const double2* __restrict__ XG, const double* __restrict__ u,
                    double* __restrict__ y, int64_t c0, int64_t c1, int rounds, int accumulate,
-                   const DEO<N> D0, const WVec<N> w, const SeamPlan sp) {
+                   const DEO<N> D, const WVec<N> w, const SeamPlan sp) {
   using T = Tile<N>;
   constexpr int NPL = AxiNodal<N>::planes;  // tile planes
   __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * NPL * T::ES];
   constexpr int CW = ChainWaves<N>::value;
   __shared__ double carry[2][CW][2][N];
-  __shared__ DeoLds<N> sdeo;
   const int64_t chain = c0 + blockIdx.x;
   if (chain >= c1) return;
-  const DEO<N> D = deo_to_lds<N>(D0, sdeo);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   const int lane = threadIdx.x % WAVE;
   const int k = lane / N;
@@ -1506,16 +1463,14 @@ template <int N, int MODE, bool SEAM = false>
 __global__ void __launch_bounds__(ChainWaves<N>::block)
     k_axisym_apply(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
                    const double* __restrict__ u, double* __restrict__ y, int64_t c0, int64_t c1,
-                   int rounds, int accumulate, const DEO<N> D0, const WVec<N> w, const AxiNS ns,
+                   int rounds, int accumulate, const DEO<N> D, const WVec<N> w, const AxiNS ns,
                    const SeamPlan sp) {
   using T = Tile<N>;
   __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * 2 * T::ES];
   constexpr int CW = ChainWaves<N>::value;
   __shared__ double carry[2][CW][2][N];
-  __shared__ DeoLds<N> sdeo;
   const int64_t chain = c0 + blockIdx.x;
   if (chain >= c1) return;
-  const DEO<N> D = deo_to_lds<N>(D0, sdeo);
   const int wave = threadIdx.x / WAVE;
   const int lane = threadIdx.x % WAVE;
   const int k = lane / N;
