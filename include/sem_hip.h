@@ -229,6 +229,15 @@ int sem_set_geom(sem_ctx* ctx, const double* d_G, int op_kind, void* stream);
 int sem_apply(sem_ctx* ctx, int op_kind, const double* d_u, double* d_y, int flags,
               void* stream);
 
+/* y = K u (overwrite) and *d_dot = u . y (a device double), for the
+ * preconditioned CG's p . Kp: on the seam plan of a single-rank Poisson
+ * context the dot is summed inside the action's own two launches (each
+ * node's final value is stored exactly once: u[gid] * value at that store,
+ * per-workgroup partials, one fixed-order sum -- deterministic); on any other
+ * plan the action is followed by a separate dot pass.  Same y as sem_apply. */
+int sem_apply_dot(sem_ctx* ctx, int op_kind, const double* d_u, double* d_y, double* d_dot,
+                  void* stream);
+
 /* Reynolds number N_Re of the SEM_OP_AXISYM_NS residual and its Jacobian
  * (the n_rey scaling of the advection operator Ae, squirmer:230-250).
  * SEM_OP_AXISYM_NS with u = (psi, omega) interleaved gives

@@ -64,6 +64,7 @@ SIGNATURES = {
     "sem_set_reynolds": (C.c_int, [_vp, C.c_double]),
     "sem_set_map_shared": (C.c_int, [_vp, _vp, _vp, _vp]),
     "sem_apply": (C.c_int, [_vp, C.c_int, _vp, _vp, C.c_int, _vp]),
+    "sem_apply_dot": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp]),
     "sem_zero_shared": (C.c_int, [_vp, _vp, _vp]),
     "sem_vec_add": (C.c_int, [_vp, _vp, _i64, _vp]),
     "sem_diag": (C.c_int, [_vp, C.c_int, _vp, _vp]),

@@ -106,6 +106,9 @@ struct sem_ctx {
   bool blocks = false;       // block layout of the chains (groups_blocks)
   int64_t row_carries = 0;
   bool seam = false;
+  bool seam_dot = false;    // sem_apply_dot fuses u.y into the seam plan's launches
+  double* d_dot = nullptr;  // u.y partials of sem_apply_dot (chains + seam-sum blocks)
+  int64_t n_dot = 0;
   int seam_ns = 0;
   int64_t n_seam = 0;
   uint8_t* d_ccol = nullptr;
@@ -223,17 +226,22 @@ inline bool use_nodal(const sem_ctx* c, int op_kind) {
 }
 
 // per-order entry points (sem_launch.hip)
+// dot_out (device scalar, may be null): also u.y, fused into the seam plan's
+// launches (the caller guarantees: seam plan, Poisson, overwrite)
 template <int N>
 int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc, bool lin,
-                   hipStream_t st);
+                   hipStream_t st, double* dot_out);
 template <int N>
 int launch_geom_n(sem_ctx* c, const double* nodes, int op_kind, double* GP, double* xph,
                   double* J, double* iJ, double* dJ, double* dJW, double2* XG,
                   const double2* XGin, hipStream_t st);
 template <int N>
 int upload_deo(sem_ctx* c);
-// the seam sums of the seam plan (sem_device.hip)
-int launch_seam_sum(sem_ctx* c, double* y, int acc, hipStream_t st);
+// the seam sums of the seam plan (sem_device.hip); du / dot: also the u.y
+// partials of the seam nodes, one per block of seam_sum_blocks(c)
+int launch_seam_sum(sem_ctx* c, double* y, int acc, hipStream_t st, const double* du = nullptr,
+                    double* dot = nullptr);
+int64_t seam_sum_blocks(const sem_ctx* c);
 
 #define SEM_DISPATCH_N(rc, n, FN, ...)          \
   switch (n) {                                  \

@@ -563,6 +563,8 @@ struct PcgScratch {
 };
 
 const bool g_sync_each = std::getenv("SEM_PCG_SYNC_EACH") != nullptr;  // diagnostic
+// SEM_PCG_SEPARATE_PQ=1: the p.q pass after the action even on one GPU (A/B)
+const bool g_separate_pq = std::getenv("SEM_PCG_SEPARATE_PQ") != nullptr;
 
 int pcg_run(const PcgOp& op, int kind, const double* b, double* x, const uint8_t* dir,
             const uint8_t* notown, double rtol, int max_iter, int check, int* iters,
@@ -611,10 +613,16 @@ int pcg_run(const PcgOp& op, int kind, const double* b, double* x, const uint8_t
     const int blk = std::min(check, max_iter - it);
     for (int k = 0; k < blk; ++k) {
       const int o = it & 1, nw = o ^ 1;
-      SEM_TRY(op.apply(kind, p, q, st));
-      hipLaunchKernelGGL(k_cg_pq, dim3(gb), dim3(BLK), 0, st, p, q, s.flags, n, partial);
-      hipLaunchKernelGGL(k_cg_finish, dim3(1), dim3(BLK), 0, st, partial, gb, 1, pq, nullptr);
-      SEM_TRY(dd_allreduce(op.dd, pq, 1, st));
+      if (op.ctx && !g_separate_pq) {
+        // single GPU: p.q summed inside the action (sem_apply_dot; p = 0 on
+        // Dirichlet DOFs, every DOF owned)
+        SEM_TRY(sem_apply_dot(op.ctx, kind, p, q, pq, st));
+      } else {
+        SEM_TRY(op.apply(kind, p, q, st));
+        hipLaunchKernelGGL(k_cg_pq, dim3(gb), dim3(BLK), 0, st, p, q, s.flags, n, partial);
+        hipLaunchKernelGGL(k_cg_finish, dim3(1), dim3(BLK), 0, st, partial, gb, 1, pq, nullptr);
+        SEM_TRY(dd_allreduce(op.dd, pq, 1, st));
+      }
       hipLaunchKernelGGL(k_cg_update, dim3(gb), dim3(BLK), 0, st, x, r, z, p, q, dg, s.flags,
                          T[o], pq, n, partial);
       hipLaunchKernelGGL(k_cg_finish, dim3(1), dim3(BLK), 0, st, partial, gb, 2, T[nw],

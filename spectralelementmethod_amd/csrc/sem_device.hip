@@ -35,6 +35,18 @@ __global__ void k_pack_geom(const double* __restrict__ G, int64_t n_elem, int n,
   }
 }
 
+// u.y over all nodes (the fallback of sem_apply_dot on plans without seams)
+__global__ void __launch_bounds__(BLOCK)
+    k_dot_plain(const double* __restrict__ u, const double* __restrict__ y, int64_t n,
+                double* __restrict__ part) {
+  double v = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK)
+    v = fma(u[i], y[i], v);
+  __shared__ double sh[BLOCK / WAVE];
+  const double t = semk::block_sum_fixed<BLOCK / WAVE>(v, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = t;
+}
+
 __global__ void k_zero_list(double* __restrict__ y, const uint32_t* __restrict__ idx, int64_t n,
                             int dpn) {
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n;
@@ -157,7 +169,10 @@ int ctx_device(const sem_ctx* c) { return c->device; }
 namespace semd {
 // second launch of the seam plan (k_seam_sum / k_seam_sum2 over the seam
 // nodes, one instantiation per colour count)
-int launch_seam_sum(sem_ctx* c, double* y, int acc, hipStream_t st) {
+int64_t seam_sum_blocks(const sem_ctx* c) { return c->n_seam ? grid_for(c->n_seam) : 0; }
+
+int launch_seam_sum(sem_ctx* c, double* y, int acc, hipStream_t st, const double* du,
+                    double* dot) {
   if (!c->n_seam) return SEM_OK;
   const dim3 g(grid_for(c->n_seam)), b(BLOCK);
   switch (c->seam_ns) {
@@ -166,9 +181,13 @@ int launch_seam_sum(sem_ctx* c, double* y, int acc, hipStream_t st) {
     if (c->dpn == 2)                                                                       \
       hipLaunchKernelGGL(k_seam_sum2<K>, g, b, 0, st, y, c->d_seam_gid, c->d_seam_mask,    \
                          c->n_seam, c->d_seam_buf, c->n_node, acc);                        \
+    else if (dot)                                                                          \
+      hipLaunchKernelGGL((k_seam_sum<K, true>), g, b, 0, st, y, c->d_seam_gid,             \
+                         c->d_seam_mask, c->n_seam, c->d_seam_buf, c->n_node, acc, du, dot);\
     else                                                                                   \
-      hipLaunchKernelGGL(k_seam_sum<K>, g, b, 0, st, y, c->d_seam_gid, c->d_seam_mask,     \
-                         c->n_seam, c->d_seam_buf, c->n_node, acc);                        \
+      hipLaunchKernelGGL((k_seam_sum<K, false>), g, b, 0, st, y, c->d_seam_gid,            \
+                         c->d_seam_mask, c->n_seam, c->d_seam_buf, c->n_node, acc, nullptr, \
+                         nullptr);                                                         \
     break;
     SEAM_NS(1) SEAM_NS(2) SEAM_NS(3) SEAM_NS(4) SEAM_NS(5) SEAM_NS(6) SEAM_NS(7) SEAM_NS(8)
 #undef SEAM_NS
@@ -198,6 +217,16 @@ int check_op(sem_ctx* c, int op_kind) {
 // factor slot of an operator kind: the two Navier-Stokes kinds share one
 int gp_slot(int op_kind) {
   return op_kind == SEM_OP_POISSON ? 0 : (op_kind == SEM_OP_AXISYM_STOKES ? 1 : 2);
+}
+
+// partial-sum buffer of sem_apply_dot (grown on demand, never shrunk)
+int ensure_dot(sem_ctx* c, int64_t n) {
+  if (c->d_dot && c->n_dot >= n) return SEM_OK;
+  (void)hipFree(c->d_dot);
+  c->d_dot = nullptr;
+  HIP_TRY(hipMalloc(&c->d_dot, std::max<int64_t>(n, 1) * sizeof(double)));
+  c->n_dot = std::max<int64_t>(n, 1);
+  return SEM_OK;
 }
 
 // The zero fill is ordered on the stream of the kernels that fill the
@@ -250,6 +279,7 @@ struct Plan {
   int64_t n_atomic_groups = 0;
   int64_t n_slots = 0;
   bool conforming = true;
+  int64_t n_rmw = 0;       // read-modify-write entries (a node's final value elsewhere)
   bool blocks = false;     // block layout (groups_blocks)
   int block_rounds = 0;
   int64_t row_carries = 0;  // entries carried to the next round in registers
@@ -589,6 +619,8 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
   for (int64_t i = 0; i < n_node; ++i)
     if (cnt[i] == 0 && (node_state.empty() || !node_state[i])) P.zero.push_back((uint32_t)i);
   std::sort(P.zero.begin(), P.zero.end());
+  P.n_rmw = 0;
+  for (const uint32_t e : P.mapP) P.n_rmw += ((e >> CODE_SHIFT) & 3u) == W_RMW ? 1 : 0;
   if (P.seam) {
     if (P.n_atomic_groups || seam_conflict) {  // sharing the seam slots cannot express
       P.seam = false;
@@ -1019,6 +1051,7 @@ void sem_ctx_destroy(sem_ctx* c) {
   (void)hipFree(c->d_seam_gid);
   (void)hipFree(c->d_seam_mask);
   (void)hipFree(c->d_seam_buf);
+  (void)hipFree(c->d_dot);
   delete c;
 }
 
@@ -1152,6 +1185,9 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
   }
   c->colour_start = P.colour_start;
   c->seam = P.seam;
+  // sem_apply_dot's fused form: every node's final value is one STORE (or a
+  // seam sum): no read-modify-write, nothing zeroed separately
+  c->seam_dot = P.seam && P.n_rmw == 0 && P.zero.empty() && state.empty();
   c->seam_ns = P.seam_ns;
   c->n_seam = (int64_t)P.seam_gid.size();
   (void)hipFree(c->d_ccol);
@@ -1370,10 +1406,47 @@ int sem_apply(sem_ctx* c, int op_kind, const double* u, double* y, int flags, vo
   if (!accumulate && !(flags & SEM_APPLY_SKIP_ZERO) && c->n_zero)
     hipLaunchKernelGGL(k_zero_list, dim3(grid_for(c->n_zero, BLOCK, 4096)), dim3(BLOCK), 0, st, y,
                        c->d_zero, c->n_zero, c->dpn);
-  SEM_DISPATCH_N(rc, c->n, launch_apply_n, c, op_kind, u, y, accumulate, lin, st);
+  SEM_DISPATCH_N(rc, c->n, launch_apply_n, c, op_kind, u, y, accumulate, lin, st, nullptr);
   if (rc) return rc;
   HIP_TRY(hipGetLastError());
   if (lin) c->lin_valid = true;
+  return SEM_OK;
+}
+
+int sem_apply_dot(sem_ctx* c, int op_kind, const double* u, double* y, double* d_dot,
+                  void* stream) {
+  if (!c || !d_dot) return fail(SEM_E_INVALID, "null argument");
+  if (!(c->seam_dot && op_kind == SEM_OP_POISSON && c->dpn == 1)) {
+    // no fused form on this plan: the action, then a separate u.y pass
+    int rc = sem_apply(c, op_kind, u, y, 0, stream);
+    if (rc) return rc;
+    DeviceGuard g(c->device);
+    hipStream_t st = S(stream);
+    const int64_t n = c->n_node * c->dpn;
+    const int nb = grid_for(n, BLOCK, 2048);
+    if ((rc = ensure_dot(c, nb))) return rc;
+    hipLaunchKernelGGL(k_dot_plain, dim3(nb), dim3(BLOCK), 0, st, u, y, n, c->d_dot);
+    hipLaunchKernelGGL(k_dot_finish, dim3(1), dim3(BLOCK), 0, st, c->d_dot, (int64_t)nb,
+                       c->d_dot, (int64_t)0, d_dot);
+    HIP_TRY(hipGetLastError());
+    return SEM_OK;
+  }
+  int rc;
+  if ((rc = check_op(c, op_kind))) return rc;
+  if (!c->have_basis || !c->d_mapP) return fail(SEM_E_STATE, "basis and map must be set");
+  if (!use_nodal(c, op_kind) && !c->d_GP[gp_slot(op_kind)])
+    return fail(SEM_E_STATE, "geometry for this operator has not been computed");
+  {
+    const size_t nb = (size_t)c->n_node * sizeof(double);
+    const char *a = reinterpret_cast<const char*>(u), *b = reinterpret_cast<const char*>(y);
+    if (a < b + nb && b < a + nb) return fail(SEM_E_INVALID, "sem_apply_dot: u and y overlap");
+  }
+  DeviceGuard g(c->device);
+  const int64_t nch = c->colour_start.back() - c->colour_start.front();
+  if ((rc = ensure_dot(c, nch + seam_sum_blocks(c)))) return rc;
+  SEM_DISPATCH_N(rc, c->n, launch_apply_n, c, op_kind, u, y, 0, false, S(stream), d_dot);
+  if (rc) return rc;
+  HIP_TRY(hipGetLastError());
   return SEM_OK;
 }
 

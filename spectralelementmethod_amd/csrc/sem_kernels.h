@@ -766,13 +766,18 @@ __device__ __forceinline__ void poisson_group_nodal(const MapRef& mref,
 // Scatter of one group's column values through the coded map, with the
 // in-group merge (next lane) and the chain carry (previous group) applied.
 // ncomp values per node (1: Poisson, 2: axisymmetric block).
-template <int N, int NC, bool PRE = false, int CW = ChainWaves<N>::value, bool SEAM = false>
+// DOT (seam plan, overwrite mode, one DOF per node): dot += u[gid] * value
+// at every STORE -- the node's one and only final value outside the seams.
+template <int N, int NC, bool PRE = false, int CW = ChainWaves<N>::value, bool SEAM = false,
+          bool DOT = false>
 __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_t (&raw)[N],
                                            double (&v)[NC][N], int lane, int wave, int rd,
                                            bool in_wave, double (*carry)[CW][NC][N],
                                            double (&rowc)[NC], int accumulate,
                                            const double* prev = nullptr,
-                                           const SeamOut& so = SeamOut()) {
+                                           const SeamOut& so = SeamOut(),
+                                           const double* __restrict__ du = nullptr,
+                                           double* dot = nullptr) {
   constexpr int LW = Tile<N>::LW;
   // row carry between rounds (block layout): before any merge, row 0 takes
   // the row n-1 value this lane held back in the previous round
@@ -811,8 +816,12 @@ __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_
   if (in_wave) {
 #pragma unroll
     for (int p = 0; p < N; ++p) {
-      if constexpr (SEAM && NC == 1)
+      if constexpr (SEAM && NC == 1) {
         emit1_seam(y, raw[p], v[0][p], accumulate, so);
+        if constexpr (DOT)
+          if (((raw[p] >> CODE_SHIFT) & 3u) == W_STORE)
+            *dot = fma(du[raw[p] & GID_MASK], v[0][p], *dot);
+      }
       else if constexpr (PRE)
         emit1p(y, raw[p], v[0][p], prev[p]);
       else if (NC == 1)
@@ -863,9 +872,25 @@ struct SeamPlan {
   const uint8_t* __restrict__ colour;  // [chain]
   double* buf;                         // [colour][node]
   int64_t n_node;
+  double* dot = nullptr;  // DOT kernels: one partial of u.y per workgroup
 };
 
-template <int N, bool NODAL, bool M16, bool SEAM = false>
+// sum of one value per thread over the workgroup, in a fixed order (wave
+// reductions, then the waves in order), returned by thread 0
+template <int NW>
+__device__ __forceinline__ double block_sum_fixed(double v, double* sh) {
+#pragma unroll
+  for (int o = WAVE / 2; o > 0; o >>= 1) v += __shfl_down(v, o, WAVE);
+  if (threadIdx.x % WAVE == 0) sh[threadIdx.x / WAVE] = v;
+  __syncthreads();
+  double s = 0.0;
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int w = 0; w < NW; ++w) s += sh[w];
+  return s;
+}
+
+template <int N, bool NODAL, bool M16, bool SEAM = false, bool DOT = false>
 __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODAL>::value))
     k_poisson_apply(const MapRef mref, const double* __restrict__ GP,
                     const double2* __restrict__ XG, const double* __restrict__ u,
@@ -877,7 +902,12 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
   constexpr int CW = ChainWaves<N>::value;
   __shared__ double carry[2][CW][1][N];
   const int64_t chain = c0 + xcd_block(blockIdx.x, gridDim.x);
-  if (chain >= c1) return;  // uniform over the workgroup
+  if (chain >= c1) {  // uniform over the workgroup
+    if constexpr (DOT)
+      if (threadIdx.x == 0) sp.dot[blockIdx.x] = 0.0;
+    return;
+  }
+  double dotv = 0.0;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);  // provably uniform
   const int lane = threadIdx.x % WAVE;
   const int k = lane / N;
@@ -905,8 +935,13 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
                                    accumulate, prev, pre);
     SeamOut so;
     if constexpr (SEAM) so.base = sp.buf + sp.colour[chain] * sp.n_node;
-    chain_emit<N, 1, PRE, CW, SEAM>(y, raw, v, lane, wave, rd, in_wave, carry, rowc, accumulate,
-                                        prev, so);
+    chain_emit<N, 1, PRE, CW, SEAM, DOT>(y, raw, v, lane, wave, rd, in_wave, carry, rowc,
+                                         accumulate, prev, so, u, &dotv);
+  }
+  if constexpr (DOT) {
+    __shared__ double sh[CW];
+    const double t = block_sum_fixed<CW>(dotv, sh);
+    if (threadIdx.x == 0) sp.dot[blockIdx.x] = t;
   }
 }
 
@@ -916,10 +951,12 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
 // holds a value (SEM_NODE_PRIOR)
 // NS colours: the slot loads of a node are issued together (predicated
 // buffer loads: an unused slot reads past the range, 0 and no traffic).
-template <int NS>
-__global__ void k_seam_sum(double* __restrict__ y, const uint32_t* __restrict__ gid,
-                           const uint16_t* __restrict__ mask, int64_t n,
-                           const double* __restrict__ buf, int64_t n_node, int accumulate);
+template <int NS, bool DOT = false>
+__global__ void __launch_bounds__(BLOCK)
+    k_seam_sum(double* __restrict__ y, const uint32_t* __restrict__ gid,
+               const uint16_t* __restrict__ mask, int64_t n, const double* __restrict__ buf,
+               int64_t n_node, int accumulate, const double* __restrict__ du = nullptr,
+               double* __restrict__ dot = nullptr);
 
 // two DOFs per node (axisymmetric block): slots are double2, buf[colour][node]
 template <int NS>
@@ -944,10 +981,13 @@ __global__ void k_seam_sum2(double* __restrict__ y, const uint32_t* __restrict__
   }
 }
 
-template <int NS>
-__global__ void k_seam_sum(double* __restrict__ y, const uint32_t* __restrict__ gid,
-                           const uint16_t* __restrict__ mask, int64_t n,
-                           const double* __restrict__ buf, int64_t n_node, int accumulate) {
+template <int NS, bool DOT>
+__global__ void __launch_bounds__(BLOCK)
+    k_seam_sum(double* __restrict__ y, const uint32_t* __restrict__ gid,
+               const uint16_t* __restrict__ mask, int64_t n, const double* __restrict__ buf,
+               int64_t n_node, int accumulate, const double* __restrict__ du,
+               double* __restrict__ dot) {
+  double dotv = 0.0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t g = gid[i];
@@ -973,8 +1013,28 @@ __global__ void k_seam_sum(double* __restrict__ y, const uint32_t* __restrict__ 
         first = false;
       }
     y[g] = s;
+    if constexpr (DOT) dotv = fma(du[g], s, dotv);
+  }
+  if constexpr (DOT) {
+    __shared__ double sh[BLOCK / WAVE];
+    const double t = block_sum_fixed<BLOCK / WAVE>(dotv, sh);
+    if (threadIdx.x == 0) dot[blockIdx.x] = t;
   }
 }
+
+// fixed-order sum of the DOT partials of an action: na chain partials, then
+// nb seam-sum partials -> *out
+static __global__ void __launch_bounds__(BLOCK)
+    k_dot_finish(const double* __restrict__ a, int64_t na, const double* __restrict__ b,
+                 int64_t nb, double* __restrict__ out) {
+  double v = 0.0;
+  for (int64_t i = threadIdx.x; i < na; i += BLOCK) v += a[i];
+  for (int64_t i = threadIdx.x; i < nb; i += BLOCK) v += b[i];
+  __shared__ double sh[BLOCK / WAVE];
+  const double t = block_sum_fixed<BLOCK / WAVE>(v, sh);
+  if (threadIdx.x == 0) *out = t;
+}
+
 
 // ---------------------------------------------------------------------------
 // Axisymmetric Stokes block (Re = 0), dpn = 2 interleaved (psi, omega):

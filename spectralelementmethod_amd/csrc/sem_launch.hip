@@ -16,11 +16,31 @@ namespace semd {
 template <int N, bool SEAM>
 void launch_chains(sem_ctx* c, int op_kind, bool nodal, const double* u, double* y, int acc,
                    bool lin, int64_t c0, int64_t c1, const DEO<N>& D, const WVec<N>& w,
-                   hipStream_t st) {
+                   hipStream_t st, double* dot_part = nullptr) {
   const dim3 g((unsigned)(c1 - c0)), b(ChainWaves<N>::block);
   const MapRef mr{c->d_mapP, c->d_map16, c->d_mbase};
   const int R = c->rounds;
-  const SeamPlan sp{c->d_ccol, c->d_seam_buf, c->n_node};
+  SeamPlan sp{c->d_ccol, c->d_seam_buf, c->n_node};
+  sp.dot = dot_part;
+  if constexpr (SEAM) {
+    if (dot_part) {  // Poisson, one DOF per node, overwrite: u.y partials per chain
+      const double* GP = nodal ? nullptr : c->d_GP[0];
+      const double2* XG = nodal ? c->d_XG : nullptr;
+      if (nodal && c->map16)
+        hipLaunchKernelGGL((k_poisson_apply<N, true, true, true, true>), g, b, 0, st, mr, GP, XG, u,
+                           y, c0, c1, R, acc, D, w, sp);
+      else if (nodal)
+        hipLaunchKernelGGL((k_poisson_apply<N, true, false, true, true>), g, b, 0, st, mr, GP, XG,
+                           u, y, c0, c1, R, acc, D, w, sp);
+      else if (c->map16)
+        hipLaunchKernelGGL((k_poisson_apply<N, false, true, true, true>), g, b, 0, st, mr, GP, XG,
+                           u, y, c0, c1, R, acc, D, w, sp);
+      else
+        hipLaunchKernelGGL((k_poisson_apply<N, false, false, true, true>), g, b, 0, st, mr, GP, XG,
+                           u, y, c0, c1, R, acc, D, w, sp);
+      return;
+    }
+  }
   if (op_kind == SEM_OP_POISSON) {
     const double* GP = nodal ? nullptr : c->d_GP[0];
     const double2* XG = nodal ? c->d_XG : nullptr;
@@ -61,15 +81,22 @@ void launch_chains(sem_ctx* c, int op_kind, bool nodal, const double* u, double*
 
 template <int N>
 int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc, bool lin,
-                   hipStream_t st) {
+                   hipStream_t st, double* dot_out) {
   const DEO<N> D = make_deo<N>(c);
   WVec<N> w;
   std::memcpy(w.v, c->hw, sizeof(w.v));
   const bool nodal = use_nodal(c, op_kind);
   if (c->seam) {  // one launch + the seam sums (SeamPlan)
-    launch_chains<N, true>(c, op_kind, nodal, u, y, acc, lin, c->colour_start.front(),
-                           c->colour_start.back(), D, w, st);
-    return launch_seam_sum(c, y, acc, st);
+    const int64_t c0 = c->colour_start.front(), c1 = c->colour_start.back();
+    // dot_out: u.y fused into the two launches (partials, then a fixed-order sum)
+    double* part = dot_out ? c->d_dot : nullptr;
+    launch_chains<N, true>(c, op_kind, nodal, u, y, acc, lin, c0, c1, D, w, st, part);
+    const int rc = launch_seam_sum(c, y, acc, st, dot_out ? u : nullptr,
+                                   part ? part + (c1 - c0) : nullptr);
+    if (rc || !dot_out) return rc;
+    hipLaunchKernelGGL(k_dot_finish, dim3(1), dim3(BLOCK), 0, st, part, c1 - c0,
+                       part + (c1 - c0), seam_sum_blocks(c), dot_out);
+    return SEM_OK;
   }
   const size_t nc = c->colour_start.size() - 1;
   for (size_t k = 0; k < nc; ++k) {
@@ -116,7 +143,8 @@ int upload_deo(sem_ctx* c) {
 }
 
 #define SEM_INSTANTIATE(N)                                                                     \
-  template int launch_apply_n<N>(sem_ctx*, int, const double*, double*, int, bool, hipStream_t); \
+  template int launch_apply_n<N>(sem_ctx*, int, const double*, double*, int, bool, hipStream_t, \
+                                 double*);                                                     \
   template int launch_geom_n<N>(sem_ctx*, const double*, int, double*, double*, double*, double*, \
                                 double*, double*, double2*, const double2*, hipStream_t);        \
   template int upload_deo<N>(sem_ctx*);

@@ -300,6 +300,21 @@ class SEMOperator(object):
             return out.cpu().numpy()
         return out
 
+    def apply_dot(self, u, out=None, stream=None):
+        """(K u, u . K u) for the Poisson operator (sem_apply_dot): on the
+        seam plan the dot is summed inside the action's own launches (what
+        the device PCG uses for p . q).  Returns (out, 0-d device tensor)."""
+        if _geom_key(POISSON) not in self._geom_ready:
+            self.compute_geometry(POISSON, stream=stream)
+        u = self._vec(u, "u")
+        if out is None:
+            out = torch.empty_like(u)
+        dot = torch.empty((), dtype=torch.float64, device=self.device)
+        with torch.cuda.device(self.device):
+            _lib.check(self._lib.sem_apply_dot(self._ctx, POISSON, _lib.tptr(u), _lib.tptr(out),
+                                               _lib.tptr(dot), self._stream(stream)))
+        return out, dot
+
     def assemble(self, elem_vals, out=None, accumulate=False, stream=None):
         """Sum element-local nodal values [E, n, n] through the element map
         into a global vector (sem_assemble): the reference's RHS assembly
