@@ -41,11 +41,11 @@ sys.path.insert(0, ROOT)
 METRIC = "global stiffness-action DOF-updates/s (and % HBM roofline), Poisson p=8"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FP64_PEAK_TFLOPS = 78.6  # MI355X vector fp64 (256 CUs x 128 FLOP/clk x 2.4 GHz)
-# PMC-measured HBM bytes of the headline workload (tools/gpu_profile.sh +
-# tools/pmc_traffic.py), per geometry mode
-# (copies of profiles/r01/pmc_traffic_p8_1024x1024.json and
-# profiles/r02/pmc_traffic_nodal_p8_1024x1024.json in bench_traffic/, which
-# travels to the GPU box; profiles/ does not)
+# PMC-measured HBM bytes per action of the headline workload (separate
+# rocprofv3 --pmc passes, FETCH_SIZE x2 + WRITE_SIZE, all launches of one
+# action), per geometry mode: copies of profiles/r01/pmc_traffic_p8_1024x1024.json
+# and profiles/r03/pmc_default/traffic_per_action.json in bench_traffic/, which
+# travels to the GPU box; profiles/ does not
 DEFAULT_TRAFFIC = {"stored": "pmc_traffic_stored_p8_1024x1024.json",
                    "nodal": "pmc_traffic_nodal_p8_1024x1024.json"}
 
@@ -310,11 +310,10 @@ def torch_index(a, device):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # defaults time the sustained rate: the shader clock dips for the first
-    # ~10 actions of a back-to-back run (power management);
-    # 20 warm-up actions pass the dip, 200 timed ones take ~0.12 s
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    # the driver's own command (--steps 20 --warmup 5); the per-action kernel
+    # time quartiles in the JSON show the clock under sustained fp64 load
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--p", type=int, default=8)
     ap.add_argument("--nex", type=int, default=1024,
                     help="element columns of the global mesh (strong) or per rank (weak)")

@@ -315,7 +315,11 @@ int sem_pcg_solve(sem_ctx* ctx, int op_kind, const double* d_b, double* d_x,
  * d_sc_rhs [n_elem][ne]; d_work [n_elem][nl-ne][nl+1] keeps
  * A_ii^-1 [A_ie | b_i] for sem_schur_backsolve.  Gauss-Jordan with partial
  * pivoting, one workgroup per element (nl - ne <= 512).  SEM_E_INVALID
- * (count in *n_singular) when an interior block is singular. */
+ * (count in *n_singular) when an interior block is singular (a pivot column
+ * exactly zero) or holds a NaN or an off-diagonal inf, where the reference's
+ * linalg.solve(..., check_finite=False) raises too; non-finite couplings
+ * A_ie, A_ei, b_i and infinite diagonal entries of A_ii propagate as they
+ * do there (sem/discrete.py:465-468). */
 int sem_schur_batched(int64_t n_elem, int nl, int ne, const double* d_mat, const double* d_rhs,
                       double* d_work, double* d_sc_mat, double* d_sc_rhs, int64_t* n_singular,
                       void* stream);

@@ -61,12 +61,23 @@ def build(force=False, verbose=True, out=None, defines=(), orders=None):
         units.append(("sem_launch.hip", ["-DSEM_N_LO=%d" % lo, "-DSEM_N_HI=%d" % hi],
                       os.path.join(objdir, "sem_launch_%d_%d.o" % (lo, hi))))
 
+    headers = [os.path.join(CSRC, d) for d in DEPS if d.endswith(".h")]
+    headers.append(os.path.join(os.path.dirname(PKG_DIR), "include", "sem_hip.h"))
+    t_headers = max(os.path.getmtime(h) for h in headers if os.path.exists(h))
+
     def compile_one(u):
         src, extra, obj = u
         cmd = common + extra + ["-c", os.path.join(CSRC, src), "-o", obj]
+        stamp = obj + ".cmd"  # incremental: same command, object newer than its inputs
+        if (not force and os.path.exists(obj) and os.path.exists(stamp)
+                and open(stamp).read() == " ".join(cmd)
+                and os.path.getmtime(obj) > max(t_headers, os.path.getmtime(cmd[-3]))):
+            return obj
         if verbose:
             print("[sem build]", " ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
+        with open(stamp, "w") as f:
+            f.write(" ".join(cmd))
         return obj
 
     with ThreadPoolExecutor(_jobs()) as ex:

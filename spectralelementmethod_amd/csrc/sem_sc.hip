@@ -61,9 +61,19 @@ __global__ void __launch_bounds__(SCB)
       X[t] = j < ni ? A[(int64_t)row * nl + ne + j]
                     : (j < ni + ne ? A[(int64_t)row * nl + (j - ni)] : b[row]);
     }
-    __syncthreads();
-    bool singular = false;
-    for (int k = 0; k < ni; ++k) {
+    // The reference (scipy linalg.solve, check_finite=False) raises when the
+    // interior block holds a NaN or an off-diagonal inf (LAPACK reports the
+    // block singular or an illegal value) but lets an infinite diagonal entry
+    // through: that unknown decouples (1/inf = 0).  Same rule here; non-finite
+    // couplings A_ie, A_ei, b propagate into S and s.
+    bool bad_block = false;
+    for (int t = threadIdx.x; t < ni * ni; t += SCB) {
+      const int i = t / ni, j = t - i * ni;
+      const double a = X[(int64_t)i * W + j];
+      bad_block |= isnan(a) || (isinf(a) && i != j);
+    }
+    bool singular = __syncthreads_or(bad_block);
+    for (int k = 0; k < ni && !singular; ++k) {
       // partial pivoting: largest |X[r][k]|, r >= k (first index on ties, like LAPACK)
       double best = -1.0;
       int bi = k;
@@ -91,7 +101,8 @@ __global__ void __launch_bounds__(SCB)
       if (threadIdx.x == 0) s_piv = s_idx[0];
       const double pv = s_val[0];
       __syncthreads();
-      if (!(pv > 0.0) || !isfinite(pv)) {  // singular interior block: skip the column
+      // an exactly zero pivot column is singular (LAPACK gesv info > 0)
+      if (pv == 0.0) {
         singular = true;
         continue;
       }

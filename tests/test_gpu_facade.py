@@ -174,3 +174,47 @@ def test_compute_local_sc_system_matches_dense(poisson_solution):
     lmat[ne:, ne:] = 0.0
     with pytest.raises(np.linalg.LinAlgError):
         dm.compute_local_sc_system(fe, (lmat, lrhs))
+
+
+def test_local_sc_system_non_finite_like_reference():
+    """the reference calls linalg.solve(..., check_finite=False)
+    (sem/discrete.py:465-468) so that non-finite values (axisymmetry axes)
+    flow into the Schur complement.  Non-finite couplings and an infinite
+    interior diagonal entry propagate (pattern and finite entries equal to
+    the reference's formula, scipy as the checker); a NaN or an off-diagonal
+    inf inside the interior block raises, as scipy does (LinAlgError, a
+    ValueError)."""
+    from scipy import linalg
+    from spectralelementmethod_amd.basis_functions import gll_basis_2d
+    from spectralelementmethod_amd.discrete import DOFManagerSC
+    rng = np.random.default_rng(9)
+    p = 3
+    dm = DOFManagerSC(_mesh(p, 2, 2, 0.05), 1, gll_basis_2d(p))
+    fe = next(dm.finite_elements())
+    nl, ne = fe.ndof, fe.ndof_exterior
+    ext, itr = slice(None, ne), slice(ne, None)
+    B = rng.standard_normal((nl, nl))
+    base = B @ B.T + nl * np.eye(nl)
+    lrhs = rng.standard_normal(nl)
+
+    def ref(lmat):
+        with np.errstate(all="ignore"):
+            tmp = linalg.solve(lmat[itr, itr].T, lmat[ext, itr].T, check_finite=False).T
+            return lmat[ext, ext] - tmp.dot(lmat[itr, ext]), lrhs[ext] - tmp.dot(lrhs[itr])
+
+    for i, j, v in ((0, ne + 1, np.nan), (ne + 1, 2, np.inf), (ne + 2, ne + 2, np.inf)):
+        lmat = base.copy()
+        lmat[i, j] = v
+        S_ref, s_ref = ref(lmat)
+        S, s = dm.compute_local_sc_system(fe, (lmat, lrhs))
+        for got, want in ((S, S_ref), (s, s_ref)):
+            bad = ~np.isfinite(want)
+            assert np.array_equal(~np.isfinite(got), bad), (i, j, v)
+            assert np.abs(got[~bad] - want[~bad]).max() < 1e-12 * np.abs(want[~bad]).max()
+    for i, j, v in ((ne, ne, np.nan), (ne + 1, ne, np.nan), (ne + 3, ne + 2, np.inf)):
+        lmat = base.copy()
+        lmat[i, j] = v
+        with pytest.raises(ValueError):
+            ref(lmat)
+        with pytest.raises(np.linalg.LinAlgError):
+            dm.compute_local_sc_system(fe, (lmat, lrhs))
