@@ -400,13 +400,14 @@ int sem_copy_async(void* dst, const void* src, int64_t nbytes, void* stream);
  * device makes [11] the device time up to the exchange). */
 int sem_dd_info(sem_dd* dd, int64_t* info, int n_info);
 
-/* Captured step (default on; SEM_DD_GRAPH=0 in the environment turns it
- * off): sem_dd_apply and the PCG operator action replay the step's launches
+/* Captured step (default off; SEM_DD_GRAPH=1 in the environment turns it
+ * on): sem_dd_apply and the PCG operator action replay the step's launches
  * as four HIP graphs around the transport call (side stream: gather,
  * interface elements, pack | unpack; caller's stream: interior elements |
  * final add), re-captured when the operator kind or the u / y pointers
  * change.  Same kernels, same order, same results as the eager path; the
- * host enqueues 4 graph launches instead of ~15 kernel launches. */
+ * host enqueues 4 graph launches instead of ~15 kernel launches, which on
+ * ROCm 7 costs more host time, not less. */
 int sem_dd_set_graphs(sem_dd* dd, int enable);
 
 /* y = K u on this rank's DOFs, shared DOFs summed over all ranks (u, y local

@@ -121,25 +121,25 @@ __global__ void k_cg_flags(const uint8_t* __restrict__ dir, const uint8_t* __res
 }
 
 // diag -> 1 / diag in place (once per solve: the Jacobi preconditioner is
-// then a multiply in the update pass, not an fp64 division per DOF)
-__global__ void k_cg_invert(double* __restrict__ d, int64_t n) {
+// then a multiply in the update pass, not an fp64 division per DOF); 0 on
+// Dirichlet DOFs, so that z = r * dinv is 0 there without a flag
+__global__ void k_cg_invert(double* __restrict__ d, const uint8_t* __restrict__ f, int64_t n) {
   for (int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x; t < n; t += (int64_t)gridDim.x * BLK)
-    d[t] = 1.0 / d[t];
+    d[t] = (f[t] & F_DIR) ? 0.0 : 1.0 / d[t];
 }
 
-// r = b - K x on free DOFs (r holds K x on entry), z = r / diag, p = z;
+// r = b - K x on free DOFs (r holds K x on entry), p = z = r / diag;
 // partial sums of r.z and r.r over owned DOFs
 __global__ void __launch_bounds__(BLK)
-    k_cg_start(const double* __restrict__ b, double* __restrict__ r, const double* __restrict__ diag,
-               const uint8_t* __restrict__ f, int64_t n, double* __restrict__ z,
-               double* __restrict__ p, double* __restrict__ partial) {
+    k_cg_start(const double* __restrict__ b, double* __restrict__ r, const double* __restrict__ dinv,
+               const uint8_t* __restrict__ f, int64_t n, double* __restrict__ p,
+               double* __restrict__ partial) {
   double s0 = 0.0, s1 = 0.0;
   for (int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x; t < n; t += (int64_t)gridDim.x * BLK) {
     const uint8_t ft = f[t];
     const double rt = (ft & F_DIR) ? 0.0 : b[t] - r[t];
-    const double zt = (ft & F_DIR) ? 0.0 : rt * diag[t];  // diag holds 1 / diag
+    const double zt = rt * dinv[t];
     r[t] = rt;
-    z[t] = zt;
     p[t] = zt;
     if (!(ft & F_NOTOWN)) {
       s0 = fma(rt, zt, s0);
@@ -149,94 +149,155 @@ __global__ void __launch_bounds__(BLK)
   write_partials(s0, s1, partial);
 }
 
+// V consecutive doubles (V = 2: one 16-byte access) of item i, nontemporal:
+// every vector entry is touched once per pass (tools/r03/stream_bench.cpp on
+// one MI355X: the residual pass 4.28 -> 4.78 TB/s, the step pass 4.46 ->
+// 4.66, against 5.0 TB/s for a plain double2 copy on that box)
+template <int V>
+__device__ __forceinline__ void ldv(const double* __restrict__ a, int64_t i, double (&o)[V]) {
+#pragma unroll
+  for (int e = 0; e < V; ++e) o[e] = __builtin_nontemporal_load(a + i * V + e);
+}
+template <int V>
+__device__ __forceinline__ void stv(double* __restrict__ a, int64_t i, const double (&o)[V]) {
+#pragma unroll
+  for (int e = 0; e < V; ++e) __builtin_nontemporal_store(o[e], a + i * V + e);
+}
+template <int V>
+__device__ __forceinline__ void ldf(const uint8_t* __restrict__ f, int64_t i, uint8_t (&o)[V]) {
+  if constexpr (V == 2) {
+    const uchar2 t = reinterpret_cast<const uchar2*>(f)[i];
+    o[0] = t.x;
+    o[1] = t.y;
+  } else {
+    o[0] = f[i];
+  }
+}
+
+// The vector kernels walk n / V items of V DOFs (16-byte accesses when
+// V = 2) in a grid-stride sequence, UNR / V items at a time with every load
+// issued before any use; the n % V last DOFs go to thread 0 of block 0.
 // partial sums of p.q over owned DOFs (p = 0 on Dirichlet DOFs)
+template <int V>
 __global__ void __launch_bounds__(BLK)
     k_cg_pq(const double* __restrict__ p, const double* __restrict__ q,
             const uint8_t* __restrict__ f, int64_t n, double* __restrict__ partial) {
+  constexpr int U = UNR / V;
   double s0 = 0.0;
-  const int64_t st = (int64_t)gridDim.x * BLK;
-  for (int64_t t0 = blockIdx.x * (int64_t)BLK + threadIdx.x; t0 < n; t0 += UNR * st) {
-    double pv[UNR], qv[UNR];
-    uint8_t fv[UNR];
+  const int64_t nv = n / V, st = (int64_t)gridDim.x * BLK;
+  for (int64_t i0 = blockIdx.x * (int64_t)BLK + threadIdx.x; i0 < nv; i0 += U * st) {
+    double pv[U][V], qv[U][V];
+    uint8_t fv[U][V];
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const int64_t t = t0 + u * st;
-      const bool ok = t < n;
-      pv[u] = ok ? p[t] : 0.0;
-      qv[u] = ok ? q[t] : 0.0;
-      fv[u] = ok ? f[t] : F_NOTOWN;
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * st < nv ? i0 + u * st : 0;
+      ldv<V>(p, i, pv[u]);
+      ldv<V>(q, i, qv[u]);
+      ldf<V>(f, i, fv[u]);
     }
 #pragma unroll
-    for (int u = 0; u < UNR; ++u)
-      if (!(fv[u] & F_NOTOWN)) s0 = fma(pv[u], qv[u], s0);
+    for (int u = 0; u < U; ++u)
+      if (i0 + u * st < nv)
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+          if (!(fv[u][e] & F_NOTOWN)) s0 = fma(pv[u][e], qv[u][e], s0);
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    for (int64_t t = nv * V; t < n; ++t)
+      if (!(f[t] & F_NOTOWN)) s0 = fma(p[t], q[t], s0);
   write_partials(s0, 0.0, partial);
 }
 
-// alpha = rz / pq (on the device); x += alpha p; r -= alpha q (free DOFs);
-// z = r / diag; partial sums of r.z and r.r
-__global__ void __launch_bounds__(BLK)
-    k_cg_update(double* __restrict__ x, double* __restrict__ r, double* __restrict__ z,
-                const double* __restrict__ p, const double* __restrict__ q,
-                const double* __restrict__ diag, const uint8_t* __restrict__ f,
-                const double* __restrict__ rz_old, const double* __restrict__ pq, int64_t n,
-                double* __restrict__ partial) {
+__device__ __forceinline__ double cg_alpha(const double* rz_old, const double* pq) {
   const double den = *pq;
-  const double alpha = den != 0.0 ? *rz_old / den : 0.0;
+  return den != 0.0 ? *rz_old / den : 0.0;
+}
+
+// alpha = rz / pq (on the device); r -= alpha q on free DOFs; partial sums of
+// r.z and r.r with z = r / diag formed on the fly (not stored: the step
+// kernel forms it again from r)
+template <int V>
+__global__ void __launch_bounds__(BLK)
+    k_cg_residual(double* __restrict__ r, const double* __restrict__ q,
+                  const double* __restrict__ dinv, const uint8_t* __restrict__ f,
+                  const double* __restrict__ rz_old, const double* __restrict__ pq, int64_t n,
+                  double* __restrict__ partial) {
+  constexpr int U = UNR / V;
+  const double alpha = cg_alpha(rz_old, pq);
   double s0 = 0.0, s1 = 0.0;
-  const int64_t st = (int64_t)gridDim.x * BLK;
-  for (int64_t t0 = blockIdx.x * (int64_t)BLK + threadIdx.x; t0 < n; t0 += UNR * st) {
-    double xv[UNR], pv[UNR], qv[UNR], rv[UNR], dv[UNR];
-    uint8_t fv[UNR];
+  auto one = [&](double qt, double rt, double dt, uint8_t ft) {
+    rt = (ft & F_DIR) ? 0.0 : fma(-alpha, qt, rt);
+    if (!(ft & F_NOTOWN)) {
+      s0 = fma(rt, rt * dt, s0);
+      s1 = fma(rt, rt, s1);
+    }
+    return rt;
+  };
+  const int64_t nv = n / V, st = (int64_t)gridDim.x * BLK;
+  for (int64_t i0 = blockIdx.x * (int64_t)BLK + threadIdx.x; i0 < nv; i0 += U * st) {
+    double qv[U][V], rv[U][V], dv[U][V];
+    uint8_t fv[U][V];
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const int64_t t = t0 + u * st;
-      const bool ok = t < n;
-      const int64_t tc = ok ? t : 0;
-      xv[u] = x[tc];
-      pv[u] = p[tc];
-      qv[u] = q[tc];
-      rv[u] = r[tc];
-      dv[u] = diag[tc];
-      fv[u] = ok ? f[tc] : (F_DIR | F_NOTOWN);
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * st < nv ? i0 + u * st : 0;
+      ldv<V>(q, i, qv[u]);
+      ldv<V>(r, i, rv[u]);
+      ldv<V>(dinv, i, dv[u]);
+      ldf<V>(f, i, fv[u]);
     }
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const int64_t t = t0 + u * st;
-      if (t >= n) continue;
-      x[t] = fma(alpha, pv[u], xv[u]);
-      const double rt = (fv[u] & F_DIR) ? 0.0 : fma(-alpha, qv[u], rv[u]);
-      const double zt = (fv[u] & F_DIR) ? 0.0 : rt * dv[u];  // dv = 1 / diag
-      r[t] = rt;
-      z[t] = zt;
-      if (!(fv[u] & F_NOTOWN)) {
-        s0 = fma(rt, zt, s0);
-        s1 = fma(rt, rt, s1);
-      }
+    for (int u = 0; u < U; ++u) {
+      if (i0 + u * st >= nv) continue;
+#pragma unroll
+      for (int e = 0; e < V; ++e) rv[u][e] = one(qv[u][e], rv[u][e], dv[u][e], fv[u][e]);
+      stv<V>(r, i0 + u * st, rv[u]);
     }
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    for (int64_t t = nv * V; t < n; ++t) r[t] = one(q[t], r[t], dinv[t], f[t]);
   write_partials(s0, s1, partial);
 }
 
-// beta = rz_new / rz_old (on the device); p = z + beta p
+// the rest of the iteration in one pass: x += alpha p with the p of this
+// iteration, then p = z + beta p with z = r / diag (0 on Dirichlet DOFs:
+// dinv is 0 there); beta = rz_new / rz_old on the device
+template <int V>
 __global__ void __launch_bounds__(BLK)
-    k_cg_p(double* __restrict__ p, const double* __restrict__ z,
-           const double* __restrict__ rz_new, const double* __restrict__ rz_old, int64_t n) {
+    k_cg_step(double* __restrict__ x, double* __restrict__ p, const double* __restrict__ r,
+              const double* __restrict__ dinv, const double* __restrict__ rz_new,
+              const double* __restrict__ rz_old, const double* __restrict__ pq, int64_t n) {
+  constexpr int U = UNR / V;
+  const double alpha = cg_alpha(rz_old, pq);
   const double den = *rz_old;
   const double beta = den != 0.0 ? *rz_new / den : 0.0;
-  const int64_t st = (int64_t)gridDim.x * BLK;
-  for (int64_t t0 = blockIdx.x * (int64_t)BLK + threadIdx.x; t0 < n; t0 += UNR * st) {
-    double pv[UNR], zv[UNR];
+  const int64_t nv = n / V, st = (int64_t)gridDim.x * BLK;
+  for (int64_t i0 = blockIdx.x * (int64_t)BLK + threadIdx.x; i0 < nv; i0 += U * st) {
+    double xv[U][V], pv[U][V], rv[U][V], dv[U][V];
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const int64_t tc = t0 + u * st < n ? t0 + u * st : 0;
-      pv[u] = p[tc];
-      zv[u] = z[tc];
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * st < nv ? i0 + u * st : 0;
+      ldv<V>(x, i, xv[u]);
+      ldv<V>(p, i, pv[u]);
+      ldv<V>(r, i, rv[u]);
+      ldv<V>(dinv, i, dv[u]);
     }
 #pragma unroll
-    for (int u = 0; u < UNR; ++u)
-      if (t0 + u * st < n) p[t0 + u * st] = fma(beta, pv[u], zv[u]);
+    for (int u = 0; u < U; ++u) {
+      if (i0 + u * st >= nv) continue;
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        xv[u][e] = fma(alpha, pv[u][e], xv[u][e]);
+        pv[u][e] = fma(beta, pv[u][e], rv[u][e] * dv[u][e]);
+      }
+      stv<V>(x, i0 + u * st, xv[u]);
+      stv<V>(p, i0 + u * st, pv[u]);
+    }
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    for (int64_t t = nv * V; t < n; ++t) {
+      x[t] = fma(alpha, p[t], x[t]);
+      p[t] = fma(beta, p[t], r[t] * dinv[t]);
+    }
 }
 
 // fixed-order sum of the partials: out[0..nd) (deterministic run to run);
@@ -322,8 +383,12 @@ struct sem_dd {
   // HIP graphs around the transport call -- S: gather, interface elements,
   // pack (side stream); M: interior elements (caller's stream); F: unpack
   // per peer (side); G: y[cidx] += y_c (caller's) -- replayed while the
-  // kind and the u / y pointers stay the same
-  bool graphs = true;
+  // kind and the u / y pointers stay the same.  Off by default: on ROCm 7
+  // a graph launch costs more host time than the launches it replaces
+  // (profiles/r03/multirank/: 2-rank rehearsal 0.787 ms per step eager,
+  // 0.866 captured; tools/r03/stream_bench.cpp: 11.3 us per 2-kernel graph
+  // replay against 4.7 us eager); SEM_DD_GRAPH=1 or sem_dd_set_graphs opt in
+  bool graphs = false;
   hipStream_t cap = nullptr;  // capture stream of M and G
   hipGraphExec_t gS = nullptr, gM = nullptr, gF = nullptr, gG = nullptr;
   int g_kind = -1;
@@ -577,17 +642,20 @@ int pcg_run(const PcgOp& op, int kind, const double* b, double* x, const uint8_t
   DeviceGuard g(op.device);
   const int64_t n = op.n;
   PcgScratch s;
-  HIP_TRY(hipMalloc(&s.base, 5 * n * sizeof(double)));
+  // r, p, q, 1/diag; rows padded to 32 doubles (16-byte vector accesses)
+  const int64_t nn = (n + 31) / 32 * 32;
+  HIP_TRY(hipMalloc(&s.base, 4 * nn * sizeof(double)));
   HIP_TRY(hipMalloc(&s.flags, n));
   // partials [2][RED_BLOCKS], then scalars: T0 = (rz, rr), T1 = (rz, rr), pq
   HIP_TRY(hipMalloc(&s.red, (2 * RED_BLOCKS + 8) * sizeof(double)));
   HIP_TRY(hipMalloc(&s.hist, ((size_t)max_iter + 1) * sizeof(double)));
   HIP_TRY(hipHostMalloc(&s.h_hist, ((size_t)check + 1) * sizeof(double)));
   double* r = s.base;
-  double* z = r + n;
-  double* p = z + n;
-  double* q = p + n;
-  double* dg = q + n;
+  double* p = r + nn;
+  double* q = p + nn;
+  double* dg = q + nn;
+  // x is the caller's: 16-byte aligned -> the paired kernels
+  const bool v2 = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
   double* partial = s.red;
   double* T[2] = {s.red + 2 * RED_BLOCKS, s.red + 2 * RED_BLOCKS + 2};
   double* pq = s.red + 2 * RED_BLOCKS + 4;
@@ -595,9 +663,9 @@ int pcg_run(const PcgOp& op, int kind, const double* b, double* x, const uint8_t
   const bool multi = op.dd && op.dd->world > 1;  // dots need an all-reduce
   hipLaunchKernelGGL(k_cg_flags, dim3(grid_for(n)), dim3(BLK), 0, st, dir, notown, n, s.flags);
   SEM_TRY(op.diag(kind, dg, st));
-  hipLaunchKernelGGL(k_cg_invert, dim3(grid_for(n)), dim3(BLK), 0, st, dg, n);
+  hipLaunchKernelGGL(k_cg_invert, dim3(grid_for(n)), dim3(BLK), 0, st, dg, s.flags, n);
   SEM_TRY(op.apply(kind, x, r, st));
-  hipLaunchKernelGGL(k_cg_start, dim3(gb), dim3(BLK), 0, st, b, r, dg, s.flags, n, z, p, partial);
+  hipLaunchKernelGGL(k_cg_start, dim3(gb), dim3(BLK), 0, st, b, r, dg, s.flags, n, p, partial);
   hipLaunchKernelGGL(k_cg_finish, dim3(1), dim3(BLK), 0, st, partial, gb, 2, T[0], nullptr);
   HIP_TRY(hipGetLastError());
   SEM_TRY(dd_allreduce(op.dd, T[0], 2, st));
@@ -619,19 +687,24 @@ int pcg_run(const PcgOp& op, int kind, const double* b, double* x, const uint8_t
         SEM_TRY(sem_apply_dot(op.ctx, kind, p, q, pq, st));
       } else {
         SEM_TRY(op.apply(kind, p, q, st));
-        hipLaunchKernelGGL(k_cg_pq, dim3(gb), dim3(BLK), 0, st, p, q, s.flags, n, partial);
+        hipLaunchKernelGGL(k_cg_pq<2>, dim3(gb), dim3(BLK), 0, st, p, q, s.flags, n, partial);
         hipLaunchKernelGGL(k_cg_finish, dim3(1), dim3(BLK), 0, st, partial, gb, 1, pq, nullptr);
         SEM_TRY(dd_allreduce(op.dd, pq, 1, st));
       }
-      hipLaunchKernelGGL(k_cg_update, dim3(gb), dim3(BLK), 0, st, x, r, z, p, q, dg, s.flags,
-                         T[o], pq, n, partial);
+      hipLaunchKernelGGL(k_cg_residual<2>, dim3(gb), dim3(BLK), 0, st, r, q, dg, s.flags, T[o],
+                         pq, n, partial);
       hipLaunchKernelGGL(k_cg_finish, dim3(1), dim3(BLK), 0, st, partial, gb, 2, T[nw],
                          multi ? nullptr : s.hist + it + 1);
       if (multi) {
         SEM_TRY(dd_allreduce(op.dd, T[nw], 2, st));
         hipLaunchKernelGGL(k_cg_record, dim3(1), dim3(WV), 0, st, T[nw] + 1, s.hist + it + 1);
       }
-      hipLaunchKernelGGL(k_cg_p, dim3(gb), dim3(BLK), 0, st, p, z, T[nw], T[o], n);
+      if (v2)
+        hipLaunchKernelGGL(k_cg_step<2>, dim3(gb), dim3(BLK), 0, st, x, p, r, dg, T[nw], T[o], pq,
+                           n);
+      else
+        hipLaunchKernelGGL(k_cg_step<1>, dim3(gb), dim3(BLK), 0, st, x, p, r, dg, T[nw], T[o], pq,
+                           n);
       HIP_TRY(hipGetLastError());
       if (g_sync_each) HIP_TRY(hipDeviceSynchronize());  // diagnostic
       ++it;

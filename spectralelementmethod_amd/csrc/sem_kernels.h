@@ -399,33 +399,60 @@ __device__ __forceinline__ void emit2(double* __restrict__ y, uint32_t raw, doub
   }
 }
 
-// row i of the tile (RS doubles, 16-B aligned when RS is even) -> registers
-template <int N, int RS>
-__device__ __forceinline__ void load_row(const double* L, int i, double (&r)[RS]) {
-  if constexpr (RS % 2 == 0) {
+// SEM_LDS_SPLIT: tile loads of the nodal kernel as single 8-byte LDS reads.
+// The compiler pairs neighbouring reads into ds_read2_b64, which the MI355X
+// LDS serves at half the rate of two ds_read_b64 (MI355X_MICROARCH.md §LDS:
+// 8 cycles against 2 x 2); a volatile access is never paired (and keeps the
+// LDS address space: a generic volatile pointer became flat loads and
+// spilled).  p = 8 at 1024^2, alternating on one box: 0.6726-0.6803 against
+// 0.6827-0.6882 ms per step (profiles/r03/tile_layout/).
+#ifndef SEM_LDS_SPLIT
+#define SEM_LDS_SPLIT 1
+#endif
+#ifndef SEM_LDS_SPLIT_STORED  // the same for the column reads of the stored-factor kernel
+#define SEM_LDS_SPLIT_STORED 0
+#endif
+template <bool SPLIT>
+__device__ __forceinline__ double lds_ld(const double* p) {
+  if constexpr (SPLIT)
+    return *(const volatile __attribute__((address_space(3))) double*)(p);
+  else
+    return *p;
+}
+
+// row i of the tile (RL doubles at row stride RS; 16-B aligned loads when
+// both are even) -> registers
+template <int N, int RS, int RL = RS, bool SPLIT = false>
+__device__ __forceinline__ void load_row(const double* L, int i, double (&r)[RL]) {
+  if constexpr (RL % 2 == 0 && RS % 2 == 0) {
     const double2* row = reinterpret_cast<const double2*>(L + i * RS);
 #pragma unroll
-    for (int s = 0; s < RS / 2; ++s) {
+    for (int s = 0; s < RL / 2; ++s) {
       const double2 v = row[s];
       r[2 * s] = v.x;
       r[2 * s + 1] = v.y;
     }
   } else {
 #pragma unroll
-    for (int s = 0; s < RS; ++s) r[s] = L[i * RS + s];
+    for (int s = 0; s < RL; ++s) r[s] = lds_ld<SPLIT>(L + i * RS + s);
   }
 }
 
-template <int N, int RS>
-__device__ __forceinline__ void store_row(double* L, int i, const double (&t)[N]) {
+// ACTIVE false: the lane stores at L + JUNK instead of its row (padding
+// lanes of the wave-linear tile, whose row would run into the next tile row;
+// an address select, not a branch: a masked store region spilled registers)
+template <int N, int RS, int JUNK = 0>
+__device__ __forceinline__ void store_row(double* L, int i, const double (&t)[N],
+                                          bool active = true) {
+  double* row = L + (active ? i * RS : JUNK);
   if constexpr (RS % 2 == 0) {
-    double2* row = reinterpret_cast<double2*>(L + i * RS);
+    double2* row2 = reinterpret_cast<double2*>(row);
 #pragma unroll
-    for (int s = 0; s < N / 2; ++s) row[s] = make_double2(t[2 * s], t[2 * s + 1]);
-    if (N % 2) L[i * RS + N - 1] = t[N - 1];
+    for (int s = 0; s < N / 2; ++s) row2[s] = make_double2(t[2 * s], t[2 * s + 1]);
+    if (N % 2) row[N - 1] = t[N - 1];
   } else {
 #pragma unroll
-    for (int s = 0; s < N; ++s) L[i * RS + s] = t[s];
+    for (int s = 0; s < N; ++s) row[s] = t[s];
   }
 }
 
@@ -458,17 +485,42 @@ struct Tile {
   }
 };
 
+// Wave-linear tiles (nodal Poisson kernel): the wave's EPW element tiles
+// side by side, element k at column offset k*N of one N x WL_RS array,
+//   T[k][r][c] at  wave base + r*WL_RS + k*N + c,   WL_RS = 65 (= 1 mod 32).
+// A column access (fixed r) is the wave's lanes in order, a row access
+// (lane (k, j) reads row j) is lane + 64 j + c: both free of bank conflicts
+// for 64-bit LDS accesses (MI355X_MICROARCH.md §LDS), where the element-slot
+// layout (slot stride N*N) has 2-way conflicts on every column access.  The
+// padding lanes' columns are the spare columns LW..64 of each row; their
+// row stores go to a junk row after the wave's N rows (theirs would run into
+// the next tile row).
+#ifndef SEM_TILE_WL
+#define SEM_TILE_WL 0
+#endif
+constexpr int WL_RS = 65;
+template <int N>
+struct WLTile {
+  static constexpr int RS = WL_RS;
+  static constexpr int LW = (WAVE / N) * N;
+  static constexpr int WS = N * WL_RS + N;  // doubles per wave: N rows + the junk row
+  static constexpr int JUNK = N * WL_RS - LW;  // junk row, from a padding lane's base
+  __device__ static int base(int wave, int k) { return wave * WS + k * N; }
+};
+
 // Row pass on a wave-private tile: the lane's row j (written column-wise by
 // the wave and synchronised) is contracted with D (or D^T when TR) and
 // written back, so the tile again holds the result in column layout.  REL
 // differentiates relative to the row's first entry (see poisson_group_nodal).
+// RL: doubles loaded per row (RS, or N on the wave-linear tile); ACTIVE:
+// whether the lane stores its row.
 #ifndef SEM_ROW_STORE_PAIRS_N
 #define SEM_ROW_STORE_PAIRS_N 17  // orders from which row passes store output pairs directly
 #endif
-template <int N, int RS, bool TR, bool REL>
-__device__ __forceinline__ void row_pass(double* L, int j, const DEO<N>& D) {
-  double r[RS], x[N];
-  load_row<N, RS>(L, j, r);
+template <int N, int RS, bool TR, bool REL, int RL = RS, int JUNK = 0, bool SPLIT = false>
+__device__ __forceinline__ void row_pass(double* L, int j, const DEO<N>& D, bool active = true) {
+  double r[RL], x[N];
+  load_row<N, RS, RL, SPLIT>(L, j, r);
 #pragma unroll
   for (int q = 0; q < N; ++q) x[q] = REL ? r[q] - r[0] : r[q];
   if constexpr (N >= SEM_ROW_STORE_PAIRS_N) {
@@ -482,7 +534,7 @@ __device__ __forceinline__ void row_pass(double* L, int j, const DEO<N>& D) {
     else
       deo_apply<N>(D, x, t);
     wave_sync();
-    store_row<N, RS>(L, j, t);
+    store_row<N, RS, JUNK>(L, j, t, active);
   }
   wave_sync();
 }
@@ -558,6 +610,7 @@ __device__ __forceinline__ void poisson_group_stored(const MapRef& mref,
   using T = Tile<N, SEM_TILE_PAD_STORED>;
   constexpr int LW = T::LW;
   constexpr int RS = T::RS;
+  constexpr bool SP = SEM_LDS_SPLIT_STORED;
   const double* gp = GP + g * (int64_t)(3 * N * LW) + lane;
   double uc[N];
   load_map<N, M16>(mref, g, lane, in_wave, raw);
@@ -578,7 +631,7 @@ __device__ __forceinline__ void poisson_group_stored(const MapRef& mref,
     double w0[N];
 #pragma unroll
     for (int m = 0; m < N; ++m) {
-      const double d1 = L[m * RS + j];
+      const double d1 = lds_ld<SP>(L + m * RS + j);
       const double g00 = gp[(0 * N + m) * LW];
       const double g01 = gp[(1 * N + m) * LW];
       const double g11 = gp[(2 * N + m) * LW];
@@ -595,7 +648,7 @@ __device__ __forceinline__ void poisson_group_stored(const MapRef& mref,
   // row i = j: yb[i][q] = sum_n D[n][q] w1[i][n]
   row_pass<N, RS, true, false>(L, j, D);
 #pragma unroll
-  for (int p = 0; p < N; ++p) v[p] += L[p * RS + j];
+  for (int p = 0; p < N; ++p) v[p] += lds_ld<SP>(L + p * RS + j);
   wave_sync();  // the tile is rewritten by the next group of this wave
 }
 
@@ -648,11 +701,23 @@ __device__ __forceinline__ void gather_u(const double* __restrict__ u, const uin
 // geometry of the group from its node coordinates: (dx/dr, dy/dr) along the
 // column, (dx/ds, dy/ds) along the row -> G00, G01 in registers, G11 parked
 // in tile B (free until the next group) to save registers
+// the nodal kernel's tile: wave-linear (SEM_TILE_WL) below the orders whose
+// row passes store pairs directly (unmasked), element slots otherwise
+template <int N>
+struct NodalTile {
+  static constexpr bool wl = SEM_TILE_WL && N < SEM_ROW_STORE_PAIRS_N;
+  static constexpr int RS = wl ? WL_RS : Tile<N, SEM_TILE_PAD_NODAL>::RS;
+  static constexpr int RL = wl ? N : RS;  // doubles loaded per row
+  static constexpr int JUNK = wl ? WLTile<N>::JUNK : 0;
+  static constexpr bool split = SEM_LDS_SPLIT;
+};
+
 template <int N>
 __device__ __forceinline__ void nodal_geometry(const double2 (&xc)[N], int j, double* A, double* B,
                                                const DEO<N>& D, const WVec<N>& w, double wj,
-                                               double (&g00)[N], double (&g01)[N]) {
-  constexpr int RS = Tile<N, SEM_TILE_PAD_NODAL>::RS;
+                                               double (&g00)[N], double (&g01)[N], bool in_wave) {
+  constexpr int RS = NodalTile<N>::RS;
+  constexpr int RL = NodalTile<N>::RL;
   double jr0[N], jr1[N];
   {
     double ta[N], tb[N];
@@ -671,9 +736,9 @@ __device__ __forceinline__ void nodal_geometry(const double2 (&xc)[N], int j, do
   }
   wave_sync();
   {
-    double xa[RS], xb[RS], ra[N], rb[N], ta[N], tb[N];
-    load_row<N, RS>(A, j, xa);
-    load_row<N, RS>(B, j, xb);
+    double xa[RL], xb[RL], ra[N], rb[N], ta[N], tb[N];
+    load_row<N, RS, RL, NodalTile<N>::split>(A, j, xa);
+    load_row<N, RS, RL, NodalTile<N>::split>(B, j, xb);
 #pragma unroll
     for (int q = 0; q < N; ++q) {
       ra[q] = xa[q] - xa[0];
@@ -682,13 +747,14 @@ __device__ __forceinline__ void nodal_geometry(const double2 (&xc)[N], int j, do
     deo_apply<N>(D, ra, ta);
     deo_apply<N>(D, rb, tb);
     wave_sync();
-    store_row<N, RS>(A, j, ta);
-    store_row<N, RS>(B, j, tb);
+    store_row<N, RS, NodalTile<N>::JUNK>(A, j, ta, in_wave || !NodalTile<N>::wl);
+    store_row<N, RS, NodalTile<N>::JUNK>(B, j, tb, in_wave || !NodalTile<N>::wl);
   }
   wave_sync();
 #pragma unroll
   for (int m = 0; m < N; ++m) {
-    const double js0 = A[m * RS + j], js1 = B[m * RS + j];
+    constexpr bool SP = NodalTile<N>::split;
+    const double js0 = lds_ld<SP>(A + m * RS + j), js1 = lds_ld<SP>(B + m * RS + j);
     const double det = jr0[m] * js1 - js0 * jr1[m];
     // (w_m w_j) / det, associated so that no loop-invariant w_m w_j array
     // is hoisted out of the round loop (9 doubles spilled at 4 waves/SIMD)
@@ -707,21 +773,25 @@ __device__ __forceinline__ void nodal_laplacian(const double (&uc)[N], int j, do
                                                 const double (&g00)[N], const double (&g01)[N],
                                                 double (&v)[N], const double* __restrict__ y,
                                                 const uint32_t (&raw)[N], int accumulate,
-                                                double (&prev)[N], const Pre& pre = Pre()) {
-  constexpr int RS = Tile<N, SEM_TILE_PAD_NODAL>::RS;
+                                                double (&prev)[N], bool in_wave,
+                                                const Pre& pre = Pre()) {
+  constexpr int RS = NodalTile<N>::RS;
+  constexpr int RL = NodalTile<N>::RL;
+  const bool act = in_wave || !NodalTile<N>::wl;
   double d0[N];
   deo_apply<N>(D, uc, d0);
 #pragma unroll
   for (int r = 0; r < N; ++r) A[r * RS + j] = uc[r];
   wave_sync();
-  row_pass<N, RS, false, false>(A, j, D);
+  constexpr bool SP = NodalTile<N>::split;
+  row_pass<N, RS, false, false, RL, NodalTile<N>::JUNK, SP>(A, j, D, act);
   {
     double w0[N];
 #pragma unroll
     for (int m = 0; m < N; ++m) {
-      const double d1 = A[m * RS + j];
+      const double d1 = lds_ld<SP>(A + m * RS + j);
       w0[m] = fma(g00[m], d0[m], g01[m] * d1);
-      A[m * RS + j] = fma(g01[m], d0[m], B[m * RS + j] * d1);
+      A[m * RS + j] = fma(g01[m], d0[m], lds_ld<SP>(B + m * RS + j) * d1);
     }
     constexpr int PF = Pre::prefetch ? RmwPrefetch<N>::value : 0;
     if constexpr (PF) pre();
@@ -730,9 +800,9 @@ __device__ __forceinline__ void nodal_laplacian(const double (&uc)[N], int j, do
     if constexpr (PF == 2) rmw_prefetch<N, Pre::aux>(y, raw, accumulate, prev);
   }
   wave_sync();
-  row_pass<N, RS, true, false>(A, j, D);
+  row_pass<N, RS, true, false, RL, NodalTile<N>::JUNK, SP>(A, j, D, act);
 #pragma unroll
-  for (int p = 0; p < N; ++p) v[p] += A[p * RS + j];
+  for (int p = 0; p < N; ++p) v[p] += lds_ld<SP>(A + p * RS + j);
   wave_sync();  // the tiles are rewritten by the next group of this wave
 }
 
@@ -755,11 +825,11 @@ __device__ __forceinline__ void poisson_group_nodal(const MapRef& mref,
   gather_u<N>(u, raw, uc);
 #endif
   double g00[N], g01[N];
-  nodal_geometry<N>(xc, j, A, B, D, w, wj, g00, g01);
+  nodal_geometry<N>(xc, j, A, B, D, w, wj, g00, g01, in_wave);
 #if !SEM_NODAL_EARLY_U
   gather_u<N>(u, raw, uc);
 #endif
-  nodal_laplacian<N>(uc, j, A, B, D, g00, g01, v, y, raw, accumulate, prev, pre);
+  nodal_laplacian<N>(uc, j, A, B, D, g00, g01, v, y, raw, accumulate, prev, in_wave, pre);
 }
 
 
@@ -898,8 +968,10 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
                     const DEO<N> D, const WVec<N> w, const SeamPlan sp) {
   using T = Tile<N, NODAL ? SEM_TILE_PAD_NODAL : SEM_TILE_PAD_STORED>;
   constexpr int NT = NODAL ? 2 : 1;  // tiles per element slot
-  __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * T::ES * NT];
   constexpr int CW = ChainWaves<N>::value;
+  constexpr bool WL = NODAL && NodalTile<N>::wl;
+  constexpr int PLANE = WL ? CW * WLTile<N>::WS : T::TILE_SLOTS * T::ES;  // doubles per tile plane
+  __shared__ __attribute__((aligned(16))) double lds[PLANE * NT];
   __shared__ double carry[2][CW][1][N];
   const int64_t chain = c0 + xcd_block(blockIdx.x, gridDim.x);
   if (chain >= c1) {  // uniform over the workgroup
@@ -913,11 +985,11 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
   const int k = lane / N;
   const int j = lane - k * N;
   const bool in_wave = lane < T::LW;
-  // tile planes: all slots of tile A, then all slots of tile B (slot stride
-  // ES in each plane; interleaving A/B per slot doubles the stride and makes
-  // the column accesses 2-way bank conflicts)
-  double* L = lds + T::slot(wave, k, in_wave) * T::ES;
-  double* LB = L + (NT - 1) * T::TILE_SLOTS * T::ES;
+  // tile planes: all of tile A, then all of tile B (interleaving A/B per
+  // slot doubles the stride and makes the column accesses 2-way bank
+  // conflicts)
+  double* L = lds + (WL ? WLTile<N>::base(wave, k) : T::slot(wave, k, in_wave) * T::ES);
+  double* LB = L + (NT - 1) * PLANE;
   const double wj = pick<N>(w, j);
   double rowc[1] = {0.0};
   for (int rd = 0; rd < rounds; ++rd) {

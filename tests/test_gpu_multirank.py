@@ -377,7 +377,7 @@ def _graph_worker(rank, world, port, q):
 
 
 def test_captured_step_equals_eager(gpu):
-    """sem_dd_apply through its captured graphs (the default) equals the
+    """sem_dd_apply through its captured graphs (opt-in) equals the
     eager enqueue bit for bit on 2 ranks of one device (torch transport
     between the graph segments); the PCG over the decomposition agrees to
     rounding (its Jacobi diagonal is an atomic sum)."""
