@@ -405,7 +405,7 @@ __device__ __forceinline__ void emit2(double* __restrict__ y, uint32_t raw, doub
 // 8 cycles against 2 x 2); a volatile access is never paired (and keeps the
 // LDS address space: a generic volatile pointer became flat loads and
 // spilled).  p = 8 at 1024^2, alternating on one box: 0.6726-0.6803 against
-// 0.6827-0.6882 ms per step (profiles/r03/tile_layout/).
+// 0.6827-0.6882 ms per step (profiles/r03/lds_split/).
 #ifndef SEM_LDS_SPLIT
 #define SEM_LDS_SPLIT 1
 #endif
