@@ -409,8 +409,14 @@ __device__ __forceinline__ void emit2(double* __restrict__ y, uint32_t raw, doub
 #ifndef SEM_LDS_SPLIT
 #define SEM_LDS_SPLIT 1
 #endif
-#ifndef SEM_LDS_SPLIT_STORED  // the same for the column reads of the stored-factor kernel
-#define SEM_LDS_SPLIT_STORED 0
+// the same for the column reads of the stored-factor kernel, from order
+// SEM_LDS_SPLIT_STORED_N (profiles/r03/lds_split/stored/: p = 16 0.141-0.146
+// -> 0.138-0.139 ms, but p = 6 0.126 -> 0.134 and p = 12 neutral)
+#ifndef SEM_LDS_SPLIT_STORED_N
+#define SEM_LDS_SPLIT_STORED_N 17
+#endif
+#ifndef SEM_LDS_SPLIT_AXI  // and of the fields-first axisymmetric nodal kernel
+#define SEM_LDS_SPLIT_AXI 0
 #endif
 template <bool SPLIT>
 __device__ __forceinline__ double lds_ld(const double* p) {
@@ -610,7 +616,7 @@ __device__ __forceinline__ void poisson_group_stored(const MapRef& mref,
   using T = Tile<N, SEM_TILE_PAD_STORED>;
   constexpr int LW = T::LW;
   constexpr int RS = T::RS;
-  constexpr bool SP = SEM_LDS_SPLIT_STORED;
+  constexpr bool SP = N >= SEM_LDS_SPLIT_STORED_N;
   const double* gp = GP + g * (int64_t)(3 * N * LW) + lane;
   double uc[N];
   load_map<N, M16>(mref, g, lane, in_wave, raw);
@@ -1450,6 +1456,7 @@ __device__ __forceinline__ void axisym_group_nodal3(const MapRef& mref,
                                                     uint32_t (&raw)[N], double (&vo)[N],
                                                     double (&vp)[N]) {
   constexpr int RS = Tile<N>::RS;
+  constexpr bool SP = SEM_LDS_SPLIT_AXI;
   load_map<N, M16>(mref, g, lane, in_wave, raw);
   const double2* u2 = reinterpret_cast<const double2*>(u);
   double om[N], d0p[N], d0o[N];
@@ -1490,7 +1497,7 @@ __device__ __forceinline__ void axisym_group_nodal3(const MapRef& mref,
     wave_sync();
     row_pass<N, RS, false, true>(LG, j, D);
 #pragma unroll
-    for (int m = 0; m < N; ++m) js0[m] = LG[m * RS + j];
+    for (int m = 0; m < N; ++m) js0[m] = lds_ld<SP>(LG + m * RS + j);
     wave_sync();
 #pragma unroll
     for (int r = 0; r < N; ++r) LG[r * RS + j] = xc[r].y;
@@ -1498,12 +1505,12 @@ __device__ __forceinline__ void axisym_group_nodal3(const MapRef& mref,
   wave_sync();
   row_pass<N, RS, false, true>(LG, j, D);
 #pragma unroll
-  for (int m = 0; m < N; ++m) js1[m] = LG[m * RS + j];
+  for (int m = 0; m < N; ++m) js1[m] = lds_ld<SP>(LG + m * RS + j);
   // pointwise (squirmer-axisymmetric.py:193-227), as axisym_group_nodal
 #pragma unroll
   for (int m = 0; m < N; ++m) {
-    const double d1p = LP[m * RS + j];
-    const double d1o = LO[m * RS + j];
+    const double d1p = lds_ld<SP>(LP + m * RS + j);
+    const double d1o = lds_ld<SP>(LO + m * RS + j);
     const double det = jr0[m] * js1[m] - js0[m] * jr1[m];
     const double wm = w.v[m];
     const double rs = rho[m] * (wm * (wj * fast_rcp(det)));
@@ -1536,8 +1543,8 @@ __device__ __forceinline__ void axisym_group_nodal3(const MapRef& mref,
   row_pass<N, RS, true, false>(LO, j, D);
 #pragma unroll
   for (int p = 0; p < N; ++p) {
-    vo[p] += LO[p * RS + j];
-    vp[p] += LP[p * RS + j];
+    vo[p] += lds_ld<SP>(LO + p * RS + j);
+    vp[p] += lds_ld<SP>(LP + p * RS + j);
   }
   wave_sync();
 }
