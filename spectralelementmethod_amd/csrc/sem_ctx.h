@@ -105,6 +105,7 @@ struct sem_ctx {
   // seam plan of the Poisson column kernel (SeamPlan, sem_kernels.h)
   bool blocks = false;       // block layout of the chains (groups_blocks)
   int64_t row_carries = 0;
+  bool round_sync = true;  // a chain writes some node in two rounds (Plan::round_rmw)
   bool seam = false;
   bool seam_dot = false;    // sem_apply_dot fuses u.y into the seam plan's launches
   double* d_dot = nullptr;  // u.y partials of sem_apply_dot (chains + seam-sum blocks)

@@ -283,6 +283,7 @@ struct Plan {
   bool blocks = false;     // block layout (groups_blocks)
   int block_rounds = 0;
   int64_t row_carries = 0;  // entries carried to the next round in registers
+  bool round_rmw = true;  // some chain read-modify-writes a node it stored in an earlier round
   // seam plan: chains in element order, one launch; nodes written by several
   // chains go through per-colour slots summed by k_seam_sum
   bool seam = false;
@@ -516,6 +517,7 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
   std::vector<uint8_t> act((size_t)CH * n * lw);
   P.n_atomic_groups = 0;
   P.row_carries = 0;
+  P.round_rmw = false;
   bool seam_conflict = false;
   auto lane_elem = [&](int64_t g, int lane) -> int64_t {
     const int k = lane / n;
@@ -564,8 +566,9 @@ int build_plan(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node,
                 // an earlier round of this chain stored the node into its
                 // seam slot: a second plain slot store would drop it
                 seam_conflict = true;
+              } else {
+                P.round_rmw = true;  // an earlier round of this chain: sequential, RMW
               }
-              // else: an earlier round of this chain -> sequential, RMW
             }
             lastc[gid] = ch;
             lastt[gid] = tag;
@@ -1142,6 +1145,7 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
   c->rounds = mfma ? 1 : rounds;
   c->blocks = !mfma && !c->ecol && P.blocks;
   c->row_carries = c->blocks ? P.row_carries : 0;
+  c->round_sync = c->ecol || P.round_rmw;
   c->n_slots = P.n_slots;
   std::vector<uint32_t>().swap(h);
   c->d_e2n = d_e2n;

@@ -839,6 +839,28 @@ __device__ __forceinline__ void poisson_group_nodal(const MapRef& mref,
 }
 
 
+// the value of lane + 1 (lane 63: its own).  SEM_DPP_SHIFT: a DPP
+// wave_shl:1 move per dword (two VALU moves) instead of __shfl_down, whose
+// ds_bpermute goes through the LDS and waits on it
+#ifndef SEM_DPP_SHIFT
+#define SEM_DPP_SHIFT 1
+#endif
+__device__ __forceinline__ double lane_next(double x) {
+#if SEM_DPP_SHIFT
+  constexpr int WAVE_SHL1 = 0x130;
+  const int lo = __double2loint(x), hi = __double2hiint(x);
+  return __hiloint2double(__builtin_amdgcn_update_dpp(hi, hi, WAVE_SHL1, 0xF, 0xF, false),
+                          __builtin_amdgcn_update_dpp(lo, lo, WAVE_SHL1, 0xF, 0xF, false));
+#else
+  return __shfl_down(x, 1, WAVE);
+#endif
+}
+
+#ifndef SEM_ROUND_SYNC_ALWAYS
+#define SEM_ROUND_SYNC_ALWAYS 0
+#endif
+constexpr int CARRY_BUFS = 3;
+
 // Scatter of one group's column values through the coded map, with the
 // in-group merge (next lane) and the chain carry (previous group) applied.
 // ncomp values per node (1: Poisson, 2: axisymmetric block).
@@ -849,7 +871,7 @@ template <int N, int NC, bool PRE = false, int CW = ChainWaves<N>::value, bool S
 __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_t (&raw)[N],
                                            double (&v)[NC][N], int lane, int wave, int rd,
                                            bool in_wave, double (*carry)[CW][NC][N],
-                                           double (&rowc)[NC], int accumulate,
+                                           double (&rowc)[NC], int accumulate, bool round_sync,
                                            const double* prev = nullptr,
                                            const SeamOut& so = SeamOut(),
                                            const double* __restrict__ du = nullptr,
@@ -868,7 +890,7 @@ __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_
   for (int c = 0; c < NC; ++c)
 #pragma unroll
     for (int p = 0; p < N; ++p) {
-      const double vn = __shfl_down(v[c][p], 1, WAVE);
+      const double vn = lane_next(v[c][p]);
       if ((raw[p] >> CODE_SHIFT) & W_MERGE) v[c][p] += vn;
     }
   // hand the last lane's column to the next group of the chain
@@ -876,12 +898,12 @@ __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_
 #pragma unroll
     for (int c = 0; c < NC; ++c)
 #pragma unroll
-      for (int p = 0; p < N; ++p) carry[rd & 1][wave][c][p] = v[c][p];
+      for (int p = 0; p < N; ++p) carry[rd % CARRY_BUFS][wave][c][p] = v[c][p];
   }
   __syncthreads();
   if (lane == 0) {
-    const double* src = (wave > 0) ? &carry[rd & 1][wave - 1][0][0]
-                                   : &carry[(rd + 1) & 1][CW - 1][0][0];
+    const double* src = (wave > 0) ? &carry[rd % CARRY_BUFS][wave - 1][0][0]
+                                   : &carry[(rd + CARRY_BUFS - 1) % CARRY_BUFS][CW - 1][0][0];
 #pragma unroll
     for (int p = 0; p < N; ++p)
       if ((raw[p] >> CODE_SHIFT) & W_CARRY) {
@@ -909,8 +931,12 @@ __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_
         emit2(y, raw[p], v[0][p], v[NC - 1][p], accumulate);
     }
   }
-  // this round's stores and carry reads complete before the next round
-  __syncthreads();
+  // this round's stores complete before the next round's read-modify-writes
+  // of the same nodes: only plans in which a chain writes a node in two
+  // rounds need it (SeamPlan::round_sync); the carry slots need no second
+  // barrier with three buffers (a slot is rewritten three rounds later,
+  // after its reader has passed the next round's first barrier)
+  if (SEM_ROUND_SYNC_ALWAYS || round_sync) __syncthreads();
 }
 
 // Workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8 share
@@ -949,6 +975,7 @@ struct SeamPlan {
   double* buf;                         // [colour][node]
   int64_t n_node;
   double* dot = nullptr;  // DOT kernels: one partial of u.y per workgroup
+  int round_sync = 1;     // a chain writes some node in two rounds: order the rounds
 };
 
 // sum of one value per thread over the workgroup, in a fixed order (wave
@@ -978,7 +1005,7 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
   constexpr bool WL = NODAL && NodalTile<N>::wl;
   constexpr int PLANE = WL ? CW * WLTile<N>::WS : T::TILE_SLOTS * T::ES;  // doubles per tile plane
   __shared__ __attribute__((aligned(16))) double lds[PLANE * NT];
-  __shared__ double carry[2][CW][1][N];
+  __shared__ double carry[CARRY_BUFS][CW][1][N];
   const int64_t chain = c0 + xcd_block(blockIdx.x, gridDim.x);
   if (chain >= c1) {  // uniform over the workgroup
     if constexpr (DOT)
@@ -1014,7 +1041,7 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
     SeamOut so;
     if constexpr (SEAM) so.base = sp.buf + sp.colour[chain] * sp.n_node;
     chain_emit<N, 1, PRE, CW, SEAM, DOT>(y, raw, v, lane, wave, rd, in_wave, carry, rowc,
-                                         accumulate, prev, so, u, &dotv);
+                                         accumulate, sp.round_sync, prev, so, u, &dotv);
   }
   if constexpr (DOT) {
     __shared__ double sh[CW];
@@ -1569,7 +1596,7 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, AxiNodal<N>::waves)
   constexpr int NPL = AxiNodal<N>::planes;  // tile planes
   __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * NPL * T::ES];
   constexpr int CW = ChainWaves<N>::value;
-  __shared__ double carry[2][CW][2][N];
+  __shared__ double carry[CARRY_BUFS][CW][2][N];
   const int64_t chain = c0 + blockIdx.x;
   if (chain >= c1) return;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
@@ -1594,7 +1621,7 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, AxiNodal<N>::waves)
     SeamOut so;
     if constexpr (SEAM) so.base = sp.buf + sp.colour[chain] * sp.n_node * 2;
     chain_emit<N, 2, false, CW, SEAM>(y, raw, v, lane, wave, rd, in_wave, carry, rowc, accumulate,
-                                          nullptr, so);
+                                      sp.round_sync, nullptr, so);
   }
 }
 
@@ -1607,7 +1634,7 @@ __global__ void __launch_bounds__(ChainWaves<N>::block)
   using T = Tile<N>;
   __shared__ __attribute__((aligned(16))) double lds[T::TILE_SLOTS * 2 * T::ES];
   constexpr int CW = ChainWaves<N>::value;
-  __shared__ double carry[2][CW][2][N];
+  __shared__ double carry[CARRY_BUFS][CW][2][N];
   const int64_t chain = c0 + blockIdx.x;
   if (chain >= c1) return;
   const int wave = threadIdx.x / WAVE;
@@ -1628,7 +1655,7 @@ __global__ void __launch_bounds__(ChainWaves<N>::block)
     SeamOut so;
     if constexpr (SEAM) so.base = sp.buf + sp.colour[chain] * sp.n_node * 2;
     chain_emit<N, 2, false, CW, SEAM>(y, raw, v, lane, wave, rd, in_wave, carry, rowc, accumulate,
-                                          nullptr, so);
+                                      sp.round_sync, nullptr, so);
   }
 }
 

@@ -22,6 +22,7 @@ void launch_chains(sem_ctx* c, int op_kind, bool nodal, const double* u, double*
   const int R = c->rounds;
   SeamPlan sp{c->d_ccol, c->d_seam_buf, c->n_node};
   sp.dot = dot_part;
+  sp.round_sync = c->round_sync ? 1 : 0;
   if constexpr (SEAM) {
     if (dot_part) {  // Poisson, one DOF per node, overwrite: u.y partials per chain
       const double* GP = nodal ? nullptr : c->d_GP[0];
