@@ -140,6 +140,10 @@ int sem_set_map_shared(sem_ctx* ctx, const uint32_t* d_e2n, const uint8_t* d_nod
  * written by several chains stored per writer colour and summed in colour
  * order by a second launch, bitwise equal to the colour launches; [5] is
  * then 1 and [8] the chain count.  (3 was a retired one-launch plan.)
+ * 5: the n = 17 MFMA kernel's seam form (default there; SEM_SEAM=0 keeps
+ * its colour launches): every element in one launch in breadth-first
+ * order, a node of several elements stored per element colour and summed
+ * by the seam launch.
  * [21] the axisymmetric Stokes geometry mode (as [19]; 0 when
  * dofs_per_node != 2).  [22] seam nodes of the seam plan.  [23] 1 when the
  * chains use the block layout (structured numberings: a chain is [6]
@@ -336,6 +340,19 @@ int sem_csr_pcg_solve(int64_t n, const int64_t* d_rowptr, const int32_t* d_colin
                       const double* d_val, const double* d_b, double* d_x,
                       const uint8_t* d_dirichlet, double rtol, int max_iter, int* iters,
                       double* final_relres, int device, void* stream);
+/* Direct solve of a general (non-symmetric) square CSR system A x = b by
+ * banded LU with partial pivoting: the condensed exterior system of
+ * _solve_boundary_dofs when it is not symmetric (the axisymmetric Stokes /
+ * Navier-Stokes block; scipy.sparse.linalg.spsolve in the reference,
+ * sem/discrete.py:502-511).  kl / ku: lower / upper bandwidth of A as
+ * ordered by the caller (reverse Cuthill-McKee, as the reference orders its
+ * nodes); kl < 1024.  Duplicate entries are summed.  Band storage
+ * n (2 kl + ku + 1) doubles, allocated on the stream.  *info = 0 on
+ * success, j + 1 when column j has an exactly zero pivot (A singular; x is
+ * then not written), as LAPACK gbsv.  Synchronises the stream. */
+int sem_band_lu_solve(int64_t n, int kl, int ku, const int64_t* d_rowptr, const int32_t* d_colind,
+                      const double* d_val, const double* d_b, double* d_x, int* info,
+                      void* stream);
 
 /* ------------------------------------------------------------------ */
 /* Domain decomposition across GPUs (one process per GPU)              */

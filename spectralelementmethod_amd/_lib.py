@@ -80,6 +80,8 @@ SIGNATURES = {
     "sem_schur_backsolve": (C.c_int, [_i64, C.c_int, C.c_int, _vp, _vp, _vp, _vp]),
     "sem_csr_pcg_solve": (C.c_int, [_i64, _vp, _vp, _vp, _vp, _vp, _vp, C.c_double, C.c_int,
                                     C.POINTER(C.c_int), C.POINTER(C.c_double), C.c_int, _vp]),
+    "sem_band_lu_solve": (C.c_int, [_i64, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp,
+                                    C.POINTER(C.c_int), _vp]),
     "sem_rccl_unique_id": (C.c_int, [_vp, C.c_int]),
     "sem_copy_async": (C.c_int, [_vp, _vp, _i64, _vp]),
     "sem_dd_create": (C.c_int, [C.POINTER(_vp), _vp, _vp, _i64, _vp, _i64, C.c_int,

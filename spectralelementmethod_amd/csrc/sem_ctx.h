@@ -194,10 +194,10 @@ inline bool nodal_mode(const sem_ctx* c) {
 // 0.129, p = 14 0.143 / 0.141, p = 15 0.142 / 0.112; profiles/r02/final),
 // so AUTO no longer picks it (SEM_KERNEL_MFMA still does).
 #ifndef SEM_MFMA_MIN_N
-#define SEM_MFMA_MIN_N 17
+#define SEM_MFMA_MIN_N 18
 #endif
 inline bool want_mfma(const sem_ctx* c) {
-  if (c->dpn != 1 || c->n > 16) return false;
+  if (c->dpn != 1 || c->n > 17) return false;
   if (c->kernel == SEM_KERNEL_MFMA) return true;
   if (c->kernel == SEM_KERNEL_COLUMN) return false;
   return c->n >= SEM_MFMA_MIN_N && c->geom_mode != SEM_GEOM_NODAL;

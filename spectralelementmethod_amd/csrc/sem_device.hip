@@ -698,8 +698,16 @@ static bool build_map16(const Plan& P, int64_t n_elem, int n, int epw, int64_t n
 // shareable nodes are written with atomics.  Group = slot = one element, so
 // the packed map and factors are compact per element ([slot][r][j]).
 // ---------------------------------------------------------------------------
+// seam = 1 (n = 17 kernel): one launch over all elements in breadth-first
+// order instead of one per colour; a node of several elements is stored by
+// each into the slot of its element's colour and summed by k_seam_sum (the
+// column kernel's seam plan with one element per chain).
+// seams for the n = 17 MFMA kernel under AUTO (SEM_SEAM=0 / 1 forces)
+#ifndef MFMA_SEAM_AUTO
+#define MFMA_SEAM_AUTO 1
+#endif
 int build_plan_elem(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node, int n,
-                    const std::vector<uint8_t>& node_state, Plan& P) {
+                    const std::vector<uint8_t>& node_state, Plan& P, int seam = 0) {
   const int nn = n * n;
   auto is_bnd = [n](int r, int jj) { return r == 0 || r == n - 1 || jj == 0 || jj == n - 1; };
   std::vector<uint32_t> cnt(n_node, 0);
@@ -789,12 +797,22 @@ int build_plan_elem(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_
     colour[e] = c;
   }
   std::vector<uint8_t>().swap(cmask);
-  std::vector<int64_t> count(MAX_COLOURS + 2, 0);
-  for (int64_t e = 0; e < n_elem; ++e) count[colour[e] + 1]++;
-  P.colour_start.assign(MAX_COLOURS + 2, 0);
-  for (int q = 0; q <= MAX_COLOURS; ++q) P.colour_start[q + 1] = P.colour_start[q] + count[q + 1];
   std::vector<int64_t> order(n_elem);
-  {
+  int maxc = 0;
+  for (int64_t e = 0; e < n_elem; ++e) maxc = std::max(maxc, colour[e]);
+  P.seam = seam == 1 && conforming && maxc < MAX_COLOURS;
+  if (P.seam) {
+    order = bfs;
+    P.colour_start = {0, n_elem};
+    P.seam_ns = maxc + 1;
+    P.chain_colour.resize(n_elem);
+    for (int64_t q = 0; q < n_elem; ++q) P.chain_colour[q] = (uint8_t)colour[order[q]];
+  } else {
+    std::vector<int64_t> count(MAX_COLOURS + 2, 0);
+    for (int64_t e = 0; e < n_elem; ++e) count[colour[e] + 1]++;
+    P.colour_start.assign(MAX_COLOURS + 2, 0);
+    for (int q = 0; q <= MAX_COLOURS; ++q)
+      P.colour_start[q + 1] = P.colour_start[q] + count[q + 1];
     std::vector<int64_t> fill(P.colour_start.begin(), P.colour_start.end() - 1);
     for (int64_t e = 0; e < n_elem; ++e) order[fill[colour[e]]++] = e;
   }
@@ -816,7 +834,9 @@ int build_plan_elem(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_
       for (int jj = 0; jj < n; ++jj) {
         const uint32_t gid = e2n[e * nn + r * n + jj];
         uint32_t code;
-        if (atomic && shared_local(r, jj)) {
+        if (P.seam && cnt[gid] >= 2) {
+          code = W_ATOMIC;  // seam slot of this element's colour (k_seam_sum)
+        } else if (atomic && shared_local(r, jj)) {
           code = W_ATOMIC;
           if (!written[gid]) P.zero.push_back(gid);
         } else {
@@ -829,6 +849,19 @@ int build_plan_elem(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_
   for (int64_t i = 0; i < n_node; ++i)
     if (cnt[i] == 0 && (node_state.empty() || !node_state[i])) P.zero.push_back((uint32_t)i);
   std::sort(P.zero.begin(), P.zero.end());
+  P.n_rmw = 0;
+  for (const uint32_t e : P.mapP) P.n_rmw += ((e >> CODE_SHIFT) & 3u) == W_RMW ? 1 : 0;
+  if (P.seam) {
+    std::vector<uint16_t> smask(n_node, 0);
+    for (int64_t e = 0; e < n_elem; ++e)
+      for (int t = 0; t < nn; ++t) smask[e2n[e * nn + t]] |= (uint16_t)(1u << colour[e]);
+    for (int64_t i = 0; i < n_node; ++i)
+      if (cnt[i] >= 2) {
+        P.seam_gid.push_back((uint32_t)i);
+        const bool prior = !node_state.empty() && (node_state[i] & SEM_NODE_PRIOR);
+        P.seam_mask.push_back((uint16_t)(smask[i] | (prior ? 0x100u : 0u)));
+      }
+  }
   return SEM_OK;
 }
 
@@ -1108,11 +1141,14 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
   // seam plan: one launch + seam sums; SEM_SEAM=1 / 0 forces / forbids it;
   // default AUTO (seam_auto, per dofs per node)
   int seam = 0;
-  if (!mfma) {
+  {
     const char* e = std::getenv("SEM_SEAM");
     seam = e ? (std::atoi(e) == 1 ? 1 : 0) : 2;
   }
-  int rc = mfma ? build_plan_elem(h, c->n_elem, c->n_node, n, state, P)
+  // the n = 17 MFMA kernel takes seams by default (MFMA_SEAM_AUTO); the
+  // n <= 16 MFMA kernel has no seam form
+  const int eseam = (mfma && n == 17) ? (seam == 2 ? MFMA_SEAM_AUTO : seam) : 0;
+  int rc = mfma ? build_plan_elem(h, c->n_elem, c->n_node, n, state, P, eseam)
                 : build_plan(h, c->n_elem, c->n_node, n, rounds, state, P, seam, c->dpn, brounds);
   if (!rc && P.seam_failed) {
     P = Plan();
@@ -1191,7 +1227,7 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
   c->seam = P.seam;
   // sem_apply_dot's fused form: every node's final value is one STORE (or a
   // seam sum): no read-modify-write, nothing zeroed separately
-  c->seam_dot = P.seam && P.n_rmw == 0 && P.zero.empty() && state.empty();
+  c->seam_dot = !mfma && P.seam && P.n_rmw == 0 && P.zero.empty() && state.empty();
   c->seam_ns = P.seam_ns;
   c->n_seam = (int64_t)P.seam_gid.size();
   (void)hipFree(c->d_ccol);
@@ -1254,8 +1290,9 @@ int sem_plan_info(sem_ctx* c, int64_t* info, int n_info) {
   const bool eff_nodal = c->xg_valid ? true : (c->d_GP[0] ? false : nodal_mode(c));
   vals[NV - 6] = eff_nodal ? SEM_GEOM_NODAL : SEM_GEOM_STORED;
   // plan: 0 chains (colour launches), 1 element-coloured chains, 2 elements
-  // (MFMA kernel), 4 chains + seam sums (3 was the retired one-launch plan)
-  vals[NV - 5] = c->mfma ? 2 : (c->ecol ? 1 : (c->seam ? 4 : 0));
+  // (MFMA kernel), 4 chains + seam sums (3 was the retired one-launch plan),
+  // 5 elements + seam sums (n = 17 MFMA kernel)
+  vals[NV - 5] = c->mfma ? (c->seam ? 5 : 2) : (c->ecol ? 1 : (c->seam ? 4 : 0));
   // the same for the axisymmetric Stokes block (dofs_per_node = 2)
   const bool axi_nodal =
       c->xg_axi ? true : (c->d_GP[1] ? false : nodal_mode_op(c, SEM_OP_AXISYM_STOKES));
@@ -1295,8 +1332,8 @@ int sem_set_kernel(sem_ctx* c, int kernel) {
   if (!c) return fail(SEM_E_INVALID, "null ctx");
   if (kernel != SEM_KERNEL_COLUMN && kernel != SEM_KERNEL_MFMA && kernel != SEM_KERNEL_AUTO)
     return fail(SEM_E_INVALID, "unknown kernel " + std::to_string(kernel));
-  if (kernel == SEM_KERNEL_MFMA && (c->dpn != 1 || c->n > 16))
-    return fail(SEM_E_NOTIMPL, "the MFMA kernel needs dofs_per_node == 1 and p <= 15");
+  if (kernel == SEM_KERNEL_MFMA && (c->dpn != 1 || c->n > 17))
+    return fail(SEM_E_NOTIMPL, "the MFMA kernel needs dofs_per_node == 1 and p <= 16");
   c->kernel = kernel;
   return SEM_OK;
 }

@@ -1847,6 +1847,234 @@ __global__ void __launch_bounds__(BLOCK, SEM_MFMA_MIN_WAVES)
 }
 
 // ---------------------------------------------------------------------------
+// Poisson stiffness action on the fp64 matrix cores for n = 17 (p = 16),
+// where one element no longer fits a 16 x 16 tile.
+//
+// The contraction along one index is a GEMM whose N dimension is the other
+// index: d0[:, j] = D U[:, j] for every line j of every element.  A pair of
+// wavefronts takes EW = 3 elements and flattens their lines, f = 17 e + l,
+// into T = 4 N-tiles of 16 (51 of 64 used, the column kernel's lane use),
+// two tiles per wavefront.  The output and contraction index (17) is folded
+// by the centro-antisymmetry of D (D[16-m][16-r] = -D[m][r]): with
+// ua_a = x_a - x_{16-a}, us_a = x_a + x_{16-a} (a < 8),
+//   s'_m = sum_a (D[m][a] - D[m][16-a]) / 2 ua_a      (m < 8),   out[8] = sum_a D[8][a] ua_a
+//   t'_m = sum_a (D[m][a] + D[m][16-a]) / 2 us_a + D[m][8] x_8
+//   out[m] = s'_m + t'_m,  out[16-m] = s'_m - t'_m
+// i.e. one accumulator over K = ua (2 k-steps: s' rows 0..7 and out[8] in
+// row 8) and one over K = us plus x_8 (3 k-steps: t' rows 0..7): 5 MFMAs per
+// tile and contraction instead of 2 x 5 for the unfolded 17 x 17.  Lane
+// (h = lane >> 4, c = lane & 15) of tile t holds line f = 16 t + c at the
+// entries a = h, 4 + h, 16 - h, 12 - h (+ 8 for h = 0): exactly the B
+// operands it supplies, and -- C row = h + 4 i -- exactly the outputs it
+// receives, so a contraction maps a lane's five entries to the same five
+// entries.  The same code contracts along the other index when the lines
+// are the element's rows ("Y" layout) instead of its columns ("X").
+//
+//   d0 = D U (X),  d1 = U D^T (Y),  w0/w1 pointwise (X),
+//   y = D^T w0 (X) + w1 D (Y)
+//
+// X <-> Y go through the pair's [3][17][17] LDS plane, updated in place (in
+// each phase a lane writes back exactly the entries it read), with a
+// workgroup barrier between phases.  Elements of one launch share no node
+// (element colouring, build_plan_elem); stored factors per element slot as
+// for k_poisson_mfma.  The scatter reads its read-modify-write operands for
+// all of a lane's entries at once, before the last contraction (predicated
+// buffer loads as in rmw_prefetch); a branch around a load and its store per
+// entry serialised the round trips (first form: 68 us per colour launch at
+// p = 16, 198^2, against 0.16 ms per action for the column kernel).
+// ---------------------------------------------------------------------------
+constexpr int MF17_N = 17;
+constexpr int MF17_EW = 3;                          // elements per wavefront pair
+constexpr int MF17_TW = 2;                          // N-tiles per wavefront (4 per pair)
+constexpr int MF17_PAIRS = BLOCK / (2 * WAVE);      // wavefront pairs per workgroup
+constexpr int MF17_PLANE = MF17_EW * 17 * 17 + 2 * WAVE;  // doubles per pair plane (+ junk)
+
+// A operands of one centro-antisymmetric 17 x 17 matrix M (lane row rho =
+// lane & 15, k = lane >> 4): s-steps, t-steps, the x_8 step
+struct MF17A {
+  double s0, s1, t0, t1, m;
+};
+
+__device__ __forceinline__ MF17A mf17_operands(const double* __restrict__ gD, bool tr, int lane) {
+  const int rho = lane & 15, q = lane >> 4;
+  auto M = [&](int i, int j) { return tr ? gD[j * MF17_N + i] : gD[i * MF17_N + j]; };
+  MF17A A;
+  const int rr = rho < 8 ? rho : 0;
+  const double s0 = 0.5 * (M(rr, q) - M(rr, 16 - q)), s1 = 0.5 * (M(rr, 4 + q) - M(rr, 12 - q));
+  const double t0 = 0.5 * (M(rr, q) + M(rr, 16 - q)), t1 = 0.5 * (M(rr, 4 + q) + M(rr, 12 - q));
+  const double m8a = M(8, q), m8b = M(8, 4 + q), mm = M(rr, 8);
+  A.s0 = rho < 8 ? s0 : (rho == 8 ? m8a : 0.0);
+  A.s1 = rho < 8 ? s1 : (rho == 8 ? m8b : 0.0);
+  A.t0 = rho < 8 ? t0 : 0.0;
+  A.t1 = rho < 8 ? t1 : 0.0;
+  A.m = (rho < 8 && q == 0) ? mm : 0.0;
+  return A;
+}
+
+// v[0..4] = line entries a = h, 4 + h, 16 - h, 12 - h, 8 (v[4] zero unless
+// h = 0) -> the same entries of M times the line
+__device__ __forceinline__ void mf17_contract(const MF17A& A, double (&v)[5]) {
+  const dbl4 z = {0.0, 0.0, 0.0, 0.0};
+  const double ua0 = v[0] - v[2], ua1 = v[1] - v[3];
+  const double us0 = v[0] + v[2], us1 = v[1] + v[3];
+  dbl4 as = mfma_f64(A.s0, ua0, z);
+  dbl4 at = mfma_f64(A.t0, us0, z);
+  as = mfma_f64(A.s1, ua1, as);
+  at = mfma_f64(A.t1, us1, at);
+  at = mfma_f64(A.m, v[4], at);
+  v[0] = as[0] + at[0];
+  v[2] = as[0] - at[0];
+  v[1] = as[1] + at[1];
+  v[3] = as[1] - at[1];
+  v[4] = as[2];  // row 8 + h: out[8] for h = 0, zero rows otherwise
+}
+
+#ifndef SEM_MF17_WAVES
+#define SEM_MF17_WAVES 3
+#endif
+// SEAM: code W_ATOMIC stores into the seam slot of the element's colour
+// (sp.colour indexed by element slot), summed by k_seam_sum
+template <int N, bool SEAM>
+__global__ void __launch_bounds__(BLOCK, SEM_MF17_WAVES)
+    k_poisson_mfma17(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
+                     const double* __restrict__ u, double* __restrict__ y,
+                     const double* __restrict__ gD, int64_t s0, int64_t s1, int accumulate,
+                     SeamPlan sp) {
+  static_assert(N == MF17_N, "folded multi-element form of n = 17");
+  constexpr int NN = N * N, T = MF17_TW;
+  __shared__ double lds[MF17_PAIRS][MF17_PLANE];
+  const int lane = threadIdx.x % WAVE;
+  const int wave = threadIdx.x / WAVE;
+  const int pair = wave >> 1, half = wave & 1;
+  const int64_t slot0 = s0 + ((int64_t)blockIdx.x * MF17_PAIRS + pair) * MF17_EW;
+  // a pair past the end still runs (workgroup barriers below) on slot s0's
+  // data and writes nothing
+  const int64_t sb = slot0 < s1 ? slot0 : s0;
+  double* P = lds[pair];
+  const int h = lane >> 4, c = lane & 15;
+  const bool hm = h == 0;  // owner of the middle entry
+  const int R[5] = {h, 4 + h, 16 - h, 12 - h, 8};
+  const MF17A AD = mf17_operands(gD, false, lane);
+  constexpr int JUNK = MF17_EW * NN;  // per-lane junk slots for entries off the plane
+  // tile 2 half + t: line f = 16 (2 half + t) + c of element e = f / 17.
+  // xb / yb: the line's base in the plane for the X / Y layouts (entry k at
+  // xb + R[k] * 17 / yb + R[k]); xb is also the line's offset in the
+  // element-slot map relative to slot sb
+  int xb[T], yb[T], el[T];
+  bool ok[T];  // the line's element slot exists
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int f = 16 * (2 * half + t) + c;
+    const int e = f / N;
+    const int l = f - e * N;
+    ok[t] = e < MF17_EW && slot0 + e < s1;
+    el[t] = ok[t] ? e : 0;  // element 0 of slot sb stands in for a missing slot
+    xb[t] = el[t] * NN + l;
+    yb[t] = el[t] * NN + l * N;
+  }
+  auto live = [&](int t, int k) { return ok[t] && (k < 4 || hm); };
+  auto xo = [&](int t, int k) { return live(t, k) ? xb[t] + R[k] * N : JUNK + half * WAVE + lane; };
+  auto yo = [&](int t, int k) { return live(t, k) ? yb[t] + R[k] : JUNK + half * WAVE + lane; };
+  auto go = [&](int t, int k) { return xb[t] + (k < 4 || hm ? R[k] : 0) * N; };
+  const uint32_t* mp = mapP + sb * NN;
+
+  // phase A: gather (X), d0 = D U, U into the plane
+  uint32_t raw[T][5];
+  double d0[T][5];
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const uint32_t e = mp[go(t, k)];
+      raw[t][k] = live(t, k) ? e : (W_SKIP << CODE_SHIFT);
+      d0[t][k] = u[e & GID_MASK];
+      d0[t][k] = live(t, k) ? d0[t][k] : 0.0;
+    }
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) P[xo(t, k)] = d0[t][k];
+    mf17_contract(AD, d0[t]);
+  }
+  __syncthreads();
+  // phase B: d1 = U D^T along the rows (Y), in place
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    double v[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) v[k] = live(t, k) ? P[yo(t, k)] : 0.0;
+    mf17_contract(AD, v);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) P[yo(t, k)] = v[k];
+  }
+  __syncthreads();
+  // phase C: factors (X), w0 = G00 d0 + G01 d1 -> y0 = D^T w0, w1 = G01 d0 + G11 d1 in place
+  const MF17A AT = mf17_operands(gD, true, lane);
+  const double* gq = GP + sb * (3 * NN);
+  double y0[T][5];
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    double w1[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const double* gp = gq + go(t, k) + el[t] * (2 * NN);  // slot stride 3 NN
+      const double g0 = gp[0], g1 = gp[NN], g2 = gp[2 * NN];
+      const double d1 = P[xo(t, k)];
+      y0[t][k] = live(t, k) ? fma(g0, d0[t][k], g1 * d1) : 0.0;
+      w1[k] = live(t, k) ? fma(g1, d0[t][k], g2 * d1) : 0.0;
+    }
+    mf17_contract(AT, y0[t]);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) P[xo(t, k)] = w1[k];
+  }
+  __syncthreads();
+  // read-modify-write operands of the scatter, all in flight together
+  const __amdgpu_buffer_rsrc_t ry = y_rsrc(y);
+  double prev[T][5];
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const uint32_t a = (raw[t][k] >> CODE_SHIFT) & 3u;
+      const bool need = a == W_RMW || (a == W_STORE && accumulate);
+      const uint32_t off = need ? (raw[t][k] & GID_MASK) * 8u : 0x80000000u;
+      prev[t][k] =
+          __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(ry, off, 0, CPOL_NT));
+    }
+  // phase D: y1 = w1 D along the rows (Y), in place
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    double v[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) v[k] = live(t, k) ? P[yo(t, k)] : 0.0;
+    mf17_contract(AT, v);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) P[yo(t, k)] = v[k];
+  }
+  __syncthreads();
+  // phase E: y = y0 + y1 (X), scatter
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    double* sbase = nullptr;
+    if constexpr (SEAM) sbase = sp.buf + (int64_t)sp.colour[sb + el[t]] * sp.n_node;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const uint32_t a = (raw[t][k] >> CODE_SHIFT) & 3u;
+      const uint32_t gid = raw[t][k] & GID_MASK;
+      const double v = y0[t][k] + P[xo(t, k)];
+      if (a == W_STORE || a == W_RMW) {
+        y[gid] = prev[t][k] + v;
+      } else if (a == W_ATOMIC) {
+        if constexpr (SEAM)
+          sbase[gid] = v;
+        else
+          atomic_add_f64(y + gid, v);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Geometry: nodes -> x_phys -> J -> det/inv -> W -> operator factors.
 // Thread per local node, EPB elements per block, LDS staging (setup path).
 // ---------------------------------------------------------------------------

@@ -87,6 +87,21 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
   WVec<N> w;
   std::memcpy(w.v, c->hw, sizeof(w.v));
   const bool nodal = use_nodal(c, op_kind);
+  if constexpr (N == MF17_N) {
+    if (c->seam && c->mfma) {  // n = 17 MFMA kernel, one launch + the seam sums
+      if (op_kind != SEM_OP_POISSON) return sem::fail(SEM_E_NOTIMPL, "MFMA kernel: Poisson only");
+      if (nodal) return sem::fail(SEM_E_NOTIMPL, "the n = 17 MFMA kernel takes stored factors");
+      const int64_t c0 = c->colour_start.front(), c1 = c->colour_start.back();
+      constexpr int per_block = MF17_PAIRS * MF17_EW;
+      const dim3 g((unsigned)((c1 - c0 + per_block - 1) / per_block));
+      const SeamPlan sp{c->d_ccol, c->d_seam_buf, c->n_node};
+      hipLaunchKernelGGL((k_poisson_mfma17<N, true>), g, dim3(BLOCK), 0, st, c->d_mapP,
+                         c->d_GP[0], u, y, c->d_D, c0, c1, acc, sp);
+      const int rc = launch_seam_sum(c, y, acc, st);
+      if (rc || !dot_out) return rc;
+      return sem::fail(SEM_E_STATE, "fused dot on the MFMA seam plan");
+    }
+  }
   if (c->seam) {  // one launch + the seam sums (SeamPlan)
     const int64_t c0 = c->colour_start.front(), c1 = c->colour_start.back();
     // dot_out: u.y fused into the two launches (partials, then a fixed-order sum)
@@ -113,8 +128,14 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
         else
           hipLaunchKernelGGL((k_poisson_mfma<N, false>), g, dim3(BLOCK), 0, st, c->d_mapP,
                              c->d_GP[0], nullptr, u, y, c->d_D, w, c0, c1, acc);
+      } else if constexpr (N == MF17_N) {
+        if (nodal) return sem::fail(SEM_E_NOTIMPL, "the n = 17 MFMA kernel takes stored factors");
+        constexpr int per_block = MF17_PAIRS * MF17_EW;
+        const dim3 g((unsigned)((c1 - c0 + per_block - 1) / per_block));
+        hipLaunchKernelGGL((k_poisson_mfma17<N, false>), g, dim3(BLOCK), 0, st, c->d_mapP,
+                           c->d_GP[0], u, y, c->d_D, c0, c1, acc, SeamPlan{});
       } else {
-        return sem::fail(SEM_E_NOTIMPL, "the MFMA kernel needs n <= 16");
+        return sem::fail(SEM_E_NOTIMPL, "the MFMA kernel needs n <= 17");
       }
     } else {
       launch_chains<N, false>(c, op_kind, nodal, u, y, acc, lin, c0, c1, D, w, st);

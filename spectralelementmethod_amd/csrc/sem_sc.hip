@@ -160,6 +160,120 @@ __global__ void k_sc_backsolve(int64_t n_elem, int ni, int ne, const double* __r
   }
 }
 
+// ---------------------------------------------------------------------------
+// Banded LU with partial pivoting for the condensed exterior system when it
+// is not symmetric (the axisymmetric Stokes / Navier-Stokes block that
+// examples/squirmer-axisymmetric.py:299-387 condenses; the reference solves
+// it with scipy.sparse.linalg.spsolve, sem/discrete.py:502-511).  The caller
+// orders the unknowns by reverse Cuthill-McKee (as the reference orders its
+// nodes, sem/discrete.py:169-178, 400), so the matrix is banded with lower /
+// upper bandwidths kl / ku; row interchanges widen U to KU = kl + ku.
+// Column-major band storage: entry (i, k) at AB[k * W + i - k + KU],
+// W = KU + kl + 1 (LAPACK gbtrf's layout, without its separate kl rows).
+// ---------------------------------------------------------------------------
+constexpr int BLU = 1024;  // threads of the one factorising workgroup
+
+__global__ void k_band_fill(int64_t n, int KU, int W, const int64_t* __restrict__ rowptr,
+                            const int32_t* __restrict__ colind, const double* __restrict__ val,
+                            double* __restrict__ AB) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    for (int64_t t = rowptr[i]; t < rowptr[i + 1]; ++t) {
+      const int64_t k = colind[t];
+      AB[k * W + (i - k + KU)] += val[t];  // duplicates summed (COO semantics)
+    }
+}
+
+// One workgroup: the elimination is a chain of n dependent steps; each step
+// (pivot search over kl + 1 entries, row swap over KU + 1 columns, rank-1
+// update of a kl x KU block) is spread over the workgroup.  b is eliminated
+// alongside; then the column-oriented back substitution (U's column j above
+// the diagonal is contiguous in this layout).  info = j + 1 for an exactly
+// zero pivot in column j (LAPACK's convention), 0 otherwise.
+__global__ void __launch_bounds__(BLU)
+    k_band_lu_solve(int64_t n, int kl, int KU, int W, double* __restrict__ AB,
+                    double* __restrict__ b, double* __restrict__ x, int* __restrict__ info) {
+  __shared__ double s_val[BLU];
+  __shared__ int s_idx[BLU];
+  __shared__ double s_l[BLU];  // multipliers of the step (kl < BLU)
+  const int tid = threadIdx.x;
+  for (int64_t j = 0; j < n; ++j) {
+    const int64_t ilast = min<int64_t>(n - 1, j + kl);
+    const int nr = (int)(ilast - j);  // rows below the diagonal
+    double best = -1.0;
+    int bi = 0;
+    for (int r = tid; r <= nr; r += BLU) {
+      const double a = fabs(AB[j * W + r + KU]);
+      if (a > best) {
+        best = a;
+        bi = r;
+      }
+    }
+    s_val[tid] = best;
+    s_idx[tid] = bi;
+    __syncthreads();
+    for (int o = BLU / 2; o > 0; o >>= 1) {
+      if (tid < o) {
+        const double v2 = s_val[tid + o];
+        const int i2 = s_idx[tid + o];
+        if (v2 > s_val[tid] || (v2 == s_val[tid] && i2 < s_idx[tid])) {
+          s_val[tid] = v2;
+          s_idx[tid] = i2;
+        }
+      }
+      __syncthreads();
+    }
+    const double pv = s_val[0];
+    const int p = s_idx[0];
+    if (!(pv > 0.0)) {  // exactly zero (or NaN) pivot column
+      if (tid == 0) *info = (int)(j + 1);
+      return;           // uniform: every thread read the same s_val[0]
+    }
+    const int64_t klast = min<int64_t>(n - 1, j + KU);
+    if (p != 0) {
+      for (int64_t k = j + tid; k <= klast; k += BLU) {
+        double* a = AB + k * W + (j - k + KU);
+        const double t = a[0];
+        a[0] = a[p];
+        a[p] = t;
+      }
+      if (tid == 0) {
+        const double t = b[j];
+        b[j] = b[j + p];
+        b[j + p] = t;
+      }
+    }
+    __syncthreads();
+    const double inv = 1.0 / AB[j * W + KU];
+    const double bj = b[j];
+    for (int r = 1 + tid; r <= nr; r += BLU) {
+      const double l = AB[j * W + KU + r] * inv;
+      s_l[r] = l;
+      b[j + r] = fma(-l, bj, b[j + r]);
+    }
+    __syncthreads();
+    // A(j + r, k) -= l_r A(j, k) for r in [1, nr], k in (j, klast]
+    const int nc = (int)(klast - j);
+    const int64_t tot = (int64_t)nr * nc;
+    for (int64_t t = tid; t < tot; t += BLU) {
+      const int c = 1 + (int)(t / nr), r = 1 + (int)(t % nr);
+      double* col = AB + (j + c) * W + (KU - c);  // (i, j + c) at col[i - j]
+      col[r] = fma(-s_l[r], col[0], col[r]);
+    }
+    __syncthreads();
+  }
+  // back substitution, column-oriented: x_j = b_j / U_jj, then b_i -= U_ij x_j
+  for (int64_t j = n - 1; j >= 0; --j) {
+    const double xj = b[j] / AB[j * W + KU];
+    __syncthreads();  // every thread read b[j] before it can change again
+    if (tid == 0) x[j] = xj;
+    const int64_t i0 = max<int64_t>(0, j - KU);
+    for (int64_t i = i0 + tid; i < j; i += BLU) b[i] = fma(-AB[j * W + (i - j + KU)], xj, b[i]);
+    __syncthreads();
+  }
+  if (tid == 0) *info = 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -187,6 +301,41 @@ int sem_schur_batched(int64_t n_elem, int nl, int ne, const double* d_mat, const
   if (n_singular) *n_singular = (int64_t)bad;
   if (bad)
     return fail(SEM_E_INVALID, "singular interior block in " + std::to_string(bad) + " elements");
+  return SEM_OK;
+}
+
+int sem_band_lu_solve(int64_t n, int kl, int ku, const int64_t* d_rowptr, const int32_t* d_colind,
+                      const double* d_val, const double* d_b, double* d_x, int* info,
+                      void* stream) {
+  if (n < 0 || kl < 0 || ku < 0 || kl >= BLU) return fail(SEM_E_INVALID, "sem_band_lu_solve: bad sizes");
+  if (n && (!d_rowptr || !d_colind || !d_val || !d_b || !d_x || !info))
+    return fail(SEM_E_INVALID, "sem_band_lu_solve: null argument");
+  if (!n) {
+    *info = 0;
+    return SEM_OK;
+  }
+  const int KU = kl + ku;
+  const int W = KU + kl + 1;
+  hipStream_t st = S(stream);
+  double *AB = nullptr, *b = nullptr;
+  int* d_info = nullptr;
+  HIP_TRY(hipMallocAsync((void**)&AB, (size_t)n * W * sizeof(double), st));
+  HIP_TRY(hipMallocAsync((void**)&b, (size_t)n * sizeof(double), st));
+  HIP_TRY(hipMallocAsync((void**)&d_info, sizeof(int), st));
+  HIP_TRY(hipMemsetAsync(AB, 0, (size_t)n * W * sizeof(double), st));
+  HIP_TRY(hipMemcpyAsync(b, d_b, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, st));
+  const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_band_fill, dim3(grid), dim3(256), 0, st, n, KU, W, d_rowptr, d_colind, d_val,
+                     AB);
+  hipLaunchKernelGGL(k_band_lu_solve, dim3(1), dim3(BLU), 0, st, n, kl, KU, W, AB, b, d_x, d_info);
+  HIP_TRY(hipGetLastError());
+  int h_info = 0;
+  HIP_TRY(hipMemcpyAsync(&h_info, d_info, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipFreeAsync(AB, st));
+  HIP_TRY(hipFreeAsync(b, st));
+  HIP_TRY(hipFreeAsync(d_info, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  *info = h_info;
   return SEM_OK;
 }
 

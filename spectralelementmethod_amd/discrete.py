@@ -462,6 +462,51 @@ class DOFManager(object):
         raise NotImplementedError("point location (sem/discrete.py:263-280) is out of scope")
 
 
+def band_lu_solve(A, b, device):
+    """x = A^-1 b for a square sparse matrix on the device: reverse
+    Cuthill-McKee order (host, scipy.sparse.csgraph, as the reference orders
+    its nodes: sem/discrete.py:169-178), then banded LU with partial pivoting
+    (sem_band_lu_solve).  Stands in for the reference's
+    scipy.sparse.linalg.spsolve (sem/discrete.py:511): a singular matrix
+    gives a MatrixRankWarning and a NaN solution, as there."""
+    import ctypes as C
+    import warnings
+    import torch
+    from scipy.sparse.csgraph import reverse_cuthill_mckee
+    from . import _lib
+    A = sparse.csr_matrix(A)
+    n = A.shape[0]
+    if n == 0:
+        return np.zeros(0)
+    pat = (abs(A) + abs(A.T)).tocsr()
+    perm = np.asarray(reverse_cuthill_mckee(pat, symmetric_mode=True), dtype=np.int64)
+    Ap = A[perm][:, perm].tocoo()
+    kl = int(max(0, (Ap.row - Ap.col).max(initial=0)))
+    ku = int(max(0, (Ap.col - Ap.row).max(initial=0)))
+    if kl >= 1024:
+        raise NotImplementedError("band_lu_solve: lower bandwidth %d after RCM (limit 1023)" % kl)
+    Ap = Ap.tocsr()
+    lib = _lib.load()
+    rp = torch.from_numpy(Ap.indptr.astype(np.int64)).to(device)
+    ci = torch.from_numpy(Ap.indices.astype(np.int32)).to(device)
+    va = torch.from_numpy(Ap.data.astype(np.float64)).to(device)
+    bp = torch.from_numpy(np.ascontiguousarray(np.asarray(b, dtype=np.float64)[perm])).to(device)
+    xp = torch.empty(n, dtype=torch.float64, device=device)
+    info = C.c_int(0)
+    with torch.cuda.device(device):
+        _lib.check(lib.sem_band_lu_solve(n, kl, ku, _lib.tptr(rp), _lib.tptr(ci), _lib.tptr(va),
+                                         _lib.tptr(bp), _lib.tptr(xp), C.byref(info),
+                                         _lib.stream_ptr()))
+    x = np.empty(n)
+    if info.value:
+        from scipy.sparse.linalg import MatrixRankWarning
+        warnings.warn("Matrix is exactly singular", MatrixRankWarning, stacklevel=3)
+        x.fill(np.nan)
+        return x
+    x[perm] = xp.cpu().numpy()
+    return x
+
+
 class DOFManagerSC(DOFManager):
     """DOFs ordered for static condensation: element-exterior nodes first
     (sem/discrete.py:283-528)."""
@@ -575,8 +620,10 @@ class DOFManagerSC(DOFManager):
     def _solve_boundary_dofs(self, global_sc_system, dof_vec, on_ebc, rtol=1e-13):
         """Solve the condensed exterior system with the essential BCs
         (sem/discrete.py:502-510).  Symmetric systems (Poisson): Jacobi-PCG on
-        the device over the assembled CSR matrix; otherwise the reference's
-        own sparse direct solve."""
+        the device over the assembled CSR matrix; otherwise (the axisymmetric
+        Stokes / Navier-Stokes block) a direct solve like the reference's
+        spsolve: banded LU with partial pivoting on the device, the unknowns
+        ordered by reverse Cuthill-McKee (sem_band_lu_solve)."""
         import torch
         from . import _lib
         sc_mat, sc_rhs = global_sc_system
@@ -604,10 +651,9 @@ class DOFManagerSC(DOFManager):
                                                  dev.index, _lib.stream_ptr()))
             ext_dofs[is_unk] = x.cpu().numpy()[is_unk]
             return its.value, rel.value
-        from scipy.sparse import linalg as spla
         A1 = A[is_unk]
         rhs1 = sc_rhs[is_unk] - A1[:, ~is_unk].dot(ext_dofs[~is_unk])
-        ext_dofs[is_unk] = spla.spsolve(A1[:, is_unk].tocsc(), rhs1)
+        ext_dofs[is_unk] = band_lu_solve(A1[:, is_unk], rhs1, self.operator().device)
         return None, None
 
     def _solve_interior_dofs(self, local_systems, dof_vec):

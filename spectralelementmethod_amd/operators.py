@@ -202,10 +202,10 @@ class SEMOperator(object):
                     map_entry_bytes=v[18],
                     geometry="nodal" if v[19] == _lib.GEOM_NODAL else "stored",
                     plan={0: "chains", 1: "element-coloured", 2: "element",
-                          4: "chains-seams"}[v[20]],
+                          4: "chains-seams", 5: "element-seams"}[v[20]],
                     geometry_axisym=(None if self.dpn != 2 else
                                      "nodal" if v[21] == _lib.GEOM_NODAL else "stored"),
-                    seam_nodes=v[22] if v[20] == 4 else 0, blocks=bool(v[23]),
+                    seam_nodes=v[22] if v[20] in (4, 5) else 0, blocks=bool(v[23]),
                     row_carries=v[24])
 
     # ------------------------------------------------------------------

@@ -347,11 +347,13 @@ def test_shared_output_split(sem, gll, geometry):
 # fp64 matrix-core kernel (k_poisson_mfma, sem_set_kernel SEM_KERNEL_MFMA)
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("geometry", GEOMETRY)
-@pytest.mark.parametrize("name", [c for c in ACTION_CASES if not c.startswith("p16")])
+@pytest.mark.parametrize("name", ACTION_CASES)
 def test_poisson_action_golden_mfma(sem, poisson_action, gll, name, geometry):
     import sem_oracle
     fx = poisson_action
     p = int(fx[name + "_p"])
+    if p == 16 and geometry == "nodal":
+        pytest.skip("the n = 17 MFMA kernel takes stored factors (nodal: test_mfma_auto_selection_and_limits)")
     op = sem.SEMOperator(p, fx[name + "_e2n"], fx[name + "_nodes"], kernel="mfma",
                          geometry=geometry)
     assert op.plan_info()["kernel"] == "mfma"
@@ -364,12 +366,15 @@ def test_poisson_action_golden_mfma(sem, poisson_action, gll, name, geometry):
 
 
 @pytest.mark.parametrize("geometry", GEOMETRY)
-@pytest.mark.parametrize("p", list(range(1, 16)))
+@pytest.mark.parametrize("p", list(range(1, 17)))
 def test_poisson_all_orders_mfma(sem, gll, p, geometry):
     """Every tile packing: 16 // (p + 1) elements per tile side for p <= 7
-    (block-diagonal D), one element per tile above; the 7 x 5 mesh leaves
-    partly filled tiles at the end of every colour."""
+    (block-diagonal D), one element per tile above, three elements' lines
+    flattened over four tiles at p = 16 (k_poisson_mfma17); the 7 x 5 mesh
+    leaves partly filled tiles / wavefronts at the end of every colour."""
     import sem_oracle
+    if p == 16 and geometry == "nodal":
+        pytest.skip("the n = 17 MFMA kernel takes stored factors")
     from spectralelementmethod_amd import meshgen
     nodes, e2n = meshgen.structured_square(7, 5, p, warp=0.05)
     prob = sem_oracle.PoissonProblem(nodes, e2n, gll["half_%d" % p])
@@ -402,9 +407,14 @@ def test_mfma_auto_selection_and_limits(sem, poisson_action):
     # nodal geometry requested explicitly keeps the column kernel under auto
     nodes, e2n = meshgen.structured_square(3, 2, 12)
     assert sem.SEMOperator(12, e2n, nodes, geometry="nodal").plan_info()["kernel"] == "column"
+    # p = 16 (n = 17): the folded multi-element MFMA kernel, stored factors only
     nodes, e2n = meshgen.structured_square(2, 2, 16)
+    op = sem.SEMOperator(16, e2n, nodes, kernel="mfma")
+    assert op.plan_info()["kernel"] == "mfma" and op.plan_info()["geometry"] == "stored"
+    assert op.plan_info()["plan"] == "element-seams"
+    op = sem.SEMOperator(16, e2n, nodes, kernel="mfma", geometry="nodal")
     with pytest.raises(NotImplementedError):
-        sem.SEMOperator(16, e2n, nodes, kernel="mfma")
+        op.apply(torch.zeros(op.ndof, dtype=torch.float64, device="cuda"))
     fx = poisson_action
     with pytest.raises(NotImplementedError):
         sem.SEMOperator(4, fx["p4_4x4_e2n"], fx["p4_4x4_nodes"], dofs_per_node=2, kernel="mfma")
@@ -443,7 +453,7 @@ def test_mfma_accumulate_unreferenced_nonconforming(sem, poisson_action, gll):
     assert rel_l2(y, sem_oracle.PoissonProblem(nodes, e2d, gll["half_4"]).apply(u)) < TOL_ACTION
 
 
-@pytest.mark.parametrize("p,geometry", [(10, "stored"), (4, "nodal"), (3, "stored")])
+@pytest.mark.parametrize("p,geometry", [(10, "stored"), (4, "nodal"), (3, "stored"), (16, "stored")])
 def test_mfma_shared_output_split(sem, p, geometry):
     from spectralelementmethod_amd import meshgen
     from spectralelementmethod_amd.distributed import split_interface_elements
@@ -462,6 +472,32 @@ def test_mfma_shared_output_split(sem, p, geometry):
     op_i.apply(u, out=y)
     op_b.apply(u, out=y)
     assert (y - ref).norm().item() <= 1e-13 * ref.norm().item()
+
+
+@pytest.mark.parametrize("nex,ney", [(40, 30), (13, 7)])
+def test_mfma17_vs_column(sem, nex, ney):
+    """p = 16: the MFMA kernel (k_poisson_mfma17: three elements per
+    wavefront, folded 17-point contractions) against the column kernel, in
+    overwrite and accumulate mode; symmetric, annihilates constants."""
+    from spectralelementmethod_amd import meshgen
+    p = 16
+    nodes, e2n = meshgen.structured_square(nex, ney, p, warp=0.05)
+    g = torch.Generator(device="cuda").manual_seed(17)
+    col = sem.SEMOperator(p, e2n, nodes, kernel="column", geometry="stored")
+    mf = sem.SEMOperator(p, e2n, nodes, kernel="mfma")
+    assert mf.plan_info()["kernel"] == "mfma"
+    u = torch.randn(col.ndof, dtype=torch.float64, device="cuda", generator=g)
+    v = torch.randn(col.ndof, dtype=torch.float64, device="cuda", generator=g)
+    ya, yb = col.apply(u), mf.apply(u)
+    assert (ya - yb).norm().item() < 1e-12 * ya.norm().item()
+    y = v.clone()
+    mf.apply(u, out=y, accumulate=True)
+    assert (y - v - ya).norm().item() < 1e-12 * ya.norm().item()
+    Kv = mf.apply(v)
+    a, b = torch.dot(v, yb).item(), torch.dot(u, Kv).item()
+    assert abs(a - b) <= 1e-11 * max(abs(a), abs(b))
+    K1 = mf.apply(torch.ones_like(u))
+    assert K1.abs().max().item() < 1e-9 * yb.abs().max().item()
 
 
 def test_mfma_vs_column_larger(sem):

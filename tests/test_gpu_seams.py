@@ -120,3 +120,33 @@ def test_seams_axisymmetric(gpu, monkeypatch, geometry):
         out[seam] = [t.cpu().numpy() for t in (ys, yn, yj)]
     for a, b in zip(out["1"], out["0"]):
         assert rel_l2(a, b) <= 1e-15
+
+
+@pytest.mark.parametrize("nex,ney", [(7, 12), (20, 9)])
+def test_mfma17_seams_match_colour_launches(gpu, gll, monkeypatch, nex, ney):
+    """p = 16 MFMA kernel (k_poisson_mfma17): the element seam plan (one
+    launch in breadth-first element order + seam sums; AUTO there) against
+    its colour launches, overwrite and accumulate, and against the oracle."""
+    from spectralelementmethod_amd import meshgen
+    from spectralelementmethod_amd.operators import SEMOperator
+    p = 16
+    nodes, e2n = meshgen.structured_square(nex, ney, p, warp=0.05)
+    u = np.random.default_rng(p).standard_normal(nodes.shape[1])
+    ut = torch.from_numpy(u).to(gpu)
+    ops = SEMOperator(p, e2n, nodes, device=gpu, kernel="mfma")
+    info = ops.plan_info()
+    assert info["plan"] == "element-seams" and info["seam_nodes"] > 0, info
+    ys = ops.apply(ut)
+    monkeypatch.setenv("SEM_SEAM", "0")
+    opc = SEMOperator(p, e2n, nodes, device=gpu, kernel="mfma")
+    assert opc.plan_info()["plan"] == "element"
+    yc = opc.apply(ut)
+    assert rel_l2(ys.cpu().numpy(), yc.cpu().numpy()) <= 1e-15
+    y0 = torch.from_numpy(np.random.default_rng(3).standard_normal(nodes.shape[1])).to(gpu)
+    a_s, a_c = y0.clone(), y0.clone()
+    ops.apply(ut, out=a_s, accumulate=True)
+    opc.apply(ut, out=a_c, accumulate=True)
+    assert rel_l2(a_s.cpu().numpy(), a_c.cpu().numpy()) <= 1e-15
+    ref, ext = _oracle(gll, nodes, e2n, p, u)
+    y = ys.cpu().numpy()
+    assert rel_l2(y, ext) <= max(1.5 * rel_l2(ref, ext), TOL)
