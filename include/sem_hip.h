@@ -140,8 +140,8 @@ int sem_set_map_shared(sem_ctx* ctx, const uint32_t* d_e2n, const uint8_t* d_nod
  * written by several chains stored per writer colour and summed in colour
  * order by a second launch, bitwise equal to the colour launches; [5] is
  * then 1 and [8] the chain count.  (3 was a retired one-launch plan.)
- * 5: the n = 17 MFMA kernel's seam form (default there; SEM_SEAM=0 keeps
- * its colour launches): every element in one launch in breadth-first
+ * 5: the n = 17 MFMA kernel's seam form (SEM_SEAM=1; measured slower than
+ * its colour launches, which stay the default): every element in one launch in breadth-first
  * order, a node of several elements stored per element colour and summed
  * by the seam launch.
  * [21] the axisymmetric Stokes geometry mode (as [19]; 0 when

@@ -702,9 +702,12 @@ static bool build_map16(const Plan& P, int64_t n_elem, int n, int epw, int64_t n
 // order instead of one per colour; a node of several elements is stored by
 // each into the slot of its element's colour and summed by k_seam_sum (the
 // column kernel's seam plan with one element per chain).
-// seams for the n = 17 MFMA kernel under AUTO (SEM_SEAM=0 / 1 forces)
+// seams for the n = 17 MFMA kernel under AUTO (SEM_SEAM=0 / 1 forces): off.
+// p = 16, 198^2 on MI355X (profiles/r03/mfma17): one launch 0.161 ms + seam
+// sums 0.052 ms (the seam slots of horizontal element edges are scattered
+// 8-byte accesses) against 4 colour launches of 0.049 ms
 #ifndef MFMA_SEAM_AUTO
-#define MFMA_SEAM_AUTO 1
+#define MFMA_SEAM_AUTO 0
 #endif
 int build_plan_elem(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_node, int n,
                     const std::vector<uint8_t>& node_state, Plan& P, int seam = 0) {

@@ -1929,8 +1929,16 @@ __device__ __forceinline__ void mf17_contract(const MF17A& A, double (&v)[5]) {
   v[4] = as[2];  // row 8 + h: out[8] for h = 0, zero rows otherwise
 }
 
+// Factors read before phase B (their latency behind its LDS and MFMA work)
+// at 2 waves per SIMD (172 VGPRs): p = 16, 198^2, alternating on one box
+// (profiles/r03/mfma17/): 0.184-0.186 ms per action against 0.195 (factors
+// read in phase C, 132 VGPRs, 3 waves), 0.190 (read early, 3 waves, 24 B of
+// scratch) and 0.197 (4 waves, 40 B of scratch).
+#ifndef SEM_MF17_GPRE
+#define SEM_MF17_GPRE 1
+#endif
 #ifndef SEM_MF17_WAVES
-#define SEM_MF17_WAVES 3
+#define SEM_MF17_WAVES (SEM_MF17_GPRE ? 2 : 3)
 #endif
 // SEAM: code W_ATOMIC stores into the seam slot of the element's colour
 // (sp.colour indexed by element slot), summed by k_seam_sum
@@ -1997,6 +2005,20 @@ __global__ void __launch_bounds__(BLOCK, SEM_MF17_WAVES)
     mf17_contract(AD, d0[t]);
   }
   __syncthreads();
+  const double* gq = GP + sb * (3 * NN);
+#if SEM_MF17_GPRE
+  // factors read before phase B (their latency behind its LDS and MFMA work)
+  double gpre[T][5][3];
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const double* gp = gq + go(t, k) + el[t] * (2 * NN);  // slot stride 3 NN
+      gpre[t][k][0] = gp[0];
+      gpre[t][k][1] = gp[NN];
+      gpre[t][k][2] = gp[2 * NN];
+    }
+#endif
   // phase B: d1 = U D^T along the rows (Y), in place
 #pragma unroll
   for (int t = 0; t < T; ++t) {
@@ -2010,15 +2032,18 @@ __global__ void __launch_bounds__(BLOCK, SEM_MF17_WAVES)
   __syncthreads();
   // phase C: factors (X), w0 = G00 d0 + G01 d1 -> y0 = D^T w0, w1 = G01 d0 + G11 d1 in place
   const MF17A AT = mf17_operands(gD, true, lane);
-  const double* gq = GP + sb * (3 * NN);
   double y0[T][5];
 #pragma unroll
   for (int t = 0; t < T; ++t) {
     double w1[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
+#if SEM_MF17_GPRE
+      const double g0 = gpre[t][k][0], g1 = gpre[t][k][1], g2 = gpre[t][k][2];
+#else
       const double* gp = gq + go(t, k) + el[t] * (2 * NN);  // slot stride 3 NN
       const double g0 = gp[0], g1 = gp[NN], g2 = gp[2 * NN];
+#endif
       const double d1 = P[xo(t, k)];
       y0[t][k] = live(t, k) ? fma(g0, d0[t][k], g1 * d1) : 0.0;
       w1[k] = live(t, k) ? fma(g1, d0[t][k], g2 * d1) : 0.0;

@@ -125,7 +125,7 @@ def test_seams_axisymmetric(gpu, monkeypatch, geometry):
 @pytest.mark.parametrize("nex,ney", [(7, 12), (20, 9)])
 def test_mfma17_seams_match_colour_launches(gpu, gll, monkeypatch, nex, ney):
     """p = 16 MFMA kernel (k_poisson_mfma17): the element seam plan (one
-    launch in breadth-first element order + seam sums; AUTO there) against
+    launch in breadth-first element order + seam sums; SEM_SEAM=1) against
     its colour launches, overwrite and accumulate, and against the oracle."""
     from spectralelementmethod_amd import meshgen
     from spectralelementmethod_amd.operators import SEMOperator
@@ -133,6 +133,7 @@ def test_mfma17_seams_match_colour_launches(gpu, gll, monkeypatch, nex, ney):
     nodes, e2n = meshgen.structured_square(nex, ney, p, warp=0.05)
     u = np.random.default_rng(p).standard_normal(nodes.shape[1])
     ut = torch.from_numpy(u).to(gpu)
+    monkeypatch.setenv("SEM_SEAM", "1")
     ops = SEMOperator(p, e2n, nodes, device=gpu, kernel="mfma")
     info = ops.plan_info()
     assert info["plan"] == "element-seams" and info["seam_nodes"] > 0, info
