@@ -1930,10 +1930,11 @@ __device__ __forceinline__ void mf17_contract(const MF17A& A, double (&v)[5]) {
 }
 
 // Factors read before phase B (their latency behind its LDS and MFMA work)
-// at 2 waves per SIMD (172 VGPRs): p = 16, 198^2, alternating on one box
-// (profiles/r03/mfma17/): 0.184-0.186 ms per action against 0.195 (factors
-// read in phase C, 132 VGPRs, 3 waves), 0.190 (read early, 3 waves, 24 B of
-// scratch) and 0.197 (4 waves, 40 B of scratch).
+// at 2 waves per SIMD (172 VGPRs): p = 16, 198^2, two runs each alternating
+// on one box (profiles/r03/mfma17/, median kernel ms per action): 0.184 /
+// 0.189 against 0.195 / 0.199 (factors read in phase C, 132 VGPRs, 3 waves),
+// 0.186 / 0.191 (read early at 3 waves, 24 B of scratch) and 0.197 / 0.197
+// (4 waves, 40 B of scratch); the column kernel 0.157 / 0.157.
 #ifndef SEM_MF17_GPRE
 #define SEM_MF17_GPRE 1
 #endif
