@@ -2100,6 +2100,209 @@ __global__ void __launch_bounds__(BLOCK, SEM_MF17_WAVES)
   }
 }
 
+// Persistent form: a grid of resident workgroups, each wavefront pair walks
+// element triples q = pair, pair + P, ... (P pairs in the grid) and reads
+// the NEXT triple's map (during phase B) and u (during phase C) while the
+// current one computes, and the current triple's factors before phase A:
+// the per-triple chain map -> gather -> factors is off the critical path
+// except for the first triple of each pair.  Same arithmetic and scatter as
+// k_poisson_mfma17.  240 VGPRs, 2 waves/SIMD, no scratch.  p = 16, 198^2,
+// two runs alternating on one box (profiles/r03/mfma17/persist/, median
+// kernel ms per action): 0.180 / 0.182 against 0.185 / 0.187 for one pair
+// per triple; the column kernel 0.159 / 0.160 -- the gain is small, so the
+// per-triple chain is not what bounds the kernel.
+#ifndef SEM_MF17P_WAVES
+#define SEM_MF17P_WAVES 2
+#endif
+template <int N, bool SEAM>
+__global__ void __launch_bounds__(BLOCK, SEM_MF17P_WAVES)
+    k_poisson_mfma17p(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
+                      const double* __restrict__ u, double* __restrict__ y,
+                      const double* __restrict__ gD, int64_t s0, int64_t s1, int accumulate,
+                      SeamPlan sp) {
+  static_assert(N == MF17_N, "folded multi-element form of n = 17");
+  constexpr int NN = N * N, T = MF17_TW;
+  __shared__ double lds[MF17_PAIRS][MF17_PLANE];
+  const int lane = threadIdx.x % WAVE;
+  const int wave = threadIdx.x / WAVE;
+  const int pair = wave >> 1, half = wave & 1;
+  const int64_t ntr = (s1 - s0 + MF17_EW - 1) / MF17_EW;  // element triples
+  const int64_t np = (int64_t)gridDim.x * MF17_PAIRS;
+  const int64_t q0 = (int64_t)blockIdx.x * MF17_PAIRS;  // the workgroup's first pair
+  // every pair of a workgroup runs the first pair's iteration count (the
+  // workgroup barriers); a pair past the end works on slot s0, writes nothing
+  const int64_t iters = q0 < ntr ? (ntr - q0 + np - 1) / np : 0;
+  double* P = lds[pair];
+  const int h = lane >> 4, c = lane & 15;
+  const bool hm = h == 0;  // owner of the middle entry
+  const int R[5] = {h, 4 + h, 16 - h, 12 - h, 8};
+  const MF17A AD = mf17_operands(gD, false, lane);
+  const MF17A AT = mf17_operands(gD, true, lane);
+  constexpr int JUNK = MF17_EW * NN;
+  int ef[T], lf[T];  // element and line of tile 2 half + t
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int f = 16 * (2 * half + t) + c;
+    ef[t] = f / N;
+    lf[t] = f - ef[t] * N;
+  }
+  // triple q: base slot, per-tile validity and the element used (0 stands in)
+  auto base = [&](int64_t q) { return q < ntr ? s0 + q * MF17_EW : s0; };
+  auto valid = [&](int64_t q, int t) {
+    return q < ntr && ef[t] < MF17_EW && s0 + q * MF17_EW + ef[t] < s1;
+  };
+  auto go = [&](int t, int el, int k) { return el * NN + lf[t] + (k < 4 || hm ? R[k] : 0) * N; };
+
+  int64_t q = q0 + pair;
+  uint32_t raw[T][5];
+  double uv[T][5];
+  {
+    const int64_t sb = base(q);
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int el = valid(q, t) ? ef[t] : 0;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) raw[t][k] = mapP[sb * NN + go(t, el, k)];
+    }
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+      for (int k = 0; k < 5; ++k) uv[t][k] = u[raw[t][k] & GID_MASK];
+  }
+  for (int64_t it = 0; it < iters; ++it, q += np) {
+    const int64_t sb = base(q), qn = q + np, sbn = base(qn);
+    bool ok[T];
+    int el[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      ok[t] = valid(q, t);
+      el[t] = ok[t] ? ef[t] : 0;
+    }
+    auto live = [&](int t, int k) { return ok[t] && (k < 4 || hm); };
+    auto xo = [&](int t, int k) {
+      return live(t, k) ? el[t] * NN + lf[t] + R[k] * N : JUNK + half * WAVE + lane;
+    };
+    auto yo = [&](int t, int k) {
+      return live(t, k) ? el[t] * NN + lf[t] * N + R[k] : JUNK + half * WAVE + lane;
+    };
+    // factors of this triple
+    double g[T][5][3];
+    {
+      const double* gq = GP + sb * (3 * NN);
+#pragma unroll
+      for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+          const double* gp = gq + go(t, el[t], k) + el[t] * (2 * NN);  // slot stride 3 NN
+          g[t][k][0] = gp[0];
+          g[t][k][1] = gp[NN];
+          g[t][k][2] = gp[2 * NN];
+        }
+    }
+    // phase A: U (X) into the plane, d0 = D U
+    double d0[T][5];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        d0[t][k] = live(t, k) ? uv[t][k] : 0.0;
+        raw[t][k] = live(t, k) ? raw[t][k] : (W_SKIP << CODE_SHIFT);
+        P[xo(t, k)] = d0[t][k];
+      }
+      mf17_contract(AD, d0[t]);
+    }
+    __syncthreads();
+    // next triple's map
+    uint32_t rawn[T][5];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int eln = valid(qn, t) ? ef[t] : 0;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) rawn[t][k] = mapP[sbn * NN + go(t, eln, k)];
+    }
+    // phase B: d1 = U D^T along the rows (Y), in place
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      double v[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) v[k] = live(t, k) ? P[yo(t, k)] : 0.0;
+      mf17_contract(AD, v);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) P[yo(t, k)] = v[k];
+    }
+    __syncthreads();
+    // next triple's u
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+      for (int k = 0; k < 5; ++k) uv[t][k] = u[rawn[t][k] & GID_MASK];
+    // phase C: w0 = G00 d0 + G01 d1 -> y0 = D^T w0, w1 = G01 d0 + G11 d1 in place
+    double y0[T][5];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      double w1[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const double d1 = P[xo(t, k)];
+        y0[t][k] = live(t, k) ? fma(g[t][k][0], d0[t][k], g[t][k][1] * d1) : 0.0;
+        w1[k] = live(t, k) ? fma(g[t][k][1], d0[t][k], g[t][k][2] * d1) : 0.0;
+      }
+      mf17_contract(AT, y0[t]);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) P[xo(t, k)] = w1[k];
+    }
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t ry = y_rsrc(y);
+    double prev[T][5];
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const uint32_t a = (raw[t][k] >> CODE_SHIFT) & 3u;
+        const bool need = a == W_RMW || (a == W_STORE && accumulate);
+        const uint32_t off = need ? (raw[t][k] & GID_MASK) * 8u : 0x80000000u;
+        prev[t][k] =
+            __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(ry, off, 0, CPOL_NT));
+      }
+    // phase D: y1 = w1 D along the rows (Y), in place
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      double v[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) v[k] = live(t, k) ? P[yo(t, k)] : 0.0;
+      mf17_contract(AT, v);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) P[yo(t, k)] = v[k];
+    }
+    __syncthreads();
+    // phase E: y = y0 + y1 (X), scatter (a lane reads only its own plane
+    // entries here and writes only those in the next phase A: no barrier)
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      double* sbase = nullptr;
+      if constexpr (SEAM) sbase = sp.buf + (int64_t)sp.colour[sb + el[t]] * sp.n_node;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const uint32_t a = (raw[t][k] >> CODE_SHIFT) & 3u;
+        const uint32_t gid = raw[t][k] & GID_MASK;
+        const double v = y0[t][k] + P[xo(t, k)];
+        if (a == W_STORE || a == W_RMW) {
+          y[gid] = prev[t][k] + v;
+        } else if (a == W_ATOMIC) {
+          if constexpr (SEAM)
+            sbase[gid] = v;
+          else
+            atomic_add_f64(y + gid, v);
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+      for (int k = 0; k < 5; ++k) raw[t][k] = rawn[t][k];
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Geometry: nodes -> x_phys -> J -> det/inv -> W -> operator factors.
 // Thread per local node, EPB elements per block, LDS staging (setup path).

@@ -80,6 +80,35 @@ void launch_chains(sem_ctx* c, int op_kind, bool nodal, const double* u, double*
   }
 }
 
+// the n = 17 MFMA kernel over element slots [c0, c1): the persistent form
+// (SEM_MF17_PERSIST, default; 3 % faster at p = 16, profiles/r03/mfma17/
+// persist) on a grid of resident workgroups, or one wavefront pair per
+// element triple
+#ifndef SEM_MF17_PERSIST
+#define SEM_MF17_PERSIST 1
+#endif
+template <bool SEAM>
+void launch_mfma17(sem_ctx* c, const double* u, double* y, int acc, int64_t c0, int64_t c1,
+                   const SeamPlan& sp, hipStream_t st) {
+  constexpr int per_block = MF17_PAIRS * MF17_EW;
+  const int64_t nwg = (c1 - c0 + per_block - 1) / per_block;
+  if (SEM_MF17_PERSIST) {
+    static int resident = 0;  // workgroups resident on the device at SEM_MF17P_WAVES
+    if (!resident) {
+      int ncu = 0;
+      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || ncu <= 0)
+        ncu = 256;
+      resident = ncu * 4 * SEM_MF17P_WAVES / (BLOCK / WAVE);
+    }
+    const dim3 g((unsigned)std::min<int64_t>(nwg, resident));
+    hipLaunchKernelGGL((k_poisson_mfma17p<MF17_N, SEAM>), g, dim3(BLOCK), 0, st, c->d_mapP,
+                       c->d_GP[0], u, y, c->d_D, c0, c1, acc, sp);
+  } else {
+    hipLaunchKernelGGL((k_poisson_mfma17<MF17_N, SEAM>), dim3((unsigned)nwg), dim3(BLOCK), 0, st,
+                       c->d_mapP, c->d_GP[0], u, y, c->d_D, c0, c1, acc, sp);
+  }
+}
+
 template <int N>
 int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc, bool lin,
                    hipStream_t st, double* dot_out) {
@@ -92,11 +121,7 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
       if (op_kind != SEM_OP_POISSON) return sem::fail(SEM_E_NOTIMPL, "MFMA kernel: Poisson only");
       if (nodal) return sem::fail(SEM_E_NOTIMPL, "the n = 17 MFMA kernel takes stored factors");
       const int64_t c0 = c->colour_start.front(), c1 = c->colour_start.back();
-      constexpr int per_block = MF17_PAIRS * MF17_EW;
-      const dim3 g((unsigned)((c1 - c0 + per_block - 1) / per_block));
-      const SeamPlan sp{c->d_ccol, c->d_seam_buf, c->n_node};
-      hipLaunchKernelGGL((k_poisson_mfma17<N, true>), g, dim3(BLOCK), 0, st, c->d_mapP,
-                         c->d_GP[0], u, y, c->d_D, c0, c1, acc, sp);
+      launch_mfma17<true>(c, u, y, acc, c0, c1, SeamPlan{c->d_ccol, c->d_seam_buf, c->n_node}, st);
       const int rc = launch_seam_sum(c, y, acc, st);
       if (rc || !dot_out) return rc;
       return sem::fail(SEM_E_STATE, "fused dot on the MFMA seam plan");
@@ -130,10 +155,7 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
                              c->d_GP[0], nullptr, u, y, c->d_D, w, c0, c1, acc);
       } else if constexpr (N == MF17_N) {
         if (nodal) return sem::fail(SEM_E_NOTIMPL, "the n = 17 MFMA kernel takes stored factors");
-        constexpr int per_block = MF17_PAIRS * MF17_EW;
-        const dim3 g((unsigned)((c1 - c0 + per_block - 1) / per_block));
-        hipLaunchKernelGGL((k_poisson_mfma17<N, false>), g, dim3(BLOCK), 0, st, c->d_mapP,
-                           c->d_GP[0], u, y, c->d_D, c0, c1, acc, SeamPlan{});
+        launch_mfma17<false>(c, u, y, acc, c0, c1, SeamPlan{}, st);
       } else {
         return sem::fail(SEM_E_NOTIMPL, "the MFMA kernel needs n <= 17");
       }
