@@ -841,19 +841,24 @@ __device__ __forceinline__ void poisson_group_nodal(const MapRef& mref,
 
 // the value of lane + 1 (lane 63: its own).  SEM_DPP_SHIFT: a DPP
 // wave_shl:1 move per dword (two VALU moves) instead of __shfl_down, whose
-// ds_bpermute goes through the LDS and waits on it
+// ds_bpermute goes through the LDS and waits on it.  Below n = 17 only: at
+// p = 16 the DPP form lifts the stored seam kernel to 169 VGPRs (2 waves per
+// SIMD), and holding it at 3 waves with a launch bound changed its code for
+// the worse -- 0.134 ms per action with __shfl_down against 0.152 (DPP,
+// 3-wave bound) and 0.157 (DPP), profiles/r03/p16_regression/.
 #ifndef SEM_DPP_SHIFT
 #define SEM_DPP_SHIFT 1
 #endif
+template <int N>
 __device__ __forceinline__ double lane_next(double x) {
-#if SEM_DPP_SHIFT
-  constexpr int WAVE_SHL1 = 0x130;
-  const int lo = __double2loint(x), hi = __double2hiint(x);
-  return __hiloint2double(__builtin_amdgcn_update_dpp(hi, hi, WAVE_SHL1, 0xF, 0xF, false),
-                          __builtin_amdgcn_update_dpp(lo, lo, WAVE_SHL1, 0xF, 0xF, false));
-#else
-  return __shfl_down(x, 1, WAVE);
-#endif
+  if constexpr (SEM_DPP_SHIFT && N < 17) {
+    constexpr int WAVE_SHL1 = 0x130;
+    const int lo = __double2loint(x), hi = __double2hiint(x);
+    return __hiloint2double(__builtin_amdgcn_update_dpp(hi, hi, WAVE_SHL1, 0xF, 0xF, false),
+                            __builtin_amdgcn_update_dpp(lo, lo, WAVE_SHL1, 0xF, 0xF, false));
+  } else {
+    return __shfl_down(x, 1, WAVE);
+  }
 }
 
 #ifndef SEM_ROUND_SYNC_ALWAYS
@@ -890,7 +895,7 @@ __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_
   for (int c = 0; c < NC; ++c)
 #pragma unroll
     for (int p = 0; p < N; ++p) {
-      const double vn = lane_next(v[c][p]);
+      const double vn = lane_next<N>(v[c][p]);
       if ((raw[p] >> CODE_SHIFT) & W_MERGE) v[c][p] += vn;
     }
   // hand the last lane's column to the next group of the chain
