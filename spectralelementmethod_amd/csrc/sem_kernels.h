@@ -1934,188 +1934,20 @@ __device__ __forceinline__ void mf17_contract(const MF17A& A, double (&v)[5]) {
   v[4] = as[2];  // row 8 + h: out[8] for h = 0, zero rows otherwise
 }
 
-// Factors read before phase B (their latency behind its LDS and MFMA work)
-// at 2 waves per SIMD (172 VGPRs): p = 16, 198^2, two runs each alternating
-// on one box (profiles/r03/mfma17/, median kernel ms per action): 0.184 /
-// 0.189 against 0.195 / 0.199 (factors read in phase C, 132 VGPRs, 3 waves),
-// 0.186 / 0.191 (read early at 3 waves, 24 B of scratch) and 0.197 / 0.197
-// (4 waves, 40 B of scratch); the column kernel 0.157 / 0.157.
-#ifndef SEM_MF17_GPRE
-#define SEM_MF17_GPRE 1
-#endif
-#ifndef SEM_MF17_WAVES
-#define SEM_MF17_WAVES (SEM_MF17_GPRE ? 2 : 3)
-#endif
-// SEAM: code W_ATOMIC stores into the seam slot of the element's colour
-// (sp.colour indexed by element slot), summed by k_seam_sum
-template <int N, bool SEAM>
-__global__ void __launch_bounds__(BLOCK, SEM_MF17_WAVES)
-    k_poisson_mfma17(const uint32_t* __restrict__ mapP, const double* __restrict__ GP,
-                     const double* __restrict__ u, double* __restrict__ y,
-                     const double* __restrict__ gD, int64_t s0, int64_t s1, int accumulate,
-                     SeamPlan sp) {
-  static_assert(N == MF17_N, "folded multi-element form of n = 17");
-  constexpr int NN = N * N, T = MF17_TW;
-  __shared__ double lds[MF17_PAIRS][MF17_PLANE];
-  const int lane = threadIdx.x % WAVE;
-  const int wave = threadIdx.x / WAVE;
-  const int pair = wave >> 1, half = wave & 1;
-  const int64_t slot0 = s0 + ((int64_t)blockIdx.x * MF17_PAIRS + pair) * MF17_EW;
-  // a pair past the end still runs (workgroup barriers below) on slot s0's
-  // data and writes nothing
-  const int64_t sb = slot0 < s1 ? slot0 : s0;
-  double* P = lds[pair];
-  const int h = lane >> 4, c = lane & 15;
-  const bool hm = h == 0;  // owner of the middle entry
-  const int R[5] = {h, 4 + h, 16 - h, 12 - h, 8};
-  const MF17A AD = mf17_operands(gD, false, lane);
-  constexpr int JUNK = MF17_EW * NN;  // per-lane junk slots for entries off the plane
-  // tile 2 half + t: line f = 16 (2 half + t) + c of element e = f / 17.
-  // xb / yb: the line's base in the plane for the X / Y layouts (entry k at
-  // xb + R[k] * 17 / yb + R[k]); xb is also the line's offset in the
-  // element-slot map relative to slot sb
-  int xb[T], yb[T], el[T];
-  bool ok[T];  // the line's element slot exists
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
-    const int f = 16 * (2 * half + t) + c;
-    const int e = f / N;
-    const int l = f - e * N;
-    ok[t] = e < MF17_EW && slot0 + e < s1;
-    el[t] = ok[t] ? e : 0;  // element 0 of slot sb stands in for a missing slot
-    xb[t] = el[t] * NN + l;
-    yb[t] = el[t] * NN + l * N;
-  }
-  auto live = [&](int t, int k) { return ok[t] && (k < 4 || hm); };
-  auto xo = [&](int t, int k) { return live(t, k) ? xb[t] + R[k] * N : JUNK + half * WAVE + lane; };
-  auto yo = [&](int t, int k) { return live(t, k) ? yb[t] + R[k] : JUNK + half * WAVE + lane; };
-  auto go = [&](int t, int k) { return xb[t] + (k < 4 || hm ? R[k] : 0) * N; };
-  const uint32_t* mp = mapP + sb * NN;
-
-  // phase A: gather (X), d0 = D U, U into the plane
-  uint32_t raw[T][5];
-  double d0[T][5];
-#pragma unroll
-  for (int t = 0; t < T; ++t)
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      const uint32_t e = mp[go(t, k)];
-      raw[t][k] = live(t, k) ? e : (W_SKIP << CODE_SHIFT);
-      d0[t][k] = u[e & GID_MASK];
-      d0[t][k] = live(t, k) ? d0[t][k] : 0.0;
-    }
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
-#pragma unroll
-    for (int k = 0; k < 5; ++k) P[xo(t, k)] = d0[t][k];
-    mf17_contract(AD, d0[t]);
-  }
-  __syncthreads();
-  const double* gq = GP + sb * (3 * NN);
-#if SEM_MF17_GPRE
-  // factors read before phase B (their latency behind its LDS and MFMA work)
-  double gpre[T][5][3];
-#pragma unroll
-  for (int t = 0; t < T; ++t)
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      const double* gp = gq + go(t, k) + el[t] * (2 * NN);  // slot stride 3 NN
-      gpre[t][k][0] = gp[0];
-      gpre[t][k][1] = gp[NN];
-      gpre[t][k][2] = gp[2 * NN];
-    }
-#endif
-  // phase B: d1 = U D^T along the rows (Y), in place
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
-    double v[5];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) v[k] = live(t, k) ? P[yo(t, k)] : 0.0;
-    mf17_contract(AD, v);
-#pragma unroll
-    for (int k = 0; k < 5; ++k) P[yo(t, k)] = v[k];
-  }
-  __syncthreads();
-  // phase C: factors (X), w0 = G00 d0 + G01 d1 -> y0 = D^T w0, w1 = G01 d0 + G11 d1 in place
-  const MF17A AT = mf17_operands(gD, true, lane);
-  double y0[T][5];
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
-    double w1[5];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-#if SEM_MF17_GPRE
-      const double g0 = gpre[t][k][0], g1 = gpre[t][k][1], g2 = gpre[t][k][2];
-#else
-      const double* gp = gq + go(t, k) + el[t] * (2 * NN);  // slot stride 3 NN
-      const double g0 = gp[0], g1 = gp[NN], g2 = gp[2 * NN];
-#endif
-      const double d1 = P[xo(t, k)];
-      y0[t][k] = live(t, k) ? fma(g0, d0[t][k], g1 * d1) : 0.0;
-      w1[k] = live(t, k) ? fma(g1, d0[t][k], g2 * d1) : 0.0;
-    }
-    mf17_contract(AT, y0[t]);
-#pragma unroll
-    for (int k = 0; k < 5; ++k) P[xo(t, k)] = w1[k];
-  }
-  __syncthreads();
-  // read-modify-write operands of the scatter, all in flight together
-  const __amdgpu_buffer_rsrc_t ry = y_rsrc(y);
-  double prev[T][5];
-#pragma unroll
-  for (int t = 0; t < T; ++t)
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      const uint32_t a = (raw[t][k] >> CODE_SHIFT) & 3u;
-      const bool need = a == W_RMW || (a == W_STORE && accumulate);
-      const uint32_t off = need ? (raw[t][k] & GID_MASK) * 8u : 0x80000000u;
-      prev[t][k] =
-          __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(ry, off, 0, CPOL_NT));
-    }
-  // phase D: y1 = w1 D along the rows (Y), in place
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
-    double v[5];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) v[k] = live(t, k) ? P[yo(t, k)] : 0.0;
-    mf17_contract(AT, v);
-#pragma unroll
-    for (int k = 0; k < 5; ++k) P[yo(t, k)] = v[k];
-  }
-  __syncthreads();
-  // phase E: y = y0 + y1 (X), scatter
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
-    double* sbase = nullptr;
-    if constexpr (SEAM) sbase = sp.buf + (int64_t)sp.colour[sb + el[t]] * sp.n_node;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      const uint32_t a = (raw[t][k] >> CODE_SHIFT) & 3u;
-      const uint32_t gid = raw[t][k] & GID_MASK;
-      const double v = y0[t][k] + P[xo(t, k)];
-      if (a == W_STORE || a == W_RMW) {
-        y[gid] = prev[t][k] + v;
-      } else if (a == W_ATOMIC) {
-        if constexpr (SEAM)
-          sbase[gid] = v;
-        else
-          atomic_add_f64(y + gid, v);
-      }
-    }
-  }
-}
-
 // Persistent form: a grid of resident workgroups, each wavefront pair walks
 // element triples q = pair, pair + P, ... (P pairs in the grid) and reads
 // the NEXT triple's map (during phase B) and u (during phase C) while the
 // current one computes, and the current triple's factors before phase A:
 // the per-triple chain map -> gather -> factors is off the critical path
-// except for the first triple of each pair.  Same arithmetic and scatter as
-// k_poisson_mfma17.  240 VGPRs, 2 waves/SIMD, no scratch.  p = 16, 198^2,
-// two runs alternating on one box (profiles/r03/mfma17/persist/, median
-// kernel ms per action): 0.180 / 0.182 against 0.185 / 0.187 for one pair
-// per triple; the column kernel 0.159 / 0.160 -- the gain is small, so the
-// per-triple chain is not what bounds the kernel.
+// except for the first triple of each pair.  240 VGPRs, 2 waves/SIMD, no
+// scratch.  p = 16, 198^2, two runs alternating on one box
+// (profiles/r03/mfma17/persist/, median kernel ms per action): 0.180 /
+// 0.182 against 0.185 / 0.187 for the earlier form with one wavefront pair
+// per triple (factors read before phase B; reading them in phase C at 3
+// waves/SIMD 0.195 / 0.199, 4 waves with scratch 0.197, profiles/r03/
+// mfma17/); the column kernel 0.159 / 0.160 on that box -- the gain is
+// small, so the per-triple chain is not what bounds the kernel (DESIGN.md
+// §4.6).  The one-pair-per-triple form was removed after these runs.
 #ifndef SEM_MF17P_WAVES
 #define SEM_MF17P_WAVES 2
 #endif

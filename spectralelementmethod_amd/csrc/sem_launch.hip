@@ -81,32 +81,24 @@ void launch_chains(sem_ctx* c, int op_kind, bool nodal, const double* u, double*
 }
 
 // the n = 17 MFMA kernel over element slots [c0, c1): the persistent form
-// (SEM_MF17_PERSIST, default; 3 % faster at p = 16, profiles/r03/mfma17/
-// persist) on a grid of resident workgroups, or one wavefront pair per
-// element triple
-#ifndef SEM_MF17_PERSIST
-#define SEM_MF17_PERSIST 1
-#endif
+// on a grid of resident workgroups (at most one generation)
 template <bool SEAM>
 void launch_mfma17(sem_ctx* c, const double* u, double* y, int acc, int64_t c0, int64_t c1,
                    const SeamPlan& sp, hipStream_t st) {
   constexpr int per_block = MF17_PAIRS * MF17_EW;
   const int64_t nwg = (c1 - c0 + per_block - 1) / per_block;
-  if (SEM_MF17_PERSIST) {
-    static int resident = 0;  // workgroups resident on the device at SEM_MF17P_WAVES
-    if (!resident) {
-      int ncu = 0;
-      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || ncu <= 0)
-        ncu = 256;
-      resident = ncu * 4 * SEM_MF17P_WAVES / (BLOCK / WAVE);
-    }
-    const dim3 g((unsigned)std::min<int64_t>(nwg, resident));
-    hipLaunchKernelGGL((k_poisson_mfma17p<MF17_N, SEAM>), g, dim3(BLOCK), 0, st, c->d_mapP,
-                       c->d_GP[0], u, y, c->d_D, c0, c1, acc, sp);
-  } else {
-    hipLaunchKernelGGL((k_poisson_mfma17<MF17_N, SEAM>), dim3((unsigned)nwg), dim3(BLOCK), 0, st,
-                       c->d_mapP, c->d_GP[0], u, y, c->d_D, c0, c1, acc, sp);
+  static int resident = 0;  // workgroups resident on the device at SEM_MF17P_WAVES
+  if (!resident) {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) !=
+            hipSuccess ||
+        ncu <= 0)
+      ncu = 256;
+    resident = ncu * 4 * SEM_MF17P_WAVES / (BLOCK / WAVE);
   }
+  const dim3 g((unsigned)std::min<int64_t>(nwg, resident));
+  hipLaunchKernelGGL((k_poisson_mfma17p<MF17_N, SEAM>), g, dim3(BLOCK), 0, st, c->d_mapP,
+                     c->d_GP[0], u, y, c->d_D, c0, c1, acc, sp);
 }
 
 template <int N>

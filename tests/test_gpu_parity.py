@@ -370,7 +370,7 @@ def test_poisson_action_golden_mfma(sem, poisson_action, gll, name, geometry):
 def test_poisson_all_orders_mfma(sem, gll, p, geometry):
     """Every tile packing: 16 // (p + 1) elements per tile side for p <= 7
     (block-diagonal D), one element per tile above, three elements' lines
-    flattened over four tiles at p = 16 (k_poisson_mfma17); the 7 x 5 mesh
+    flattened over four tiles at p = 16 (k_poisson_mfma17p); the 7 x 5 mesh
     leaves partly filled tiles / wavefronts at the end of every colour."""
     import sem_oracle
     if p == 16 and geometry == "nodal":
@@ -476,7 +476,7 @@ def test_mfma_shared_output_split(sem, p, geometry):
 
 @pytest.mark.parametrize("nex,ney", [(40, 30), (13, 7)])
 def test_mfma17_vs_column(sem, nex, ney):
-    """p = 16: the MFMA kernel (k_poisson_mfma17: three elements per
+    """p = 16: the MFMA kernel (k_poisson_mfma17p: three elements per
     wavefront, folded 17-point contractions) against the column kernel, in
     overwrite and accumulate mode; symmetric, annihilates constants."""
     from spectralelementmethod_amd import meshgen

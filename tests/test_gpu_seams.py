@@ -124,7 +124,7 @@ def test_seams_axisymmetric(gpu, monkeypatch, geometry):
 
 @pytest.mark.parametrize("nex,ney", [(7, 12), (20, 9)])
 def test_mfma17_seams_match_colour_launches(gpu, gll, monkeypatch, nex, ney):
-    """p = 16 MFMA kernel (k_poisson_mfma17): the element seam plan (one
+    """p = 16 MFMA kernel (k_poisson_mfma17p): the element seam plan (one
     launch in breadth-first element order + seam sums; SEM_SEAM=1) against
     its colour launches, overwrite and accumulate, and against the oracle."""
     from spectralelementmethod_amd import meshgen
