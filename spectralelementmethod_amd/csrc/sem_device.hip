@@ -169,12 +169,14 @@ int ctx_device(const sem_ctx* c) { return c->device; }
 namespace semd {
 // second launch of the seam plan (k_seam_sum / k_seam_sum2 over the seam
 // nodes, one instantiation per colour count)
-int64_t seam_sum_blocks(const sem_ctx* c) { return c->n_seam ? grid_for(c->n_seam) : 0; }
+int64_t seam_sum_blocks(const sem_ctx* c) {
+  return c->n_seam ? grid_for(c->n_seam, BLOCK * SEAM_ILP) : 0;
+}
 
 int launch_seam_sum(sem_ctx* c, double* y, int acc, hipStream_t st, const double* du,
                     double* dot) {
   if (!c->n_seam) return SEM_OK;
-  const dim3 g(grid_for(c->n_seam)), b(BLOCK);
+  const dim3 g(c->dpn == 2 ? grid_for(c->n_seam) : (int)seam_sum_blocks(c)), b(BLOCK);
   switch (c->seam_ns) {
 #define SEAM_NS(K)                                                                           \
   case K:                                                                                  \

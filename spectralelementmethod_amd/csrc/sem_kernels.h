@@ -371,17 +371,27 @@ struct NoPrefetch {
 struct SeamOut {
   double* base = nullptr;  // buf + colour * n_node * dpn of the chain
 };
+#ifndef SEM_NT_STORE_SEAM
+#define SEM_NT_STORE_SEAM 1  // the seam plan's y and slot stores nontemporal
+#endif
+template <bool NT = (SEM_NT_STORE_SEAM != 0)>
+__device__ __forceinline__ void st_seam(double v, double* dst) {
+  if constexpr (NT)
+    __builtin_nontemporal_store(v, dst);
+  else
+    *dst = v;
+}
 __device__ __forceinline__ void emit1_seam(double* __restrict__ y, uint32_t raw, double v,
                                            int accumulate, const SeamOut& so) {
   const uint32_t a = (raw >> CODE_SHIFT) & 3u;
   const uint32_t gid = raw & GID_MASK;
   double* dst = y + gid;
   if (a == W_STORE)
-    __builtin_nontemporal_store(accumulate ? rmw_load(dst) + v : v, dst);
+    st_seam(accumulate ? rmw_load(dst) + v : v, dst);
   else if (a == W_RMW)  // first touch of a SEM_NODE_PRIOR node
-    __builtin_nontemporal_store(rmw_load(dst) + v, dst);
+    st_seam(rmw_load(dst) + v, dst);
   else if (a == W_ATOMIC)
-    __builtin_nontemporal_store(v, so.base + gid);
+    st_seam(v, so.base + gid);
 }
 
 __device__ __forceinline__ void emit2(double* __restrict__ y, uint32_t raw, double v0, double v1,
@@ -1061,6 +1071,9 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
 // holds a value (SEM_NODE_PRIOR)
 // NS colours: the slot loads of a node are issued together (predicated
 // buffer loads: an unused slot reads past the range, 0 and no traffic).
+#ifndef SEAM_ILP
+#define SEAM_ILP 2
+#endif
 template <int NS, bool DOT = false>
 __global__ void __launch_bounds__(BLOCK)
     k_seam_sum(double* __restrict__ y, const uint32_t* __restrict__ gid,
@@ -1097,33 +1110,53 @@ __global__ void __launch_bounds__(BLOCK)
                const uint16_t* __restrict__ mask, int64_t n, const double* __restrict__ buf,
                int64_t n_node, int accumulate, const double* __restrict__ du,
                double* __restrict__ dot) {
+  // SEAM_ILP nodes per thread per pass (a block covers SEAM_ILP * BLOCK
+  // consecutive seam nodes): their index, slot and y loads are in flight
+  // together instead of one dependent chain per node
   double dotv = 0.0;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t g = gid[i];
-    const uint32_t m = mask[i];
-    const bool prior = accumulate || (m & 0x100u);
-    const double y0 = prior ? y[g] : 0.0;
-    double b[NS];
+  // one buffer resource per colour plane (each < 2^31 bytes: n_node < 2^28)
+  __amdgpu_buffer_rsrc_t rb[NS];
 #pragma unroll
-    for (int c = 0; c < NS; ++c) {
-      // one buffer resource per colour plane (each < 2^31 bytes: n_node < 2^28)
-      const __amdgpu_buffer_rsrc_t rb =
-          __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(buf + c * n_node), 0, 0x80000000,
-                                            0x00020000);
-      const uint32_t off = (m & (1u << c)) ? g * 8u : 0x80000000u;
-      b[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rb, off, 0, CPOL_NT));
+  for (int c = 0; c < NS; ++c)
+    rb[c] = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(buf + c * n_node), 0, 0x80000000,
+                                              0x00020000);
+  for (int64_t b0 = (int64_t)blockIdx.x * (SEAM_ILP * BLOCK); b0 < n;
+       b0 += (int64_t)gridDim.x * (SEAM_ILP * BLOCK)) {
+    uint32_t g[SEAM_ILP], m[SEAM_ILP];
+#pragma unroll
+    for (int q = 0; q < SEAM_ILP; ++q) {
+      const int64_t i = b0 + q * BLOCK + threadIdx.x;
+      const bool in = i < n;
+      g[q] = in ? gid[i] : 0u;
+      m[q] = in ? (uint32_t)mask[i] : 0u;
     }
-    double s = y0;
-    bool first = !prior;
+    double y0[SEAM_ILP], b[SEAM_ILP][NS];
 #pragma unroll
-    for (int c = 0; c < NS; ++c)
-      if (m & (1u << c)) {
-        s = first ? b[c] : s + b[c];
-        first = false;
+    for (int q = 0; q < SEAM_ILP; ++q) {
+      const bool prior = m[q] && (accumulate || (m[q] & 0x100u));
+      y0[q] = prior ? y[g[q]] : 0.0;
+#pragma unroll
+      for (int c = 0; c < NS; ++c) {
+        const uint32_t off = (m[q] & (1u << c)) ? g[q] * 8u : 0x80000000u;
+        b[q][c] =
+            __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rb[c], off, 0, CPOL_NT));
       }
-    y[g] = s;
-    if constexpr (DOT) dotv = fma(du[g], s, dotv);
+    }
+#pragma unroll
+    for (int q = 0; q < SEAM_ILP; ++q) {
+      if (!m[q]) continue;  // past the end
+      const bool prior = accumulate || (m[q] & 0x100u);
+      double s = y0[q];
+      bool first = !prior;
+#pragma unroll
+      for (int c = 0; c < NS; ++c)
+        if (m[q] & (1u << c)) {
+          s = first ? b[q][c] : s + b[q][c];
+          first = false;
+        }
+      y[g[q]] = s;
+      if constexpr (DOT) dotv = fma(du[g[q]], s, dotv);
+    }
   }
   if constexpr (DOT) {
     __shared__ double sh[BLOCK / WAVE];
