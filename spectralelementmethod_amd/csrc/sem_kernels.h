@@ -1071,8 +1071,11 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
 // holds a value (SEM_NODE_PRIOR)
 // NS colours: the slot loads of a node are issued together (predicated
 // buffer loads: an unused slot reads past the range, 0 and no traffic).
+// nodes per thread per pass: 2 measured slower at p = 8 (41.5-41.8 against
+// 36.7-39.3 us per seam sum) and faster at p = 16 (10.0-10.2 against
+// 11.2-11.6), 4 no better (profiles/r03/knobs/seam_ilp.txt)
 #ifndef SEAM_ILP
-#define SEAM_ILP 2
+#define SEAM_ILP 1
 #endif
 template <int NS, bool DOT = false>
 __global__ void __launch_bounds__(BLOCK)
