@@ -246,10 +246,10 @@ def test_band_lu_solve_vs_spsolve():
     Aq = A[q][:, q]
     xq = band_lu_solve(Aq, b[q], dev)
     assert rel_l2(xq, ref[q]) < 1e-10
-    S = sparse.csr_matrix(A.toarray())
+    S = A.toarray()
     S[5, :] = 0.0
     S[:, 5] = 0.0
-    S.eliminate_zeros()
+    S = sparse.csr_matrix(S)
     from scipy.sparse.linalg import MatrixRankWarning
     with pytest.warns(MatrixRankWarning):
         xs = band_lu_solve(S, b, dev)
@@ -295,6 +295,67 @@ def test_static_condensation_nonsymmetric_device_solve():
     unk = ~on
     expect = soln.copy()
     expect[unk] = spla.spsolve(K[unk][:, unk].tocsc(), f[unk] - K[unk][:, ~unk] @ soln[~unk])
+    gsys = dm.init_global_linear_system()
+    dm.assemble_global_sc_system(gsys, local_systems)
+    dm.solve(gsys, local_systems, soln, on[:dm.ndof_exterior])
+    assert rel_l2(soln, expect) < 1e-10
+
+
+def test_axisym_stokes_condensed_solve_device():
+    """The Re = 0 squirmer block (E2e, Lve, Me of examples/squirmer-
+    axisymmetric.py:193-254, 278-295) condensed and solved through the
+    reference's SC API (sem/discrete.py:404-528): the condensed system is not
+    symmetric, so DOFManagerSC.solve takes the device banded LU.  Element
+    matrices come from the NumPy oracle's matrix-free block applied to unit
+    vectors; the solution with Dirichlet data on the whole boundary equals
+    the assembled global spsolve (the reference's solver) to 1e-10."""
+    import sem_oracle
+    from scipy import sparse
+    from scipy.sparse import linalg as spla
+    from spectralelementmethod_amd import meshgen
+    from spectralelementmethod_amd.basis_functions import gll_basis_2d
+    from spectralelementmethod_amd.discrete import DOFManagerSC, Mesh
+    p, nth, nr = 4, 7, 5
+    n, nn = p + 1, (p + 1) ** 2
+    nodes0, e2n0 = meshgen.annulus(nth, nr, p)
+    half = np.load(__import__("os").path.join(__import__("conftest").ROOT, "tests", "golden",
+                                               "gll.npz"))["half_%d" % p]
+    x1, bary, quad = sem_oracle.gll_unfold(half)
+    D = sem_oracle.diff_matrix(x1, bary)
+    _, lu = sem_oracle.interp_eq_lu(x1, bary)
+    xp, _, invJ, _, detJxW = sem_oracle.geometry(nodes0, e2n0.astype(np.int64), D, quad, lu,
+                                                 batched=True)
+    F = sem_oracle.axisym_factors(xp, invJ, detJxW)
+    E = e2n0.shape[0]
+    disj = np.arange(E * nn, dtype=np.int64).reshape(E, n, n)  # every element its own nodes
+    A = np.empty((E, 2 * nn, 2 * nn))
+    for k in range(2 * nn):
+        sol = np.zeros(2 * E * nn)
+        sol[k::2 * nn] = 1.0  # local DOF k (= 2 * node + comp) of every element
+        A[:, :, k] = sem_oracle.axisym_apply(F, D, disj, sol, E * nn).reshape(E, 2 * nn)
+    mesh = Mesh.from_arrays(nodes0, e2n0)
+    dm = DOFManagerSC(mesh, 2, gll_basis_2d(p))
+    local_systems, dofs = [], []
+    for e, fe in enumerate(dm.finite_elements()):
+        g = np.asarray(fe.node_ind, dtype=np.int64).ravel()
+        dofs.append((2 * g[:, None] + np.arange(2)[None, :]).ravel())
+        local_systems.append(dm.reorder_local_system_hier(fe, (A[e], np.zeros(2 * nn))))
+    ndof = dm.ndof
+    rows = np.concatenate([np.repeat(d, d.size) for d in dofs])
+    cols = np.concatenate([np.tile(d, d.size) for d in dofs])
+    K = sparse.coo_matrix((A.reshape(E, -1).ravel(), (rows, cols)), shape=(ndof, ndof)).tocsr()
+    rho, z = mesh.nodes
+    r, th = np.hypot(rho, z), np.arctan2(rho, z)
+    bnd = (np.abs(r - 1) < 1e-9) | (np.abs(r - 4) < 1e-9) | (np.abs(th - 0.05) < 1e-9) | \
+        (np.abs(th - (np.pi - 0.05)) < 1e-9)
+    on = np.repeat(bnd, 2)
+    soln = np.zeros(ndof)
+    soln[0::2][bnd] = 0.5 * rho[bnd] ** 2      # psi
+    soln[1::2][bnd] = 0.1 * z[bnd]             # omega
+    unk = ~on
+    expect = soln.copy()
+    expect[unk] = spla.spsolve(K[unk][:, unk].tocsc(), -K[unk][:, ~unk] @ soln[~unk])
+    assert not on[dm.ndof_exterior:].any()
     gsys = dm.init_global_linear_system()
     dm.assemble_global_sc_system(gsys, local_systems)
     dm.solve(gsys, local_systems, soln, on[:dm.ndof_exterior])
