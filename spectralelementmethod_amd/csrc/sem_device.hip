@@ -1100,6 +1100,20 @@ int sem_set_basis(sem_ctx* c, const double* hD, const double* hw) {
   if (!c || !hD || !hw) return fail(SEM_E_INVALID, "null argument");
   DeviceGuard g(c->device);
   const int n = c->n;
+  // the kernels use D in even-odd form and half of w: a node set symmetric
+  // about 0 (GLL), D[n-1-i][n-1-j] = -D[i][j] and w[n-1-i] = w[i]
+  double dmax = 0.0, wmax = 0.0, dasym = 0.0, wasym = 0.0;
+  for (int i = 0; i < n; ++i) {
+    wmax = std::max(wmax, std::fabs(hw[i]));
+    wasym = std::max(wasym, std::fabs(hw[i] - hw[n - 1 - i]));
+    for (int j = 0; j < n; ++j) {
+      dmax = std::max(dmax, std::fabs(hD[i * n + j]));
+      dasym = std::max(dasym, std::fabs(hD[i * n + j] + hD[(n - 1 - i) * n + (n - 1 - j)]));
+    }
+  }
+  if (!(dasym <= 1e-12 * dmax) || !(wasym <= 1e-14 * wmax))
+    return fail(SEM_E_INVALID,
+                "sem_set_basis: D and w must come from a node set symmetric about 0 (GLL)");
   std::memcpy(c->hD, hD, sizeof(double) * n * n);
   std::memcpy(c->hw, hw, sizeof(double) * n);
   HIP_TRY(hipMemcpy(c->d_D, hD, sizeof(double) * n * n, hipMemcpyHostToDevice));
