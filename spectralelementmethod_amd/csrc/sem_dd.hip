@@ -23,6 +23,8 @@
 //   main:  ev0 ------------- interior apply (u -> y) ------------- wait ev1, y[cidx] += y_c
 //   side:  wait ev0, u_c = u[cidx], iface apply (u_c -> y_c), pack, exchange, unpack, ev1
 #include <hip/hip_runtime.h>
+
+#include <limits>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -128,20 +130,48 @@ __global__ void k_cg_invert(double* __restrict__ d, const uint8_t* __restrict__ 
     d[t] = (f[t] & F_DIR) ? 0.0 : 1.0 / d[t];
 }
 
-// r = b - K x on free DOFs (r holds K x on entry), p = z = r / diag;
+// The Jacobi preconditioner as the vector passes read it (SEM_PCG_DINV32,
+// default): 1 / diag rounded to float, with the DOF flags folded in -- 0 on
+// Dirichlet DOFs, negative on DOFs another rank owns (left out of the dots):
+// 4 bytes per DOF and pass instead of 8 + 1.  M = diag(float(1 / diag)) is
+// still symmetric positive definite, so CG converges to the same solution;
+// the iterates are those of that M.
+#ifndef SEM_PCG_DINV32
+#define SEM_PCG_DINV32 1
+#endif
+#if SEM_PCG_DINV32
+typedef float dinv_t;
+#else
+typedef double dinv_t;
+#endif
+__device__ __forceinline__ bool pc_dir(dinv_t d) { return d == (dinv_t)0; }
+__device__ __forceinline__ bool pc_own(dinv_t d) { return d >= (dinv_t)0; }
+__device__ __forceinline__ double pc_z(double r, dinv_t d) { return r * (double)fabs(d); }
+
+__global__ void k_cg_pack(const double* __restrict__ dinv, const uint8_t* __restrict__ f,
+                          int64_t n, dinv_t* __restrict__ out) {
+  for (int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x; t < n; t += (int64_t)gridDim.x * BLK) {
+    dinv_t v = (dinv_t)fabs(dinv[t]);
+    if (v == (dinv_t)0 || !(v == v)) v = std::numeric_limits<dinv_t>::min();  // free DOF: never 0
+    if (f[t] & F_DIR) v = (dinv_t)0;
+    else if (f[t] & F_NOTOWN) v = -v;
+    out[t] = v;
+  }
+}
+
+// r = b - K x on free DOFs (r holds K x on entry), p = z = M r;
 // partial sums of r.z and r.r over owned DOFs
 __global__ void __launch_bounds__(BLK)
-    k_cg_start(const double* __restrict__ b, double* __restrict__ r, const double* __restrict__ dinv,
-               const uint8_t* __restrict__ f, int64_t n, double* __restrict__ p,
-               double* __restrict__ partial) {
+    k_cg_start(const double* __restrict__ b, double* __restrict__ r, const dinv_t* __restrict__ dinv,
+               int64_t n, double* __restrict__ p, double* __restrict__ partial) {
   double s0 = 0.0, s1 = 0.0;
   for (int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x; t < n; t += (int64_t)gridDim.x * BLK) {
-    const uint8_t ft = f[t];
-    const double rt = (ft & F_DIR) ? 0.0 : b[t] - r[t];
-    const double zt = rt * dinv[t];
+    const dinv_t dt = dinv[t];
+    const double rt = pc_dir(dt) ? 0.0 : b[t] - r[t];
+    const double zt = pc_z(rt, dt);
     r[t] = rt;
     p[t] = zt;
-    if (!(ft & F_NOTOWN)) {
+    if (pc_own(dt)) {
       s0 = fma(rt, zt, s0);
       s1 = fma(rt, rt, s1);
     }
@@ -162,6 +192,11 @@ template <int V>
 __device__ __forceinline__ void stv(double* __restrict__ a, int64_t i, const double (&o)[V]) {
 #pragma unroll
   for (int e = 0; e < V; ++e) __builtin_nontemporal_store(o[e], a + i * V + e);
+}
+template <int V>
+__device__ __forceinline__ void ldv(const float* __restrict__ a, int64_t i, float (&o)[V]) {
+#pragma unroll
+  for (int e = 0; e < V; ++e) o[e] = __builtin_nontemporal_load(a + i * V + e);
 }
 template <int V>
 __device__ __forceinline__ void ldf(const uint8_t* __restrict__ f, int64_t i, uint8_t (&o)[V]) {
@@ -219,42 +254,40 @@ __device__ __forceinline__ double cg_alpha(const double* rz_old, const double* p
 template <int V>
 __global__ void __launch_bounds__(BLK)
     k_cg_residual(double* __restrict__ r, const double* __restrict__ q,
-                  const double* __restrict__ dinv, const uint8_t* __restrict__ f,
-                  const double* __restrict__ rz_old, const double* __restrict__ pq, int64_t n,
-                  double* __restrict__ partial) {
+                  const dinv_t* __restrict__ dinv, const double* __restrict__ rz_old,
+                  const double* __restrict__ pq, int64_t n, double* __restrict__ partial) {
   constexpr int U = UNR / V;
   const double alpha = cg_alpha(rz_old, pq);
   double s0 = 0.0, s1 = 0.0;
-  auto one = [&](double qt, double rt, double dt, uint8_t ft) {
-    rt = (ft & F_DIR) ? 0.0 : fma(-alpha, qt, rt);
-    if (!(ft & F_NOTOWN)) {
-      s0 = fma(rt, rt * dt, s0);
+  auto one = [&](double qt, double rt, dinv_t dt) {
+    rt = pc_dir(dt) ? 0.0 : fma(-alpha, qt, rt);
+    if (pc_own(dt)) {
+      s0 = fma(rt, pc_z(rt, dt), s0);
       s1 = fma(rt, rt, s1);
     }
     return rt;
   };
   const int64_t nv = n / V, st = (int64_t)gridDim.x * BLK;
   for (int64_t i0 = blockIdx.x * (int64_t)BLK + threadIdx.x; i0 < nv; i0 += U * st) {
-    double qv[U][V], rv[U][V], dv[U][V];
-    uint8_t fv[U][V];
+    double qv[U][V], rv[U][V];
+    dinv_t dv[U][V];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t i = i0 + u * st < nv ? i0 + u * st : 0;
       ldv<V>(q, i, qv[u]);
       ldv<V>(r, i, rv[u]);
       ldv<V>(dinv, i, dv[u]);
-      ldf<V>(f, i, fv[u]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (i0 + u * st >= nv) continue;
 #pragma unroll
-      for (int e = 0; e < V; ++e) rv[u][e] = one(qv[u][e], rv[u][e], dv[u][e], fv[u][e]);
+      for (int e = 0; e < V; ++e) rv[u][e] = one(qv[u][e], rv[u][e], dv[u][e]);
       stv<V>(r, i0 + u * st, rv[u]);
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0)
-    for (int64_t t = nv * V; t < n; ++t) r[t] = one(q[t], r[t], dinv[t], f[t]);
+    for (int64_t t = nv * V; t < n; ++t) r[t] = one(q[t], r[t], dinv[t]);
   write_partials(s0, s1, partial);
 }
 
@@ -264,7 +297,7 @@ __global__ void __launch_bounds__(BLK)
 template <int V>
 __global__ void __launch_bounds__(BLK)
     k_cg_step(double* __restrict__ x, double* __restrict__ p, const double* __restrict__ r,
-              const double* __restrict__ dinv, const double* __restrict__ rz_new,
+              const dinv_t* __restrict__ dinv, const double* __restrict__ rz_new,
               const double* __restrict__ rz_old, const double* __restrict__ pq, int64_t n) {
   constexpr int U = UNR / V;
   const double alpha = cg_alpha(rz_old, pq);
@@ -272,7 +305,8 @@ __global__ void __launch_bounds__(BLK)
   const double beta = den != 0.0 ? *rz_new / den : 0.0;
   const int64_t nv = n / V, st = (int64_t)gridDim.x * BLK;
   for (int64_t i0 = blockIdx.x * (int64_t)BLK + threadIdx.x; i0 < nv; i0 += U * st) {
-    double xv[U][V], pv[U][V], rv[U][V], dv[U][V];
+    double xv[U][V], pv[U][V], rv[U][V];
+    dinv_t dv[U][V];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t i = i0 + u * st < nv ? i0 + u * st : 0;
@@ -287,7 +321,7 @@ __global__ void __launch_bounds__(BLK)
 #pragma unroll
       for (int e = 0; e < V; ++e) {
         xv[u][e] = fma(alpha, pv[u][e], xv[u][e]);
-        pv[u][e] = fma(beta, pv[u][e], rv[u][e] * dv[u][e]);
+        pv[u][e] = fma(beta, pv[u][e], pc_z(rv[u][e], dv[u][e]));
       }
       stv<V>(x, i0 + u * st, xv[u]);
       stv<V>(p, i0 + u * st, pv[u]);
@@ -296,7 +330,7 @@ __global__ void __launch_bounds__(BLK)
   if (blockIdx.x == 0 && threadIdx.x == 0)
     for (int64_t t = nv * V; t < n; ++t) {
       x[t] = fma(alpha, p[t], x[t]);
-      p[t] = fma(beta, p[t], r[t] * dinv[t]);
+      p[t] = fma(beta, p[t], pc_z(r[t], dinv[t]));
     }
 }
 
@@ -614,12 +648,14 @@ struct PcgOp {
 
 struct PcgScratch {
   double* base = nullptr;
+  dinv_t* pc = nullptr;  // the packed preconditioner (k_cg_pack)
   uint8_t* flags = nullptr;
   double* red = nullptr;
   double* hist = nullptr;
   double* h_hist = nullptr;  // pinned
   ~PcgScratch() {
     (void)hipFree(base);
+    (void)hipFree(pc);
     (void)hipFree(flags);
     (void)hipFree(red);
     (void)hipFree(hist);
@@ -646,6 +682,7 @@ int pcg_run(const PcgOp& op, int kind, const double* b, double* x, const uint8_t
   const int64_t nn = (n + 31) / 32 * 32;
   HIP_TRY(hipMalloc(&s.base, 4 * nn * sizeof(double)));
   HIP_TRY(hipMalloc(&s.flags, n));
+  HIP_TRY(hipMalloc(&s.pc, nn * sizeof(dinv_t)));
   // partials [2][RED_BLOCKS], then scalars: T0 = (rz, rr), T1 = (rz, rr), pq
   HIP_TRY(hipMalloc(&s.red, (2 * RED_BLOCKS + 8) * sizeof(double)));
   HIP_TRY(hipMalloc(&s.hist, ((size_t)max_iter + 1) * sizeof(double)));
@@ -664,8 +701,9 @@ int pcg_run(const PcgOp& op, int kind, const double* b, double* x, const uint8_t
   hipLaunchKernelGGL(k_cg_flags, dim3(grid_for(n)), dim3(BLK), 0, st, dir, notown, n, s.flags);
   SEM_TRY(op.diag(kind, dg, st));
   hipLaunchKernelGGL(k_cg_invert, dim3(grid_for(n)), dim3(BLK), 0, st, dg, s.flags, n);
+  hipLaunchKernelGGL(k_cg_pack, dim3(grid_for(n)), dim3(BLK), 0, st, dg, s.flags, n, s.pc);
   SEM_TRY(op.apply(kind, x, r, st));
-  hipLaunchKernelGGL(k_cg_start, dim3(gb), dim3(BLK), 0, st, b, r, dg, s.flags, n, p, partial);
+  hipLaunchKernelGGL(k_cg_start, dim3(gb), dim3(BLK), 0, st, b, r, s.pc, n, p, partial);
   hipLaunchKernelGGL(k_cg_finish, dim3(1), dim3(BLK), 0, st, partial, gb, 2, T[0], nullptr);
   HIP_TRY(hipGetLastError());
   SEM_TRY(dd_allreduce(op.dd, T[0], 2, st));
@@ -691,8 +729,8 @@ int pcg_run(const PcgOp& op, int kind, const double* b, double* x, const uint8_t
         hipLaunchKernelGGL(k_cg_finish, dim3(1), dim3(BLK), 0, st, partial, gb, 1, pq, nullptr);
         SEM_TRY(dd_allreduce(op.dd, pq, 1, st));
       }
-      hipLaunchKernelGGL(k_cg_residual<2>, dim3(gb), dim3(BLK), 0, st, r, q, dg, s.flags, T[o],
-                         pq, n, partial);
+      hipLaunchKernelGGL(k_cg_residual<2>, dim3(gb), dim3(BLK), 0, st, r, q, s.pc, T[o], pq, n,
+                         partial);
       hipLaunchKernelGGL(k_cg_finish, dim3(1), dim3(BLK), 0, st, partial, gb, 2, T[nw],
                          multi ? nullptr : s.hist + it + 1);
       if (multi) {
@@ -700,10 +738,10 @@ int pcg_run(const PcgOp& op, int kind, const double* b, double* x, const uint8_t
         hipLaunchKernelGGL(k_cg_record, dim3(1), dim3(WV), 0, st, T[nw] + 1, s.hist + it + 1);
       }
       if (v2)
-        hipLaunchKernelGGL(k_cg_step<2>, dim3(gb), dim3(BLK), 0, st, x, p, r, dg, T[nw], T[o], pq,
+        hipLaunchKernelGGL(k_cg_step<2>, dim3(gb), dim3(BLK), 0, st, x, p, r, s.pc, T[nw], T[o], pq,
                            n);
       else
-        hipLaunchKernelGGL(k_cg_step<1>, dim3(gb), dim3(BLK), 0, st, x, p, r, dg, T[nw], T[o], pq,
+        hipLaunchKernelGGL(k_cg_step<1>, dim3(gb), dim3(BLK), 0, st, x, p, r, s.pc, T[nw], T[o], pq,
                            n);
       HIP_TRY(hipGetLastError());
       if (g_sync_each) HIP_TRY(hipDeviceSynchronize());  // diagnostic

@@ -978,11 +978,18 @@ __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nwg) {
 // minimum waves per SIMD requested from the register allocator.  p = 8
 // nodal: 4 (128 VGPRs, no spill; the unpadded tiles fit 4 workgroups per CU)
 // measured 0.709 vs 0.731 ms at 3 waves (profiles/r01/occupancy).
-template <int N, bool NODAL>
+// p = 14 stored, seam plan: a 5-wave request (the allocator lands at 3
+// waves with a different schedule) measured 0.128-0.129 against 0.135 ms
+// per action at 227^2 (natural 4 waves) and 0.132 (3); the same request at
+// p = 10 / 12 is 13 % / 40 % slower (profiles/r03/knobs/min_waves/), and it
+// would push the colour-launch and fused-dot forms of p = 14 to 2 waves
+// (247 / 171 VGPRs), so it applies to the seam form only
+template <int N, bool NODAL, bool SEAM = false, bool DOT = false>
 struct PoissonMinWaves {
-  static constexpr int value = SEM_POISSON_MIN_WAVES > 0 ? SEM_POISSON_MIN_WAVES
-                               : (NODAL && N == 9)      ? 4
-                                                        : 1;
+  static constexpr int value = SEM_POISSON_MIN_WAVES > 0             ? SEM_POISSON_MIN_WAVES
+                               : (NODAL && N == 9)                   ? 4
+                               : (!NODAL && N == 15 && SEAM && !DOT) ? 5
+                                                                     : 1;
 };
 
 struct SeamPlan {
@@ -1009,7 +1016,7 @@ __device__ __forceinline__ double block_sum_fixed(double v, double* sh) {
 }
 
 template <int N, bool NODAL, bool M16, bool SEAM = false, bool DOT = false>
-__global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODAL>::value))
+__global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODAL, SEAM, DOT>::value))
     k_poisson_apply(const MapRef mref, const double* __restrict__ GP,
                     const double2* __restrict__ XG, const double* __restrict__ u,
                     double* __restrict__ y, int64_t c0, int64_t c1, int rounds, int accumulate,
