@@ -462,6 +462,20 @@ class DOFManager(object):
         raise NotImplementedError("point location (sem/discrete.py:263-280) is out of scope")
 
 
+def band_order(A):
+    """Reverse Cuthill-McKee order of a square sparse matrix (on the
+    symmetrised pattern) and its lower / upper bandwidths in that order:
+    (perm, A[perm][:, perm] as CSR, kl, ku)."""
+    from scipy.sparse.csgraph import reverse_cuthill_mckee
+    A = sparse.csr_matrix(A)
+    pat = (abs(A) + abs(A.T)).tocsr()
+    perm = np.asarray(reverse_cuthill_mckee(pat, symmetric_mode=True), dtype=np.int64)
+    Ap = A[perm][:, perm].tocoo()
+    kl = int(max(0, (Ap.row - Ap.col).max(initial=0)))
+    ku = int(max(0, (Ap.col - Ap.row).max(initial=0)))
+    return perm, Ap.tocsr(), kl, ku
+
+
 def band_lu_solve(A, b, device):
     """x = A^-1 b for a square sparse matrix on the device: reverse
     Cuthill-McKee order (host, scipy.sparse.csgraph, as the reference orders
@@ -472,20 +486,14 @@ def band_lu_solve(A, b, device):
     import ctypes as C
     import warnings
     import torch
-    from scipy.sparse.csgraph import reverse_cuthill_mckee
     from . import _lib
     A = sparse.csr_matrix(A)
     n = A.shape[0]
     if n == 0:
         return np.zeros(0)
-    pat = (abs(A) + abs(A.T)).tocsr()
-    perm = np.asarray(reverse_cuthill_mckee(pat, symmetric_mode=True), dtype=np.int64)
-    Ap = A[perm][:, perm].tocoo()
-    kl = int(max(0, (Ap.row - Ap.col).max(initial=0)))
-    ku = int(max(0, (Ap.col - Ap.row).max(initial=0)))
+    perm, Ap, kl, ku = band_order(A)
     if kl >= 1024:
         raise NotImplementedError("band_lu_solve: lower bandwidth %d after RCM (limit 1023)" % kl)
-    Ap = Ap.tocsr()
     lib = _lib.load()
     rp = torch.from_numpy(Ap.indptr.astype(np.int64)).to(device)
     ci = torch.from_numpy(Ap.indices.astype(np.int32)).to(device)
