@@ -984,11 +984,17 @@ __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nwg) {
 // p = 10 / 12 is 13 % / 40 % slower (profiles/r03/knobs/min_waves/), and it
 // would push the colour-launch and fused-dot forms of p = 14 to 2 waves
 // (247 / 171 VGPRs), so it applies to the seam form only
+// p = 4 nodal colour launches (the instantiation AUTO runs on the cfg4
+// mesh): a 6-wave request (98 -> 80 VGPRs, 4 -> 6 waves) measured 0.103-0.105
+// against 0.116-0.119 ms per action (call AC, two runs alternating,
+// profiles/r03/knobs/min_waves_low/); requests at p = 2 / 6 leave their
+// AUTO instantiations' code unchanged, and cfg2 (p = 8 seams) keeps 4.
 template <int N, bool NODAL, bool SEAM = false, bool DOT = false>
 struct PoissonMinWaves {
   static constexpr int value = SEM_POISSON_MIN_WAVES > 0             ? SEM_POISSON_MIN_WAVES
                                : (NODAL && N == 9)                   ? 4
                                : (!NODAL && N == 15 && SEAM && !DOT) ? 5
+                               : (NODAL && N == 5 && !SEAM && !DOT)  ? 6
                                                                      : 1;
 };
 
