@@ -54,6 +54,7 @@ def build(force=False, verbose=True, out=None, defines=(), orders=None):
     os.makedirs(objdir, exist_ok=True)
     common = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17",
               "-munsafe-fp-atomics", "-Wall", "-Wno-unused-result",
+              "-Wno-pass-failed",  # occupancy requests the allocator meets lower (PoissonMinWaves)
               *["-D" + d for d in defines]]
     units = [(s, [], os.path.join(objdir, s + ".o")) for s in SOURCES]
     ranges = [orders] if orders else LAUNCH_RANGES
