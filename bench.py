@@ -301,6 +301,55 @@ def parity_spot_check(op, y, u, part, p, warp, cols=2):
     return out
 
 
+def global_field_at(part, gids, dev):
+    """u at arbitrary GLOBAL node ids (e.g. a neighbour's nodes next to the
+    interface): the global field of global_random_field regenerated chunk by
+    chunk on the device (the same Philox stream), entries picked."""
+    import torch
+    g = torch.Generator(device=dev).manual_seed(1234)
+    gids = torch_index(gids, dev)
+    out = torch.empty(gids.numel(), dtype=torch.float64, device=dev)
+    chunk, pos, n_glob = 1 << 24, 0, part.global_nodes
+    while pos < n_glob:
+        m = min(chunk, n_glob - pos)
+        v = torch.randn(m, dtype=torch.float64, device=dev, generator=g)
+        sel = (gids >= pos) & (gids < pos + m)
+        out[sel] = v[gids[sel] - pos]
+        pos += m
+    return out
+
+
+def parity_interface_check(y, part, p, warp, dev):
+    """The interface sum, checked against the oracle: the two element columns
+    on either side of this rank's right interface, [ex1 - 1, ex1 + 1),
+    recomputed by the NumPy oracle (u of the neighbour's column regenerated
+    from the global field) and compared on this rank's own inner nodes of the
+    block -- node lines (ex1 - 1) p + 1 .. ex1 p, the last one being the
+    shared line whose value this rank only has after the exchange."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import sem_oracle
+    from spectralelementmethod_amd import meshgen
+    if part.rank == part.world - 1:
+        return None
+    gll = np.load(os.path.join(ROOT, "tests", "golden", "gll.npz"))
+    c0 = part.ex1 - 1
+    nodes, e2n, off = meshgen.structured_strip(part.nex, part.ney, p, c0, c0 + 2, warp)
+    gids = off + np.arange(nodes.shape[1])
+    u_sub = global_field_at(part, gids, dev).cpu().numpy()
+    y_ref = sem_oracle.PoissonProblem(nodes, e2n, gll["half_%d" % p],
+                                      batched_geometry=True).apply(u_sub)
+    Ny = part.Ny
+    own = np.arange(Ny, (p + 1) * Ny)  # block node lines 1 .. p
+    loc = gids[own] - part.node_offset
+    y_gpu = y[torch_index(loc, y.device)].cpu().numpy()
+    ref = y_ref[own]
+    return dict(rel_l2=float(np.linalg.norm(y_gpu - ref) / np.linalg.norm(ref)),
+                nodes_checked=int(own.size), interface_nodes=int(Ny),
+                block="element columns [%d, %d) x %d rows across the interface with rank %d" % (
+                    c0, c0 + 2, part.ney, part.rank + 1),
+                against="float64 NumPy oracle of the reference path")
+
+
 def torch_index(a, device):
     import torch
     return torch.from_numpy(np.asarray(a, dtype=np.int64)).to(device)
@@ -345,6 +394,13 @@ def main():
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="diagnostic: every rank on cuda:0, gloo process group, torch transport "
                          "(exercises the multi-rank flow on a one-GPU box; timings meaningless)")
+    ap.add_argument("--time-rank", type=int, default=None, metavar="R",
+                    help="diagnostic: time rank R of the --gpus N strip decomposition ALONE on "
+                         "this GPU (loopback transport: the exchange returns the rank's own "
+                         "values; kernels, streams and host enqueue of the real step)")
+    ap.add_argument("--dump-interface", default=None, metavar="DIR",
+                    help="test hook: every rank writes y at its interface node lines (global "
+                         "ids, values) to DIR/iface_rank<r>.npz after the timed steps")
     ap.add_argument("--traffic-json", default=None,
                     help="JSON with PMC-measured HBM bytes per launch (profiles/)")
     args = ap.parse_args()
@@ -352,6 +408,8 @@ def main():
     if args.cpu_baseline_only:  # child process: no GPU
         print(json.dumps(cpu_baseline(args.p, args.warp, args.cpu_budget, args.cpu_workers)))
         return 0
+    if args.time_rank is not None:
+        return time_rank(args)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return launch_ranks(args.gpus, args.deadline)
 
@@ -461,7 +519,7 @@ def main():
         per_rank_ms = gathered
     kern_avg_s = float(np.mean(kern_ms)) / 1e3
 
-    parity = None
+    parity, parity_ranks, parity_iface = None, None, None
     if not args.no_check:
         assert torch.isfinite(y).all().item(), "non-finite output"
         if kind == POISSON:
@@ -469,6 +527,21 @@ def main():
             parity["tolerance"] = 1e-10
             log("rank %d: parity spot check %s" % (rank, parity))
             assert parity["rel_l2"] < parity["tolerance"], parity
+            iface = parity_interface_check(y, part, p, args.warp, dev) if world > 1 else None
+            if iface is not None:
+                iface["tolerance"] = 1e-10
+                log("rank %d: interface parity %s" % (rank, iface))
+                assert iface["rel_l2"] < iface["tolerance"], iface
+            if world > 1:
+                parity_ranks = [None] * world
+                dist.all_gather_object(parity_ranks, parity["rel_l2"])
+                parity_iface = [None] * world
+                dist.all_gather_object(parity_iface, None if iface is None else iface["rel_l2"])
+    if args.dump_interface and kind == POISSON:
+        lines = [k for k in sorted(part.neighbors)]
+        loc = np.concatenate([part.neighbors[k] for k in lines]) if lines else np.zeros(0, int)
+        np.savez(os.path.join(args.dump_interface, "iface_rank%d.npz" % rank),
+                 gid=part.node_offset + loc, y=y[torch_index(loc, dev)].cpu().numpy())
 
     value = ndof_global * args.steps / elapsed
     map_bytes = plan.get("map_entry_bytes", 4) if (
@@ -518,6 +591,9 @@ def main():
             "exchange_bytes_per_step_per_rank": 2 * op.exchange_bytes,
             "interface_elements": op.n_iface_elem,
             "kernel_ms_avg": kern_avg_s * 1e3, "kernel_ms_min": float(np.min(kern_ms)),
+            "kernel_ms_note": "avg = mean of the timed actions' HIP-event times, including the "
+                              "shader-clock ramp of the first actions (it must match the "
+                              "rocprofv3 average); the median is kernel_ms_quartiles[1]",
             "kernel_ms_quartiles": [float(q) for q in np.percentile(kern_ms, [25, 50, 75])],
             "kernel_ms_max": float(np.max(kern_ms)),
             "host_enqueue_ms_per_step": t_enqueue / args.steps * 1e3,
@@ -551,6 +627,9 @@ def main():
     }
     if parity is not None:
         result["parity"] = parity
+    if parity_ranks is not None:
+        result["parity_per_rank"] = parity_ranks
+        result["parity_interface_per_rank"] = parity_iface
     if rank == 0 and world == 1 and not args.no_cpu_baseline and kind == POISSON:
         log("timing CPU baseline (NumPy oracle of the reference path, child process)...")
         env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1",
@@ -582,6 +661,131 @@ def main():
     op.close()
     if world > 1:
         dist.destroy_process_group()
+    return 0
+
+
+def time_rank(args):
+    """One rank of the N-strip decomposition of the nex x ney mesh, alone on
+    this GPU (sem_dd_set_loopback: every exchange copies the rank's own send
+    buffer into its receive buffer -- the kernels, streams and host enqueue of
+    the real step, the values are NOT the global action).  Reports the step
+    (wall clock and HIP events on the caller's stream), the interior elements
+    alone, the side-stream chain alone (gather, interface elements, pack),
+    the exposed time of the side stream and the finish, the host enqueue split
+    by sem_dd_info, and the single-GPU step of the whole mesh on the same box:
+    strong scaling to N GPUs at >= S x needs the rank's step <= T_1 / S."""
+    import torch
+    from spectralelementmethod_amd import _lib
+    from spectralelementmethod_amd.distributed import StripPartition, OverlappedOperator
+    N, R, p = args.gpus, args.time_rank, args.p
+    if not (0 <= R < N):
+        raise SystemExit("--time-rank needs 0 <= R < --gpus")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    part = StripPartition(args.nex, args.ney, p, N, R)
+    nodes, e2n = part.local_mesh(args.warp)
+    op = OverlappedOperator(p, nodes, e2n, part.neighbors, 1, dev, owned=part.owned,
+                            transport="loopback", world=1, rank=0, decompose=True)
+    del nodes, e2n
+    u = global_random_field(part, 1, 0, op.ndof, dev)
+    y = torch.empty_like(u)
+    lib = _lib.load()
+    main = torch.cuda.current_stream(dev)
+    sp = _lib.stream_ptr(main)
+
+    def timed(fn, steps, warmup):
+        for _ in range(warmup):
+            fn()
+        torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(steps)]
+        t0 = time.perf_counter()
+        for a, b in ev:
+            a.record(main)
+            fn()
+            b.record(main)
+        t_enq = time.perf_counter() - t0
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        ms = [a.elapsed_time(b) for a, b in ev]
+        return dict(wall_ms_per_step=wall / steps * 1e3, event_ms_avg=float(np.mean(ms)),
+                    event_ms_quartiles=[float(q) for q in np.percentile(ms, [25, 50, 75])],
+                    host_enqueue_ms_per_step=t_enq / steps * 1e3)
+
+    K, W = args.steps, args.warmup
+    i0 = op.dd_info()
+    step = timed(lambda: op.step(u, y), K, W)
+    i1 = op.dd_info()
+    n_app = i1["applies"] - i0["applies"]
+    d_us = {k: (i1[k] - i0[k]) / n_app / 1e3 for k in
+            ("host_ns", "host_ns_transport", "host_ns_side", "host_ns_interior", "host_ns_finish")}
+    host_split = dict(host_us_per_apply=d_us["host_ns"],
+                      host_us_per_apply_excl_transport=d_us["host_ns"] - d_us["host_ns_transport"],
+                      host_us_transport=d_us["host_ns_transport"],
+                      host_us_side=d_us["host_ns_side"], host_us_interior=d_us["host_ns_interior"],
+                      host_us_finish=d_us["host_ns_finish"])
+    # the interior elements alone, as sem_dd_apply launches them
+    flags = 2 if i1["zero_list_in_finish"] else 0  # SEM_APPLY_SKIP_ZERO
+    interior = None
+    if op.interior is not None:
+        interior = timed(lambda: _lib.check(lib.sem_apply(op.interior._ctx, 0, _lib.tptr(u),
+                                                          _lib.tptr(y), flags, sp)), K, W)
+    # the side-stream chain alone (on the caller's stream here)
+    side = None
+    if op.iface is not None:
+        pl = op.plan
+        cidx = torch.from_numpy(pl.iface_dofs.view(np.int32)).to(dev)
+        pidx = torch.from_numpy(pl.peer_dofs.view(np.int32)).to(dev)
+        uc = torch.empty(cidx.numel(), dtype=torch.float64, device=dev)
+        yc = torch.empty_like(uc)
+        send = torch.empty(max(1, pidx.numel()), dtype=torch.float64, device=dev)
+
+        def side_chain():
+            _lib.check(lib.sem_gather(_lib.tptr(u), _lib.tptr(cidx), cidx.numel(), _lib.tptr(uc),
+                                      sp))
+            _lib.check(lib.sem_apply(op.iface._ctx, 0, _lib.tptr(uc), _lib.tptr(yc), 0, sp))
+            _lib.check(lib.sem_gather(_lib.tptr(yc), _lib.tptr(pidx), pidx.numel(),
+                                      _lib.tptr(send), sp))
+        side = timed(side_chain, K, W)
+    iface_elems, interior_elems = op.n_iface_elem, op.n_interior_elem
+    plan_int = op.interior.plan_info() if op.interior is not None else None
+    plan_if = op.iface.plan_info() if op.iface is not None else None
+    ndof = op.ndof
+    op.close()
+    del op, u, y
+    torch.cuda.empty_cache()
+    # the single-GPU step of the whole mesh on this box (the strong-scaling base)
+    single = None
+    if not args.no_check:
+        full = StripPartition(args.nex, args.ney, p, 1, 0)
+        nodes, e2n = full.local_mesh(args.warp)
+        op1 = OverlappedOperator(p, nodes, e2n, {}, 1, dev, world=1, rank=0)
+        del nodes, e2n
+        u1 = global_random_field(full, 1, 0, op1.ndof, dev)
+        y1 = torch.empty_like(u1)
+        single = timed(lambda: op1.step(u1, y1), K, W)
+        op1.close()
+    step_ms = step["wall_ms_per_step"]
+    res = {
+        "mode": "time-rank (loopback transport: the exchange returns this rank's own values; "
+                "timing only, the result is NOT the global action)",
+        "rank": R, "of_ranks": N, "p": p, "mesh": "%dx%d" % (args.nex, args.ney),
+        "strip_elements": "%d x %d" % (part.ex1 - part.ex0, part.ney), "ndof_rank": ndof,
+        "peers": sorted(part.neighbors), "interface_elements": iface_elems,
+        "interior_elements": interior_elems, "steps": K, "warmup": W,
+        "step": step, "interior_alone": interior, "side_chain_alone": side,
+        "exposed_beyond_interior_ms": (step["event_ms_avg"] - interior["event_ms_avg"])
+        if interior else None,
+        "host": host_split, "plan_interior": plan_int, "plan_iface": plan_if,
+        "single_gpu_whole_mesh": single,
+    }
+    if single is not None:
+        t1 = single["wall_ms_per_step"]
+        for S in (6, 7, N):
+            res["budget_ms_for_%dx" % S] = t1 / S
+        res["fits_6x"] = step_ms <= t1 / 6
+        res["projected_speedup_if_ranks_equal"] = t1 / step_ms
+    print(json.dumps(res), file=JSON_OUT, flush=True)
     return 0
 
 

@@ -346,7 +346,8 @@ int sem_csr_pcg_solve(int64_t n, const int64_t* d_rowptr, const int32_t* d_colin
  * Navier-Stokes block; scipy.sparse.linalg.spsolve in the reference,
  * sem/discrete.py:502-511).  kl / ku: lower / upper bandwidth of A as
  * ordered by the caller (reverse Cuthill-McKee, as the reference orders its
- * nodes); kl < 1024.  Duplicate entries are summed.  Band storage
+ * nodes); any kl (the multipliers are kept in the band, LAPACK's
+ * in-place L).  Duplicate entries are summed.  Band storage
  * n (2 kl + ku + 1) doubles, allocated on the stream.  *info = 0 on
  * success, j + 1 when column j has an exactly zero pivot (A singular; x is
  * then not written), as LAPACK gbsv.  Synchronises the stream. */
@@ -405,16 +406,27 @@ typedef int (*sem_allreduce_fn)(void* user, double* d_buf, int count, void* stre
 int sem_dd_set_transport(sem_dd* dd, sem_exchange_fn exchange, sem_allreduce_fn allreduce,
                          void* user, int world, int rank);
 
+/* Transport, diagnostic loopback: every exchange copies this rank's own send
+ * buffer into its receive buffer (one kernel on the side stream, the bytes
+ * RCCL's send/recv would move), every all-reduce is the identity, world 1.
+ * Times ONE rank of a decomposition alone on one GPU (bench.py --time-rank):
+ * the kernels, streams and host enqueue of the real step, values NOT the
+ * global action. */
+int sem_dd_set_loopback(sem_dd* dd);
+
 /* hipMemcpyAsync(dst, src, nbytes, hipMemcpyDefault, stream): lets a
  * caller-supplied transport stage the library's device buffers. */
 int sem_copy_async(void* dst, const void* src, int64_t nbytes, void* stream);
 
 /* info[0] ndof_local, [1] n_iface_dofs, [2] peers, [3] exchanged values per
- * direction, [4] transport (0 none, 1 RCCL, 2 callbacks), [5] has interior,
- * [6] captured step on (sem_dd_set_graphs), [7] captures, [8] replays,
- * [9] sem_dd_apply calls, [10] host nanoseconds spent in them, [11] of which
- * inside the transport call (a caller transport that synchronises with the
- * device makes [11] the device time up to the exchange). */
+ * direction, [4] transport (0 none, 1 RCCL, 2 callbacks, 3 loopback),
+ * [5] has interior, [6] captured step on (sem_dd_set_graphs), [7] captures,
+ * [8] replays, [9] sem_dd_apply calls, [10] host nanoseconds spent in them,
+ * [11] of which inside the transport call (a caller transport that
+ * synchronises with the device makes [11] the device time up to the
+ * exchange), eager steps only: [12] enqueueing the side-stream part (gather,
+ * interface elements, pack), [13] the interior elements, [14] the finish;
+ * [15] the interior's zero list folded into the finish. */
 int sem_dd_info(sem_dd* dd, int64_t* info, int n_info);
 
 /* Captured step (default off; SEM_DD_GRAPH=1 in the environment turns it

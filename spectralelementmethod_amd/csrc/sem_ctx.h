@@ -116,6 +116,9 @@ struct sem_ctx {
   uint32_t* d_seam_gid = nullptr;
   uint16_t* d_seam_mask = nullptr;
   double* d_seam_buf = nullptr;
+  uint64_t epoch = 0;      // sem::ctx_epoch
+  uint64_t map_epoch = 0;  // sem::ctx_map_epoch (sem_set_map_shared only)
+  int n_cu = 0;        // compute units of `device` (persistent launches), 0 = not queried
 };
 
 namespace semd {

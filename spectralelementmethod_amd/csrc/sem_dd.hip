@@ -20,8 +20,14 @@
 // small interface launches.  Only shared entries travel: 8 B per shared DOF
 // and direction, never the full vector.
 //
-//   main:  ev0 ------------- interior apply (u -> y) ------------- wait ev1, y[cidx] += y_c
-//   side:  wait ev0, u_c = u[cidx], iface apply (u_c -> y_c), pack, exchange, unpack, ev1
+//   main:  ev0 ------------- interior apply (u -> y) ------------- wait ev1, finish
+//   side:  wait ev0, u_c = u[cidx], iface apply (u_c -> y_c), pack, exchange, ev1
+//
+// finish (k_dd_finish, one launch): y[cidx[j]] += y_c[j] + the neighbours'
+// values for compact DOF j, in peer order -- the unpack and the final add of
+// one step in one kernel; it also takes over the interior operator's zero
+// list (nodes only interface elements touch are overwritten instead of
+// zeroed first), so the step enqueues no zero-fill and no unpack launches.
 #include <hip/hip_runtime.h>
 
 #include <limits>
@@ -151,8 +157,12 @@ __device__ __forceinline__ double pc_z(double r, dinv_t d) { return r * (double)
 __global__ void k_cg_pack(const double* __restrict__ dinv, const uint8_t* __restrict__ f,
                           int64_t n, dinv_t* __restrict__ out) {
   for (int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x; t < n; t += (int64_t)gridDim.x * BLK) {
+    // |1/diag| outside the float range saturates (a free DOF is never 0, never
+    // inf); a NaN diagonal stays NaN, so the solve reports a non-finite
+    // residual instead of running on a made-up preconditioner
     dinv_t v = (dinv_t)fabs(dinv[t]);
-    if (v == (dinv_t)0 || !(v == v)) v = std::numeric_limits<dinv_t>::min();  // free DOF: never 0
+    if (v == (dinv_t)0 && dinv[t] == dinv[t]) v = std::numeric_limits<dinv_t>::min();
+    if (v > std::numeric_limits<dinv_t>::max()) v = std::numeric_limits<dinv_t>::max();
     if (f[t] & F_DIR) v = (dinv_t)0;
     else if (f[t] & F_NOTOWN) v = -v;
     out[t] = v;
@@ -381,10 +391,35 @@ __global__ void k_csr_diag(int64_t n, const int64_t* __restrict__ rp, const int3
   }
 }
 
-__global__ void k_scatter_add_peer(double* __restrict__ dst, const uint32_t* __restrict__ idx,
-                                   int64_t n, const double* __restrict__ src) {
+// the unpack and final add of one step (see the file header): compact DOF
+// t < nc: v = y_c[t] + recv[rpos[rp[t]]] + ... (peer order, as the per-peer
+// unpack launches added them), then y[i] = v (overwrite flag: a node no
+// interior element touches) or y[i] + v, i = fidx[t] & 0x7fffffff; t >= nc:
+// zero the interior's remaining zero-list DOFs (nodes no element touches)
+__global__ void k_dd_finish(double* __restrict__ y, const uint32_t* __restrict__ fidx, int64_t nc,
+                            const double* __restrict__ yc, const int32_t* __restrict__ rp,
+                            const uint32_t* __restrict__ rpos, const double* __restrict__ recv,
+                            const uint32_t* __restrict__ fzero, int64_t nz) {
+  for (int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x; t < nc + nz;
+       t += (int64_t)gridDim.x * BLK) {
+    if (t < nc) {
+      double v = yc[t];
+      for (int32_t k = rp[t]; k < rp[t + 1]; ++k) v += recv[rpos[k]];
+      const uint32_t e = fidx[t];
+      const uint32_t i = e & 0x7fffffffu;
+      y[i] = ((e >> 31) ? 0.0 : y[i]) + v;
+    } else {
+      y[fzero[t - nc]] = 0.0;
+    }
+  }
+}
+
+// the loopback transport's exchange (sem_dd_set_loopback): the send buffer
+// back into the receive buffer, one kernel on the side stream as RCCL's
+// send/recv would be
+__global__ void k_dd_loopback(double* __restrict__ dst, const double* __restrict__ src, int64_t n) {
   for (int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x; t < n; t += (int64_t)gridDim.x * BLK)
-    dst[idx[t]] += src[t];
+    dst[t] = src[t];
 }
 
 }  // namespace
@@ -405,6 +440,16 @@ struct sem_dd {
   double* d_yc = nullptr;
   double* d_send = nullptr;
   double* d_recv = nullptr;
+  // finish tables (k_dd_finish; built by build_finish for the interior
+  // context's plan of map epoch fin_epoch)
+  uint32_t* d_fidx = nullptr;   // cidx[j] | overwrite << 31
+  int32_t* d_rp = nullptr;      // [nc + 1]: received values of compact DOF j at rpos[rp[j]..rp[j+1])
+  uint32_t* d_rpos = nullptr;   // positions in d_recv, peer order
+  uint32_t* d_fzero = nullptr;  // interior zero-list DOFs outside the interface
+  int64_t n_fzero = 0;
+  bool defer_zero = false;      // the interior's zero list is folded into k_dd_finish
+  uint64_t fin_epoch = ~0ull;
+  bool loopback = false;        // diagnostic transport (sem_dd_set_loopback)
   hipStream_t side = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // transport: native RCCL communicator, or caller callbacks
@@ -413,34 +458,117 @@ struct sem_dd {
   sem_allreduce_fn rfn = nullptr;
   void* user = nullptr;
   int world = 1, rank = 0;
-  // captured step (sem_dd_set_graphs): the launches of one action as four
+  // captured step (sem_dd_set_graphs): the launches of one action as three
   // HIP graphs around the transport call -- S: gather, interface elements,
-  // pack (side stream); M: interior elements (caller's stream); F: unpack
-  // per peer (side); G: y[cidx] += y_c (caller's) -- replayed while the
-  // kind and the u / y pointers stay the same.  Off by default: on ROCm 7
+  // pack (side stream); M: interior elements (caller's stream); G: the
+  // finish (caller's) -- replayed while the kind, the u / y pointers and the
+  // contexts' state stay the same.  Off by default: on ROCm 7
   // a graph launch costs more host time than the launches it replaces
   // (profiles/r03/multirank/: 2-rank rehearsal 0.787 ms per step eager,
   // 0.866 captured; tools/r03/stream_bench.cpp: 11.3 us per 2-kernel graph
   // replay against 4.7 us eager); SEM_DD_GRAPH=1 or sem_dd_set_graphs opt in
   bool graphs = false;
   hipStream_t cap = nullptr;  // capture stream of M and G
-  hipGraphExec_t gS = nullptr, gM = nullptr, gF = nullptr, gG = nullptr;
+  hipGraphExec_t gS = nullptr, gM = nullptr, gG = nullptr;
   int g_kind = -1;
   const double* g_u = nullptr;
   double* g_y = nullptr;
+  uint64_t g_ep_iface = 0, g_ep_interior = 0;  // the contexts' epochs at capture
   int64_t n_captures = 0, n_replays = 0;
-  // host time spent enqueueing sem_dd_apply, and inside the transport call
+  // host time spent enqueueing sem_dd_apply, and inside the transport call;
+  // the rest split into the side-stream part (gather, interface elements,
+  // pack), the interior elements and the finish (event + k_dd_finish)
   int64_t host_steps = 0, host_ns = 0, host_ns_transport = 0;
+  int64_t host_ns_side = 0, host_ns_main = 0, host_ns_finish = 0;
 };
 
 namespace {
 
 int64_t n_exchanged(const sem_dd* d) { return d->off.empty() ? 0 : d->off.back(); }
 
-// compute part of one step: interface elements on the side stream into y_c
-// and packed into the send buffer, interior elements on `st` into y.
-// DIAG: the operator diagonal (Jacobi) instead of the action.
-// side-stream part: interface elements into y_c, packed into the send buffer
+// changes whenever either context changes anything its captured launches
+// read (map, geometry, modes, Reynolds number, linearisation buffer):
+// a graph captured before such a call would replay stale arguments or freed
+// pointers (sem::ctx_epoch)
+uint64_t ep_iface(const sem_dd* d) { return d->iface ? sem::ctx_epoch(d->iface) : 0; }
+uint64_t ep_interior(const sem_dd* d) { return d->interior ? sem::ctx_epoch(d->interior) : 0; }
+
+using Clock = std::chrono::steady_clock;
+inline int64_t ns_since(Clock::time_point t0) {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count();
+}
+
+// the finish tables for the interior context's current plan (see the file
+// header): rebuilt when its map changes (synchronises the device then)
+int build_finish(sem_dd* d) {
+  const uint64_t ep = d->interior ? sem::ctx_map_epoch(d->interior) : 0;
+  if (ep == d->fin_epoch && d->d_fidx) return SEM_OK;
+  HIP_TRY(hipDeviceSynchronize());  // nothing in flight reads the old tables
+  const int64_t nc = d->nc, ne = n_exchanged(d);
+  std::vector<uint32_t> cidx((size_t)nc), pidx((size_t)ne);
+  if (nc) HIP_TRY(hipMemcpy(cidx.data(), d->d_cidx, nc * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (ne) HIP_TRY(hipMemcpy(pidx.data(), d->d_pidx, ne * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  // received values per compact DOF, in peer order (the order of d_recv)
+  std::vector<int32_t> rp((size_t)nc + 1, 0);
+  for (int64_t t = 0; t < ne; ++t) {
+    if (pidx[t] >= (uint64_t)nc) return fail(SEM_E_INVALID, "peer DOF outside the interface");
+    rp[pidx[t] + 1]++;
+  }
+  for (int64_t j = 0; j < nc; ++j) rp[j + 1] += rp[j];
+  std::vector<uint32_t> rpos((size_t)std::max<int64_t>(ne, 1));
+  {
+    std::vector<int32_t> fill(rp.begin(), rp.end() - 1);
+    for (int64_t t = 0; t < ne; ++t) rpos[fill[pidx[t]]++] = (uint32_t)t;
+  }
+  // the interior's zero list: interface DOFs among it are overwritten by the
+  // finish, the others zeroed by it -- only when the list holds nodes no
+  // interior element touches (no atomic first writers: those must be zero
+  // before the interior kernel runs)
+  std::vector<uint32_t> fidx(cidx), fzero;
+  bool defer = false;
+  if (d->interior) {
+    std::vector<uint32_t> z;
+    bool only_unref = false;
+    SEM_TRY(sem::ctx_zero_list(d->interior, &z, &only_unref));
+    defer = only_unref;
+    if (defer && !z.empty()) {
+      const int dpn = sem::ctx_dpn(d->interior);
+      std::vector<int32_t> compact((size_t)d->ndof, -1);
+      for (int64_t j = 0; j < nc; ++j) compact[cidx[j]] = (int32_t)j;
+      for (const uint32_t node : z)
+        for (int c = 0; c < dpn; ++c) {
+          const uint32_t dof = node * dpn + c;
+          if (compact[dof] >= 0) fidx[compact[dof]] |= 0x80000000u;
+          else fzero.push_back(dof);
+        }
+    }
+  }
+  (void)hipFree(d->d_fidx);
+  (void)hipFree(d->d_rp);
+  (void)hipFree(d->d_rpos);
+  (void)hipFree(d->d_fzero);
+  d->d_fidx = nullptr;
+  d->d_rp = nullptr;
+  d->d_rpos = nullptr;
+  d->d_fzero = nullptr;
+  HIP_TRY(hipMalloc(&d->d_fidx, std::max<int64_t>(nc, 1) * sizeof(uint32_t)));
+  HIP_TRY(hipMalloc(&d->d_rp, rp.size() * sizeof(int32_t)));
+  HIP_TRY(hipMalloc(&d->d_rpos, rpos.size() * sizeof(uint32_t)));
+  HIP_TRY(hipMalloc(&d->d_fzero, std::max<size_t>(fzero.size(), 1) * sizeof(uint32_t)));
+  if (nc) HIP_TRY(hipMemcpy(d->d_fidx, fidx.data(), nc * sizeof(uint32_t), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(d->d_rp, rp.data(), rp.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  if (ne) HIP_TRY(hipMemcpy(d->d_rpos, rpos.data(), ne * sizeof(uint32_t), hipMemcpyHostToDevice));
+  if (!fzero.empty())
+    HIP_TRY(hipMemcpy(d->d_fzero, fzero.data(), fzero.size() * sizeof(uint32_t),
+                      hipMemcpyHostToDevice));
+  d->n_fzero = (int64_t)fzero.size();
+  d->defer_zero = defer;
+  d->fin_epoch = ep;
+  return SEM_OK;
+}
+
+// side-stream part of one step: interface elements into y_c (DIAG: the
+// operator diagonal instead of the action), packed into the send buffer
 int dd_side(sem_dd* d, int op_kind, bool diag, const double* u, hipStream_t sd) {
   if (!d->iface) return SEM_OK;
   if (diag) {
@@ -452,37 +580,51 @@ int dd_side(sem_dd* d, int op_kind, bool diag, const double* u, hipStream_t sd) 
   return sem_gather(d->d_yc, d->d_pidx, n_exchanged(d), d->d_send, sd);
 }
 
-// main-stream part: interior elements into y
+// main-stream part: interior elements into y (their zero list deferred to
+// the finish when build_finish allowed it)
 int dd_main(sem_dd* d, int op_kind, bool diag, const double* u, double* y, hipStream_t st) {
   if (d->interior) {
     if (diag) return sem_diag(d->interior, op_kind, y, st);
-    return sem_apply(d->interior, op_kind, u, y, 0, st);
+    return sem_apply(d->interior, op_kind, u, y, d->defer_zero ? SEM_APPLY_SKIP_ZERO : 0, st);
   }
   HIP_TRY(hipMemsetAsync(y, 0, d->ndof * sizeof(double), st));
   return SEM_OK;
 }
 
 int dd_begin(sem_dd* d, int op_kind, bool diag, const double* u, double* y, hipStream_t st) {
+  SEM_TRY(build_finish(d));
+  auto t0 = Clock::now();
   HIP_TRY(hipEventRecord(d->ev0, st));
   HIP_TRY(hipStreamWaitEvent(d->side, d->ev0, 0));
   SEM_TRY(dd_side(d, op_kind, diag, u, d->side));
-  return dd_main(d, op_kind, diag, u, y, st);
+  d->host_ns_side += ns_since(t0);
+  t0 = Clock::now();
+  const int rc = dd_main(d, op_kind, diag, u, y, st);
+  d->host_ns_main += ns_since(t0);
+  return rc;
 }
 
 int dd_exchange_impl(sem_dd* d);
 
-// the transport call, timed on the host (sem_dd_info [10])
+// the transport call, timed on the host (sem_dd_info [11])
 int dd_exchange(sem_dd* d) {
-  const auto t0 = std::chrono::steady_clock::now();
+  const auto t0 = Clock::now();
   const int rc = dd_exchange_impl(d);
-  d->host_ns_transport += std::chrono::duration_cast<std::chrono::nanoseconds>(
-                              std::chrono::steady_clock::now() - t0).count();
+  d->host_ns_transport += ns_since(t0);
   return rc;
 }
 
 int dd_exchange_impl(sem_dd* d) {
   const int np = (int)d->peer.size();
   if (!np) return SEM_OK;
+  if (d->loopback) {
+    const int64_t ne = n_exchanged(d);
+    if (ne)
+      hipLaunchKernelGGL(k_dd_loopback, dim3(grid_for(ne)), dim3(BLK), 0, d->side, d->d_recv,
+                         d->d_send, ne);
+    HIP_TRY(hipGetLastError());
+    return SEM_OK;
+  }
   if (d->comm) {
     NCCL_TRY(ncclGroupStart());
     for (int k = 0; k < np; ++k) {
@@ -502,34 +644,29 @@ int dd_exchange_impl(sem_dd* d) {
   return fail(SEM_E_STATE, "no transport: call sem_dd_init_rccl or sem_dd_set_transport");
 }
 
-// neighbours' partial sums into y_c (one launch per peer: a DOF may be
-// shared with several peers), then y[cidx] += y_c on `st` after the side
-// stream's work
-int dd_unpack(sem_dd* d, hipStream_t sd) {
-  for (size_t k = 0; k + 1 < d->off.size(); ++k) {
-    const int64_t cnt = d->off[k + 1] - d->off[k];
-    if (cnt)
-      hipLaunchKernelGGL(k_scatter_add_peer, dim3(grid_for(cnt)), dim3(BLK), 0, sd, d->d_yc,
-                         d->d_pidx + d->off[k], cnt, d->d_recv + d->off[k]);
-  }
+// unpack + final add + deferred zero list in one launch on `st`
+int dd_add(sem_dd* d, double* y, hipStream_t st) {
+  const int64_t tot = d->nc + (d->defer_zero ? d->n_fzero : 0);
+  if (!tot) return SEM_OK;
+  hipLaunchKernelGGL(k_dd_finish, dim3(grid_for(tot)), dim3(BLK), 0, st, y, d->d_fidx, d->nc,
+                     d->d_yc, d->d_rp, d->d_rpos, d->d_recv, d->d_fzero,
+                     d->defer_zero ? d->n_fzero : 0);
   HIP_TRY(hipGetLastError());
   return SEM_OK;
 }
 
-int dd_add(sem_dd* d, double* y, hipStream_t st) {
-  return d->nc ? sem_scatter_add(y, d->d_cidx, d->nc, d->d_yc, st) : SEM_OK;
-}
-
 int dd_finish(sem_dd* d, double* y, hipStream_t st) {
-  SEM_TRY(dd_unpack(d, d->side));
+  const auto t0 = Clock::now();
   HIP_TRY(hipEventRecord(d->ev1, d->side));
   HIP_TRY(hipStreamWaitEvent(st, d->ev1, 0));
-  return dd_add(d, y, st);
+  const int rc = dd_add(d, y, st);
+  d->host_ns_finish += ns_since(t0);
+  return rc;
 }
 
 // ---------------------------------------------------------------- captured step
 void drop_graphs(sem_dd* d) {
-  for (hipGraphExec_t* g : {&d->gS, &d->gM, &d->gF, &d->gG})
+  for (hipGraphExec_t* g : {&d->gS, &d->gM, &d->gG})
     if (*g) {
       (void)hipGraphExecDestroy(*g);
       *g = nullptr;
@@ -558,30 +695,34 @@ int capture(hipStream_t s, F body, hipGraphExec_t* out) {
 int dd_capture(sem_dd* d, int op_kind, const double* u, double* y) {
   drop_graphs(d);
   if (!d->cap) HIP_TRY(hipStreamCreateWithFlags(&d->cap, hipStreamNonBlocking));
-  if (d->iface) {
-    SEM_TRY(capture(d->side, [&] { return dd_side(d, op_kind, false, u, d->side); }, &d->gS));
-    SEM_TRY(capture(d->side, [&] { return dd_unpack(d, d->side); }, &d->gF));
-    SEM_TRY(capture(d->cap, [&] { return dd_add(d, y, d->cap); }, &d->gG));
-  }
+  if (d->iface) SEM_TRY(capture(d->side, [&] { return dd_side(d, op_kind, false, u, d->side); }, &d->gS));
   SEM_TRY(capture(d->cap, [&] { return dd_main(d, op_kind, false, u, y, d->cap); }, &d->gM));
+  SEM_TRY(capture(d->cap, [&] { return dd_add(d, y, d->cap); }, &d->gG));
   d->g_kind = op_kind;
   d->g_u = u;
   d->g_y = y;
+  d->g_ep_iface = ep_iface(d);
+  d->g_ep_interior = ep_interior(d);
   d->n_captures++;
   return SEM_OK;
 }
 
 // one action through the captured graphs: the same dependency structure as
-// dd_begin / dd_exchange / dd_finish, four graph launches instead of ~15
+// dd_begin / dd_exchange / dd_finish, three graph launches instead of ~10
 // kernel launches
 int dd_apply_graphs(sem_dd* d, int op_kind, const double* u, double* y, hipStream_t st) {
-  if (d->g_kind != op_kind || d->g_u != u || d->g_y != y) SEM_TRY(dd_capture(d, op_kind, u, y));
+  SEM_TRY(build_finish(d));
+  if (d->g_kind != op_kind || d->g_u != u || d->g_y != y ||
+      d->g_ep_iface != ep_iface(d) || d->g_ep_interior != ep_interior(d)) {
+    // the previous replay may still be running on the side stream
+    HIP_TRY(hipStreamSynchronize(d->side));
+    SEM_TRY(dd_capture(d, op_kind, u, y));
+  }
   HIP_TRY(hipEventRecord(d->ev0, st));
   HIP_TRY(hipStreamWaitEvent(d->side, d->ev0, 0));
   if (d->gS) HIP_TRY(hipGraphLaunch(d->gS, d->side));
   HIP_TRY(hipGraphLaunch(d->gM, st));
   SEM_TRY(dd_exchange(d));
-  if (d->gF) HIP_TRY(hipGraphLaunch(d->gF, d->side));
   HIP_TRY(hipEventRecord(d->ev1, d->side));
   HIP_TRY(hipStreamWaitEvent(st, d->ev1, 0));
   if (d->gG) HIP_TRY(hipGraphLaunch(d->gG, st));
@@ -895,6 +1036,10 @@ void sem_dd_destroy(sem_dd* d) {
   (void)hipFree(d->d_yc);
   (void)hipFree(d->d_send);
   (void)hipFree(d->d_recv);
+  (void)hipFree(d->d_fidx);
+  (void)hipFree(d->d_rp);
+  (void)hipFree(d->d_rpos);
+  (void)hipFree(d->d_fzero);
   if (d->ev0) (void)hipEventDestroy(d->ev0);
   if (d->ev1) (void)hipEventDestroy(d->ev1);
   if (d->side) (void)hipStreamDestroy(d->side);
@@ -913,8 +1058,25 @@ int sem_dd_init_rccl(sem_dd* d, const void* h_id, int world, int rank) {
   NCCL_TRY(ncclCommInitRank(&comm, world, id, rank));
   if (d->comm) (void)ncclCommDestroy(d->comm);
   d->comm = comm;
+  d->loopback = false;
   d->world = world;
   d->rank = rank;
+  return SEM_OK;
+}
+
+int sem_dd_set_loopback(sem_dd* d) {
+  if (!d) return fail(SEM_E_INVALID, "null dd");
+  DeviceGuard g(d->device);
+  if (d->comm) {
+    (void)ncclCommDestroy(d->comm);
+    d->comm = nullptr;
+  }
+  d->xfn = nullptr;
+  d->rfn = nullptr;
+  d->user = nullptr;
+  d->world = 1;
+  d->rank = 0;
+  d->loopback = true;
   return SEM_OK;
 }
 
@@ -922,6 +1084,7 @@ int sem_dd_set_transport(sem_dd* d, sem_exchange_fn xfn, sem_allreduce_fn rfn, v
                          int world, int rank) {
   if (!d || world < 1 || rank < 0 || rank >= world)
     return fail(SEM_E_INVALID, "sem_dd_set_transport: bad arguments");
+  d->loopback = false;
   d->xfn = xfn;
   d->rfn = rfn;
   d->user = user;
@@ -937,11 +1100,13 @@ int sem_dd_set_transport(sem_dd* d, sem_exchange_fn xfn, sem_allreduce_fn rfn, v
 
 int sem_dd_info(sem_dd* d, int64_t* info, int n_info) {
   if (!d || !info || n_info < 1) return fail(SEM_E_INVALID, "bad arguments");
-  const int64_t v[12] = {d->ndof, d->nc, (int64_t)d->peer.size(), n_exchanged(d),
-                         d->comm ? 1 : (d->xfn ? 2 : 0), d->interior ? 1 : 0,
+  const int64_t v[16] = {d->ndof, d->nc, (int64_t)d->peer.size(), n_exchanged(d),
+                         d->loopback ? 3 : d->comm ? 1 : (d->xfn ? 2 : 0), d->interior ? 1 : 0,
                          d->graphs ? 1 : 0, d->n_captures, d->n_replays,
-                         d->host_steps, d->host_ns, d->host_ns_transport};
-  for (int i = 0; i < n_info && i < 12; ++i) info[i] = v[i];
+                         d->host_steps, d->host_ns, d->host_ns_transport,
+                         d->host_ns_side, d->host_ns_main, d->host_ns_finish,
+                         d->defer_zero ? 1 : 0};
+  for (int i = 0; i < n_info && i < 16; ++i) info[i] = v[i];
   return SEM_OK;
 }
 
@@ -958,8 +1123,7 @@ int sem_dd_apply(sem_dd* d, int op_kind, const double* d_u, double* d_y, void* s
   if (!d || !d_u || !d_y) return fail(SEM_E_INVALID, "null argument");
   if (d_u == d_y) return fail(SEM_E_INVALID, "sem_dd_apply: u and y must not alias");
   DeviceGuard g(d->device);
-  const auto t0 = std::chrono::steady_clock::now();
-  const int64_t tr0 = d->host_ns_transport;
+  const auto t0 = Clock::now();
   int rc;
   if (d->graphs) {
     rc = dd_apply_graphs(d, op_kind, d_u, d_y, S(stream));
@@ -968,9 +1132,7 @@ int sem_dd_apply(sem_dd* d, int op_kind, const double* d_u, double* d_y, void* s
     SEM_TRY(dd_exchange(d));
     rc = dd_finish(d, d_y, S(stream));
   }
-  (void)tr0;
-  d->host_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(
-                    std::chrono::steady_clock::now() - t0).count();
+  d->host_ns += ns_since(t0);
   d->host_steps++;
   return rc;
 }

@@ -164,6 +164,18 @@ __global__ void k_det_inv_2x2(int64_t n, const double* __restrict__ M, double* _
 namespace sem {
 int64_t ctx_ndof(const sem_ctx* c) { return c->n_node * c->dpn; }
 int ctx_device(const sem_ctx* c) { return c->device; }
+uint64_t ctx_epoch(const sem_ctx* c) { return c->epoch; }
+int ctx_dpn(const sem_ctx* c) { return c->dpn; }
+uint64_t ctx_map_epoch(const sem_ctx* c) { return c->map_epoch; }
+int ctx_zero_list(const sem_ctx* c, std::vector<uint32_t>* nodes, bool* only_unreferenced) {
+  nodes->assign((size_t)c->n_zero, 0u);
+  *only_unreferenced = c->n_atomic_groups == 0;
+  if (c->n_zero) {
+    HIP_TRY(hipMemcpy(nodes->data(), c->d_zero, c->n_zero * sizeof(uint32_t),
+                      hipMemcpyDeviceToHost));
+  }
+  return SEM_OK;
+}
 }  // namespace sem
 
 namespace semd {
@@ -1114,6 +1126,7 @@ int sem_set_basis(sem_ctx* c, const double* hD, const double* hw) {
   if (!(dasym <= 1e-12 * dmax) || !(wasym <= 1e-14 * wmax))
     return fail(SEM_E_INVALID,
                 "sem_set_basis: D and w must come from a node set symmetric about 0 (GLL)");
+  c->epoch++;
   std::memcpy(c->hD, hD, sizeof(double) * n * n);
   std::memcpy(c->hw, hw, sizeof(double) * n);
   HIP_TRY(hipMemcpy(c->d_D, hD, sizeof(double) * n * n, hipMemcpyHostToDevice));
@@ -1133,6 +1146,8 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
                        void* stream) {
   if (!c || !d_e2n) return fail(SEM_E_INVALID, "null argument");
   DeviceGuard g(c->device);
+  c->epoch++;
+  c->map_epoch++;
   hipStream_t st = S(stream);
   const int n = c->n;
   std::vector<uint32_t> h((size_t)c->n_elem * n * n);
@@ -1336,6 +1351,7 @@ int sem_set_geom_mode(sem_ctx* c, int mode) {
   if (mode != SEM_GEOM_STORED && mode != SEM_GEOM_NODAL && mode != SEM_GEOM_AUTO)
     return fail(SEM_E_INVALID, "unknown geometry mode " + std::to_string(mode));
   c->geom_mode = mode;
+  c->epoch++;
   return SEM_OK;
 }
 
@@ -1343,6 +1359,7 @@ int sem_set_reynolds(sem_ctx* c, double re) {
   if (!c) return fail(SEM_E_INVALID, "null ctx");
   if (!std::isfinite(re)) return fail(SEM_E_INVALID, "Reynolds number must be finite");
   c->reynolds = re;
+  c->epoch++;
   c->lin_valid = false;  // a recorded linearisation belongs to the old Re
   return SEM_OK;
 }
@@ -1354,6 +1371,7 @@ int sem_set_kernel(sem_ctx* c, int kernel) {
   if (kernel == SEM_KERNEL_MFMA && (c->dpn != 1 || c->n > 17))
     return fail(SEM_E_NOTIMPL, "the MFMA kernel needs dofs_per_node == 1 and p <= 16");
   c->kernel = kernel;
+  c->epoch++;
   return SEM_OK;
 }
 
@@ -1365,6 +1383,7 @@ int sem_geom_from_nodes(sem_ctx* c, const double* d_nodes, const double* h_Vinv,
   if (rc) return rc;
   if ((rc = check_op(c, op_kind))) return rc;
   const bool nodal = nodal_mode_op(c, op_kind);
+  c->epoch++;
   double* GP = nullptr;
   if (nodal) {
     if (!c->d_XG) HIP_TRY(hipMalloc(&c->d_XG, c->n_node * sizeof(double2)));
@@ -1419,6 +1438,7 @@ int sem_set_geom(sem_ctx* c, const double* d_G, int op_kind, void* stream) {
   if ((rc = check_op(c, op_kind))) return rc;
   if ((rc = ensure_gp(c, op_kind, S(stream)))) return rc;
   const int ncomp = sem_op_ncomp(op_kind);
+  c->epoch++;
   if (op_kind == SEM_OP_POISSON) c->xg_valid = false;  // caller's factors take over
   if (op_kind == SEM_OP_AXISYM_STOKES) c->xg_axi = false;
   hipLaunchKernelGGL(k_pack_geom, dim3(grid_for(c->n_elem * ncomp * c->n * c->n)), dim3(BLOCK), 0,
@@ -1458,8 +1478,10 @@ int sem_apply(sem_ctx* c, int op_kind, const double* u, double* y, int flags, vo
     return fail(SEM_E_INVALID, "SEM_APPLY_LINEARIZE applies to SEM_OP_AXISYM_NS only");
   if (op_kind == SEM_OP_AXISYM_NS_JVP && !c->lin_valid)
     return fail(SEM_E_STATE, "no linearisation: apply SEM_OP_AXISYM_NS with SEM_APPLY_LINEARIZE first");
-  if (lin && !c->d_lin)
+  if (lin && !c->d_lin) {
     HIP_TRY(hipMalloc(&c->d_lin, (size_t)c->n_slots * 5 * c->n * c->lw * sizeof(double)));
+    c->epoch++;
+  }
   DeviceGuard g(c->device);
   hipStream_t st = S(stream);
   const int accumulate = flags & SEM_APPLY_ACCUMULATE;

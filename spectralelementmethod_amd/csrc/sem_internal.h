@@ -3,6 +3,7 @@
 #pragma once
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "../../include/sem_hip.h"
 
@@ -29,4 +30,16 @@ int invert(int n, const double* A, double* Ainv);
 namespace sem {
 int64_t ctx_ndof(const sem_ctx* c);
 int ctx_device(const sem_ctx* c);
+// bumped by every call that changes what a launch reads (map, geometry,
+// basis, modes, Reynolds number, linearisation buffer): a captured step
+// compares it before replaying (sem_dd.hip)
+uint64_t ctx_epoch(const sem_ctx* c);
+// nodes the context zeroes before an overwrite (its zero list) copied to the
+// host; *only_unreferenced: the list holds only nodes none of the context's
+// elements touch (no atomic first writers), so zeroing them may be deferred
+// to any later kernel on the same stream
+int ctx_zero_list(const sem_ctx* c, std::vector<uint32_t>* nodes, bool* only_unreferenced);
+int ctx_dpn(const sem_ctx* c);
+// bumped by sem_set_map_shared only (the plan, hence the zero list, changed)
+uint64_t ctx_map_epoch(const sem_ctx* c);
 }  // namespace sem

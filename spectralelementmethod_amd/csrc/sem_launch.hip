@@ -87,15 +87,16 @@ void launch_mfma17(sem_ctx* c, const double* u, double* y, int acc, int64_t c0, 
                    const SeamPlan& sp, hipStream_t st) {
   constexpr int per_block = MF17_PAIRS * MF17_EW;
   const int64_t nwg = (c1 - c0 + per_block - 1) / per_block;
-  static int resident = 0;  // workgroups resident on the device at SEM_MF17P_WAVES
-  if (!resident) {
+  if (!c->n_cu) {  // the context's device, queried once per context
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) !=
             hipSuccess ||
         ncu <= 0)
       ncu = 256;
-    resident = ncu * 4 * SEM_MF17P_WAVES / (BLOCK / WAVE);
+    c->n_cu = ncu;
   }
+  // workgroups resident on the device at SEM_MF17P_WAVES
+  const int resident = c->n_cu * 4 * SEM_MF17P_WAVES / (BLOCK / WAVE);
   const dim3 g((unsigned)std::min<int64_t>(nwg, resident));
   hipLaunchKernelGGL((k_poisson_mfma17p<MF17_N, SEAM>), g, dim3(BLOCK), 0, st, c->d_mapP,
                      c->d_GP[0], u, y, c->d_D, c0, c1, acc, sp);

@@ -186,7 +186,8 @@ __global__ void k_band_fill(int64_t n, int KU, int W, const int64_t* __restrict_
 
 // One workgroup: the elimination is a chain of n dependent steps; each step
 // (pivot search over kl + 1 entries, row swap over KU + 1 columns, rank-1
-// update of a kl x KU block) is spread over the workgroup.  b is eliminated
+// update of a kl x KU block) is spread over the workgroup.  The multipliers
+// replace column j below the diagonal (LAPACK's in-place L), so any kl fits.  b is eliminated
 // alongside; then the column-oriented back substitution (U's column j above
 // the diagonal is contiguous in this layout).  info = j + 1 for an exactly
 // zero pivot in column j (LAPACK's convention), 0 otherwise.
@@ -195,7 +196,6 @@ __global__ void __launch_bounds__(BLU)
                     double* __restrict__ b, double* __restrict__ x, int* __restrict__ info) {
   __shared__ double s_val[BLU];
   __shared__ int s_idx[BLU];
-  __shared__ double s_l[BLU];  // multipliers of the step (kl < BLU)
   const int tid = threadIdx.x;
   for (int64_t j = 0; j < n; ++j) {
     const int64_t ilast = min<int64_t>(n - 1, j + kl);
@@ -246,9 +246,10 @@ __global__ void __launch_bounds__(BLU)
     __syncthreads();
     const double inv = 1.0 / AB[j * W + KU];
     const double bj = b[j];
+    double* lcol = AB + j * W + KU;  // (j + r, j) at lcol[r]
     for (int r = 1 + tid; r <= nr; r += BLU) {
-      const double l = AB[j * W + KU + r] * inv;
-      s_l[r] = l;
+      const double l = lcol[r] * inv;
+      lcol[r] = l;
       b[j + r] = fma(-l, bj, b[j + r]);
     }
     __syncthreads();
@@ -258,7 +259,7 @@ __global__ void __launch_bounds__(BLU)
     for (int64_t t = tid; t < tot; t += BLU) {
       const int c = 1 + (int)(t / nr), r = 1 + (int)(t % nr);
       double* col = AB + (j + c) * W + (KU - c);  // (i, j + c) at col[i - j]
-      col[r] = fma(-s_l[r], col[0], col[r]);
+      col[r] = fma(-lcol[r], col[0], col[r]);
     }
     __syncthreads();
   }
@@ -307,7 +308,8 @@ int sem_schur_batched(int64_t n_elem, int nl, int ne, const double* d_mat, const
 int sem_band_lu_solve(int64_t n, int kl, int ku, const int64_t* d_rowptr, const int32_t* d_colind,
                       const double* d_val, const double* d_b, double* d_x, int* info,
                       void* stream) {
-  if (n < 0 || kl < 0 || ku < 0 || kl >= BLU) return fail(SEM_E_INVALID, "sem_band_lu_solve: bad sizes");
+  if (n < 0 || kl < 0 || ku < 0 || (int64_t)kl + ku > (1 << 28))
+    return fail(SEM_E_INVALID, "sem_band_lu_solve: bad sizes");
   if (n && (!d_rowptr || !d_colind || !d_val || !d_b || !d_x || !info))
     return fail(SEM_E_INVALID, "sem_band_lu_solve: null argument");
   if (!n) {

@@ -492,8 +492,6 @@ def band_lu_solve(A, b, device):
     if n == 0:
         return np.zeros(0)
     perm, Ap, kl, ku = band_order(A)
-    if kl >= 1024:
-        raise NotImplementedError("band_lu_solve: lower bandwidth %d after RCM (limit 1023)" % kl)
     lib = _lib.load()
     rp = torch.from_numpy(Ap.indptr.astype(np.int64)).to(device)
     ci = torch.from_numpy(Ap.indices.astype(np.int32)).to(device)

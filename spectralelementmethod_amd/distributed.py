@@ -469,7 +469,10 @@ class OverlappedOperator(object):
     transport: "rccl" (native RCCL send/recv + all-reduce), "torch"
     (torch.distributed point-to-point, see TorchTransport), or "auto"
     (RCCL when the process group is NCCL and the communicator comes up,
-    torch otherwise).  decompose (default: world > 1) forces the sem_dd path
+    torch otherwise), or "loopback" (diagnostic, sem_dd_set_loopback: each
+    exchange returns this rank's own interface values, so ONE rank of a
+    decomposition runs and is timed alone on one GPU; the result is not the
+    global action).  decompose (default: world > 1) forces the sem_dd path
     (tests run it on one rank to exercise the native RCCL calls)."""
 
     def __init__(self, p, nodes, e2n, neighbors, dofs_per_node=1, device=None, group=None,
@@ -527,9 +530,14 @@ class OverlappedOperator(object):
             op.compute_geometry(kind)
 
     def _install_transport(self, transport, group):
-        backend = str(dist.get_backend(group)).lower()
-        if transport not in ("auto", "rccl", "torch"):
-            raise ValueError("transport must be auto, rccl or torch")
+        backend = str(dist.get_backend(group)).lower() if dist.is_initialized() else ""
+        if transport not in ("auto", "rccl", "torch", "loopback"):
+            raise ValueError("transport must be auto, rccl, torch or loopback")
+        if transport == "loopback":  # diagnostic: one rank timed alone (sem_dd_set_loopback)
+            _lib.check(self._lib.sem_dd_set_loopback(self.dd))
+            self.world, self.rank = 1, 0
+            self.transport = "loopback"
+            return
         if transport == "rccl" or (transport == "auto" and "nccl" in backend):
             try:
                 init_rccl(self.dd, self.world, self.rank, group)
@@ -569,15 +577,18 @@ class OverlappedOperator(object):
         """The decomposition's sem_dd_info as a dict (None on one rank)."""
         if not self.dd:
             return None
-        v = (C.c_int64 * 12)()
-        _lib.check(self._lib.sem_dd_info(self.dd, v, 12))
+        v = (C.c_int64 * 16)()
+        _lib.check(self._lib.sem_dd_info(self.dd, v, 16))
         steps = max(1, v[9])
         return dict(ndof=v[0], iface_dofs=v[1], peers=v[2], exchanged=v[3],
-                    transport=("none", "rccl", "callbacks")[v[4]], interior=bool(v[5]),
-                    graphs=bool(v[6]), captures=v[7], replays=v[8], applies=v[9],
-                    host_ns=v[10], host_ns_transport=v[11],
+                    transport=("none", "rccl", "callbacks", "loopback")[v[4]],
+                    interior=bool(v[5]), graphs=bool(v[6]), captures=v[7], replays=v[8],
+                    applies=v[9], host_ns=v[10], host_ns_transport=v[11],
                     host_us_per_apply=v[10] / steps / 1e3,
-                    host_us_per_apply_excl_transport=(v[10] - v[11]) / steps / 1e3)
+                    host_us_per_apply_excl_transport=(v[10] - v[11]) / steps / 1e3,
+                    host_ns_side=v[12], host_ns_interior=v[13], host_ns_finish=v[14],
+                    host_us_side=v[12] / steps / 1e3, host_us_interior=v[13] / steps / 1e3,
+                    host_us_finish=v[14] / steps / 1e3, zero_list_in_finish=bool(v[15]))
 
     def set_graphs(self, enable):
         """Captured step on / off (sem_dd_set_graphs)."""

@@ -256,6 +256,28 @@ def test_band_lu_solve_vs_spsolve():
     assert np.isnan(xs).all()
 
 
+def test_band_lu_solve_wide_band():
+    """A lower bandwidth above the factorising workgroup's 1024 threads
+    (kl >= 1024 used to raise where the reference's spsolve
+    solves): the multipliers live in the band, so any kl is accepted.
+    Non-symmetric, pivoting needed; tolerance 1e-9 relative L2 vs spsolve."""
+    from scipy import sparse
+    from scipy.sparse import linalg as spla
+    from spectralelementmethod_amd.discrete import band_lu_solve, band_order
+    rng = np.random.default_rng(12)
+    n, bw = 2600, 1100
+    A = sparse.diags([rng.standard_normal(n - abs(k)) for k in range(-bw, bw + 1)],
+                     list(range(-bw, bw + 1)), format="lil")
+    A.setdiag(1e-3 * rng.standard_normal(n) + 30.0)
+    A = A.tocsr()
+    _, _, kl, _ = band_order(A)
+    assert kl >= 1024
+    b = rng.standard_normal(n)
+    ref = spla.spsolve(A.tocsc(), b)
+    x = band_lu_solve(A, b, torch.device("cuda", 0))
+    assert rel_l2(x, ref) < 1e-9
+
+
 def test_static_condensation_nonsymmetric_device_solve():
     """The condensed exterior system of non-symmetric local systems (the
     shape of the axisymmetric Stokes / Navier-Stokes block the squirmer

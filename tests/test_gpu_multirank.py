@@ -369,8 +369,26 @@ def _graph_worker(rank, world, port, q):
         # the Jacobi diagonal is summed with atomics (setup, sem_diag): the two
         # solves differ at rounding level, not in their iteration count
         dx = ((sol[False][0] - sol[True][0]).norm() / sol[True][0].norm()).item()
+        # a context state change between two captured steps
+        # (new coordinates, geometry switched to stored factors) must
+        # re-capture; a stale graph would replay the old x_phys kernel
+        from spectralelementmethod_amd import _lib
+        op.set_graphs(True)
+        y_g = torch.zeros_like(u)
+        op.step(u, y_g)  # captured on the current state
+        for o in op.ops:
+            o.nodes[0].mul_(1.5)
+            _lib.check(o._lib.sem_set_geom_mode(o._ctx, _lib.GEOM_STORED))
+            o.compute_geometry()
+        op.step(u, y_g)
+        op.set_graphs(False)
+        y_e = torch.zeros_like(u)
+        op.step(u, y_e)
+        torch.cuda.synchronize()
+        recapture = (torch.equal(y_g, y_e), not torch.allclose(y_e, out[False]),
+                     op.dd_info()["captures"])
         q.put((rank, torch.equal(out[False], out[True]), info, dx, sol[False][1], sol[True][1],
-               enq[False] * 1e6, enq[True] * 1e6))
+               enq[False] * 1e6, enq[True] * 1e6, recapture))
         op.close()
     finally:
         dist.destroy_process_group()
@@ -396,8 +414,10 @@ def test_captured_step_equals_eager(gpu):
             pr.join(timeout=60)
     for pr in procs:
         assert pr.exitcode == 0
-    for rank, same, info, dx, its0, its1, us_eager, us_graph in res:
+    for rank, same, info, dx, its0, its1, us_eager, us_graph, recap in res:
         assert same, rank
+        assert recap[0] and recap[1], (rank, recap)  # re-captured after the state change
+        assert recap[2] > info["captures"], (rank, recap, info)
         assert info["graphs"] and info["replays"] >= 10 and info["captures"] >= 1, info
         assert dx < 1e-12 and abs(its0 - its1) <= 16, (rank, dx, its0, its1)
         print("rank %d host enqueue per step (transport call excluded): eager %.1f us, "
