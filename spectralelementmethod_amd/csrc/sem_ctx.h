@@ -161,6 +161,12 @@ DEOData<N> make_deo_data(const double* h) {
       d.cc[m] = h[m * N + H];
       d.rr[m] = h[H * N + m];
     }
+  if (DEOData<N>::TR)
+    for (int m = 0; m < H; ++m)
+      for (int q = 0; q < H; ++q) {
+        d.PT[q * H + m] = d.P[m * H + q];
+        d.QT[q * H + m] = d.Q[m * H + q];
+      }
   return d;
 }
 

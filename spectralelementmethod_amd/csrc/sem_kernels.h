@@ -103,15 +103,32 @@ struct RmwPrefetch {
 // plus, for odd N, the middle column cc[m] = D[m][H] and row rr[r] = D[H][r]:
 // 2H^2 + 2H values instead of N^2 (40 vs 81 doubles at p = 8, so D fits the
 // scalar register file next to the kernel's pointers) and ~40 % fewer FMAs.
+// TR: the transposes PT[q][m] = P[m][q], QT[q][m] = Q[m][q] as well, for the
+// device copy read with scalar loads (n >= SEM_D_SCALAR_LOAD_N): the D^T
+// contractions then read each output row's 2H coefficients as two contiguous
+// 8 x 8-byte runs (two s_load_dwordx16) instead of 2H strided single loads,
+// each followed by a wait (the p = 12..16 stall)
+#ifndef SEM_D_SCALAR_LOAD_N
+#define SEM_D_SCALAR_LOAD_N 10
+#endif
+#ifndef SEM_DEO_TRANSPOSED
+#define SEM_DEO_TRANSPOSED 1
+#endif
 template <int N>
 struct DEOData {
   static constexpr int H = N / 2;
   static constexpr int C = N % 2;
+  static constexpr bool TR = SEM_DEO_TRANSPOSED && N >= SEM_D_SCALAR_LOAD_N;
   double P[H * H];
   double Q[H * H];
   double cc[C ? H : 1];
   double rr[C ? H : 1];
+  double PT[TR ? H * H : 1];
+  double QT[TR ? H * H : 1];
 };
+// Q[m][q] and P[m][q] for a contraction over m at fixed q (D^T x)
+#define DEO_QC(E, m, q) (DEOData<N>::TR ? (E)->QT[(q) * H + (m)] : (E)->Q[(m) * H + (q)])
+#define DEO_PC(E, m, q) (DEOData<N>::TR ? (E)->PT[(q) * H + (m)] : (E)->P[(m) * H + (q)])
 
 // How the kernels see D.  Up to n = 9 the even-odd halves are kernel
 // arguments (SGPRs for the whole kernel).  Above, they no longer fit the
@@ -124,9 +141,6 @@ struct DEOData {
 // through the CU's LDS port -- slower at every order, p = 10 / 12 / 14 / 16:
 // 0.131 / 0.137 / 0.153 / 0.158 against 0.122 / 0.131 / 0.138 / 0.138 ms,
 // profiles/r03/high_order_d.)
-#ifndef SEM_D_SCALAR_LOAD_N
-#define SEM_D_SCALAR_LOAD_N 10
-#endif
 template <int N>
 using CDEOData = const __attribute__((address_space(4))) DEOData<N>;
 
@@ -200,8 +214,8 @@ __device__ __forceinline__ void deo_apply_t(const DEO<N>& D, const double (&x)[N
     if constexpr (DEOData<N>::C) tp = E->rr[q] * x[H];
 #pragma unroll
     for (int m = 0; m < H; ++m) {
-      sp = fma(E->Q[m * H + q], o[m], sp);
-      tp = fma(E->P[m * H + q], e[m], tp);
+      sp = fma(DEO_QC(E, m, q), o[m], sp);
+      tp = fma(DEO_PC(E, m, q), e[m], tp);
     }
     v[q] = sp + tp;
     v[N - 1 - q] = sp - tp;
@@ -235,8 +249,8 @@ __device__ __forceinline__ void deo_apply_to(const DEO<N>& D, const double (&x)[
     if constexpr (DEOData<N>::C) tp = (TR ? E->rr[m] : E->cc[m]) * x[H];
 #pragma unroll
     for (int r = 0; r < H; ++r) {
-      sp = fma(TR ? E->Q[r * H + m] : E->P[m * H + r], o[r], sp);
-      tp = fma(TR ? E->P[r * H + m] : E->Q[m * H + r], e[r], tp);
+      sp = fma(TR ? DEO_QC(E, r, m) : E->P[m * H + r], o[r], sp);
+      tp = fma(TR ? DEO_PC(E, r, m) : E->Q[m * H + r], e[r], tp);
     }
     out[m] = sp + tp;
     out[N - 1 - m] = sp - tp;
@@ -989,11 +1003,36 @@ __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nwg) {
 // against 0.116-0.119 ms per action (call AC, two runs alternating,
 // profiles/r03/knobs/min_waves_low/); requests at p = 2 / 6 leave their
 // AUTO instantiations' code unchanged, and cfg2 (p = 8 seams) keeps 4.
+// Stored-factor seam kernels at n = 12 / 13 / 15 / 17 (with the transposed
+// D copy, SEM_DEO_TRANSPOSED, the static register tables: n = 12 natural 126
+// VGPRs + 108 SGPRs spilled to lanes, 4-wave request 106 and none; n = 15
+// natural 118 / 4 waves, the old 5-wave request 171 / 2 waves; n = 17
+// natural 161 + 42 spilled, 3-wave request 136 and none): SEM_MW_S<n>
+// overrides the request per order (A/B builds); 0 = the default below.
+#ifndef SEM_MW_S12
+#define SEM_MW_S12 0
+#endif
+#ifndef SEM_MW_S13
+#define SEM_MW_S13 0
+#endif
+#ifndef SEM_MW_S15
+#define SEM_MW_S15 0
+#endif
+#ifndef SEM_MW_S17
+#define SEM_MW_S17 0
+#endif
+constexpr int stored_seam_mw(int n) {
+  return n == 12 ? (SEM_MW_S12 ? SEM_MW_S12 : (SEM_DEO_TRANSPOSED ? 4 : 1))
+       : n == 13 ? (SEM_MW_S13 ? SEM_MW_S13 : 1)
+       : n == 15 ? (SEM_MW_S15 ? SEM_MW_S15 : (SEM_DEO_TRANSPOSED ? 1 : 5))
+       : n == 17 ? (SEM_MW_S17 ? SEM_MW_S17 : (SEM_DEO_TRANSPOSED ? 3 : 1))
+                 : 1;
+}
 template <int N, bool NODAL, bool SEAM = false, bool DOT = false>
 struct PoissonMinWaves {
   static constexpr int value = SEM_POISSON_MIN_WAVES > 0             ? SEM_POISSON_MIN_WAVES
                                : (NODAL && N == 9)                   ? 4
-                               : (!NODAL && N == 15 && SEAM && !DOT) ? 5
+                               : (!NODAL && SEAM && !DOT)            ? stored_seam_mw(N)
                                : (NODAL && N == 5 && !SEAM && !DOT)  ? 6
                                                                      : 1;
 };

@@ -11,7 +11,8 @@ OUTDIR/label.out and stderr to OUTDIR/label.err, under its own time limit
 faults or times out ends the call: nothing after it starts.  A bench JSON
 line on a step's stdout is summarised on this process's stdout.
 TMPDIR is /tmp for every step (rocprofv3).  The command is split with shlex
-(no shell): put the program itself right after rocprofv3's `--`.
+(no shell; leading VAR=value words set the step's environment): put the
+program itself right after rocprofv3's `--`.
 """
 import json
 import os
@@ -59,7 +60,11 @@ def main():
         so, se = os.path.join(out, label + ".out"), os.path.join(out, label + ".err")
         t0 = time.time()
         with open(so, "w") as fo, open(se, "w") as fe:
-            pr = subprocess.Popen(shlex.split(cmd), stdout=fo, stderr=fe, env=env,
+            argv, step_env = shlex.split(cmd), dict(env)
+            while argv and "=" in argv[0] and not argv[0].startswith(("-", "/", ".")):
+                k, v = argv.pop(0).split("=", 1)  # leading VAR=value: environment
+                step_env[k] = v
+            pr = subprocess.Popen(argv, stdout=fo, stderr=fe, env=step_env,
                                   start_new_session=True)
             rc = None
             while rc is None:

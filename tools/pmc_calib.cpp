@@ -26,6 +26,8 @@
 //       as the first-writer stores);
 //   wscatter_rows / wscatter_rows_nt: the y scatter -- the gather_rows shape
 //       as stores;
+//   wrows_aligned: the scatter's rows as whole, 512-B aligned 64-double runs
+//       (what a line-aligned chain layout would store);
 //   wstrided8: one 8-B store per lane at a stride of 8193 doubles.
 #include <hip/hip_runtime.h>
 
@@ -100,8 +102,21 @@ __global__ void k_rows(T* __restrict__ a, int64_t rows, int64_t row_len, double*
   if (s == 1234.5) out[0] = s;
 }
 
-// n words covered at a stride: pass q, lane i -> word (i * STRIDE + q) % n
-// (STRIDE odd and n a power of two: a permutation), every word once
+// the aligned reference of the scatter shape: a wave writes 8 rows of 64
+// consecutive doubles starting on a 512-B boundary (whole 128-B lines)
+__global__ void k_wrows_aligned(double* __restrict__ a, int64_t rows, int64_t row_len) {
+  const int lane = threadIdx.x % 64;
+  const int64_t wave = (blockIdx.x * (int64_t)BLK + threadIdx.x) / 64;
+  const int64_t nwave = (int64_t)gridDim.x * BLK / 64;
+  const int64_t segs = row_len / 64;
+  for (int64_t w = wave; w < (rows / 8) * segs; w += nwave) {
+    const int64_t band = w / segs, seg = w % segs;
+    for (int r = 0; r < 8; ++r) a[(band * 8 + r) * row_len + seg * 64 + lane] = 0.0;
+  }
+}
+
+// n words covered at a stride: item i -> word (i * STRIDE) mod n (STRIDE odd
+// and n a power of two: a permutation), every word once
 template <bool WRITE>
 __global__ void k_strided(double* __restrict__ a, int64_t n, double* __restrict__ out) {
   double s = 0;
@@ -124,46 +139,66 @@ int main() {
   CK(hipMemset(a, 0, bytes + 4096));
   CK(hipDeviceSynchronize());
   const int grid = 8192;
+  // each kernel is timed with HIP events (the second run of two: the first
+  // warms the TLB); the bytes the counters see are those of both runs
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  float ms = 0.f;
+#define TIMED(launch)                      \
+  do {                                     \
+    launch;                                \
+    CK(hipEventRecord(e0));                \
+    launch;                                \
+    CK(hipEventRecord(e1));                \
+    CK(hipEventSynchronize(e1));           \
+    CK(hipEventElapsedTime(&ms, e0, e1));  \
+  } while (0)
   // rows of the row kernels: row_len a multiple of 56 (full segments), every
   // element of rows x row_len touched once
   const int64_t row_len = 56 * 146;  // 8176 nodes (one 1024^2 column is 8193)
-  std::printf("# name bytes_touched (each kernel launched once, in this order)\n");
+  std::printf("# name bytes_touched ms (each kernel launched twice in a row, this order; bytes are per launch)\n");
   auto rows_of = [&](size_t elt) { return (int64_t)(bytes / elt / row_len) / 8 * 8; };
-  k_stream<double2><<<grid, BLK>>>((const double2*)a, bytes / 16, out);
-  std::printf("stream16 %zu\n", bytes);
-  k_stream<double><<<grid, BLK>>>((const double*)a, bytes / 8, out);
-  std::printf("stream8 %zu\n", bytes);
-  k_stream<uint32_t><<<grid, BLK>>>((const uint32_t*)a, bytes / 4, out);
-  std::printf("stream4 %zu\n", bytes);
-  k_stream<uint16_t><<<grid, BLK>>>((const uint16_t*)a, bytes / 2, out);
-  std::printf("stream2 %zu\n", bytes);
+  TIMED((k_stream<double2><<<grid, BLK>>>((const double2*)a, bytes / 16, out)));
+  std::printf("stream16 %zu %.4f\n", bytes, ms);
+  TIMED((k_stream<double><<<grid, BLK>>>((const double*)a, bytes / 8, out)));
+  std::printf("stream8 %zu %.4f\n", bytes, ms);
+  TIMED((k_stream<uint32_t><<<grid, BLK>>>((const uint32_t*)a, bytes / 4, out)));
+  std::printf("stream4 %zu %.4f\n", bytes, ms);
+  TIMED((k_stream<uint16_t><<<grid, BLK>>>((const uint16_t*)a, bytes / 2, out)));
+  std::printf("stream2 %zu %.4f\n", bytes, ms);
   {
     const int64_t r = rows_of(8);
-    k_rows<double, 0><<<grid, BLK>>>((double*)a, r, row_len, out);
-    std::printf("gather_rows %lld\n", (long long)(r * row_len * 8));
+    TIMED((k_rows<double, 0><<<grid, BLK>>>((double*)a, r, row_len, out)));
+    std::printf("gather_rows %lld %.4f\n", (long long)(r * row_len * 8), ms);
   }
   {
     const int64_t r = rows_of(16);
-    k_rows<double2, 0><<<grid, BLK>>>((double2*)a, r, row_len, out);
-    std::printf("gather_rows16 %lld\n", (long long)(r * row_len * 16));
+    TIMED((k_rows<double2, 0><<<grid, BLK>>>((double2*)a, r, row_len, out)));
+    std::printf("gather_rows16 %lld %.4f\n", (long long)(r * row_len * 16), ms);
   }
-  k_strided<false><<<grid, BLK>>>((double*)a, bytes / 8, out);
-  std::printf("strided8 %zu\n", bytes);
-  k_wstream<double2, false><<<grid, BLK>>>((double2*)a, bytes / 16);
-  std::printf("wstream16 %zu\n", bytes);
-  k_wstream<double, false><<<grid, BLK>>>((double*)a, bytes / 8);
-  std::printf("wstream8 %zu\n", bytes);
-  k_wstream<double, true><<<grid, BLK>>>((double*)a, bytes / 8);
-  std::printf("wstream8_nt %zu\n", bytes);
+  TIMED((k_strided<false><<<grid, BLK>>>((double*)a, bytes / 8, out)));
+  std::printf("strided8 %zu %.4f\n", bytes, ms);
+  TIMED((k_wstream<double2, false><<<grid, BLK>>>((double2*)a, bytes / 16)));
+  std::printf("wstream16 %zu %.4f\n", bytes, ms);
+  TIMED((k_wstream<double, false><<<grid, BLK>>>((double*)a, bytes / 8)));
+  std::printf("wstream8 %zu %.4f\n", bytes, ms);
+  TIMED((k_wstream<double, true><<<grid, BLK>>>((double*)a, bytes / 8)));
+  std::printf("wstream8_nt %zu %.4f\n", bytes, ms);
   {
     const int64_t r = rows_of(8);
-    k_rows<double, 1><<<grid, BLK>>>((double*)a, r, row_len, out);
-    std::printf("wscatter_rows %lld\n", (long long)(r * row_len * 8));
-    k_rows<double, 2><<<grid, BLK>>>((double*)a, r, row_len, out);
-    std::printf("wscatter_rows_nt %lld\n", (long long)(r * row_len * 8));
+    TIMED((k_rows<double, 1><<<grid, BLK>>>((double*)a, r, row_len, out)));
+    std::printf("wscatter_rows %lld %.4f\n", (long long)(r * row_len * 8), ms);
+    TIMED((k_rows<double, 2><<<grid, BLK>>>((double*)a, r, row_len, out)));
+    std::printf("wscatter_rows_nt %lld %.4f\n", (long long)(r * row_len * 8), ms);
   }
-  k_strided<true><<<grid, BLK>>>((double*)a, bytes / 8, out);
-  std::printf("wstrided8 %zu\n", bytes);
+  {
+    const int64_t rl = 8192, r = (int64_t)(bytes / 8 / rl) / 8 * 8;
+    TIMED((k_wrows_aligned<<<grid, BLK>>>((double*)a, r, rl)));
+    std::printf("wrows_aligned %lld %.4f\n", (long long)(r * rl * 8), ms);
+  }
+  TIMED((k_strided<true><<<grid, BLK>>>((double*)a, bytes / 8, out)));
+  std::printf("wstrided8 %zu %.4f\n", bytes, ms);
   CK(hipDeviceSynchronize());
   return 0;
 }
