@@ -585,7 +585,7 @@ constexpr uint32_t M16_OFF_MASK = 0xFFFu;
 constexpr uint32_t M16_WIDE = 0xFFFFFFFFu;  // base[slot][0]: this group uses the 32-bit map
 constexpr int M16_CODE_SHIFT = 12;
 
-template <int N, bool M16 = false>
+template <int N, bool M16 = false, bool LD = false>
 __device__ __forceinline__ void load_map(const MapRef& m, int64_t g, int lane, bool in_wave,
                                          uint32_t (&raw)[N]) {
   constexpr int LW = Tile<N>::LW;
@@ -612,6 +612,11 @@ __device__ __forceinline__ void load_map(const MapRef& m, int64_t g, int lane, b
     wide = b[0] == M16_WIDE;
   }
   if (wide) {  // 32-bit map (M16: a group whose rows span >= 4096 ids)
+    // LD (RawLaunder): the rare wide group's per-lane offset is re-formed
+    // here, so the compiler cannot hoist p32 + lane out of the round loop as
+    // a 64-bit VGPR address (spilled to scratch at the headline's register
+    // limit, one store and one reload per round)
+    if constexpr (M16 && LD) asm volatile("" : "+v"(lane));
     const uint32_t* mp = m.p32 + g * (int64_t)(N * LW) + lane;
 #pragma unroll
     for (int r = 0; r < N; ++r)
@@ -628,7 +633,7 @@ __device__ __forceinline__ void load_map(const MapRef& m, int64_t g, int lane, b
 // (p = 0..N-1) of the lane's column j in v[], and the raw coded map entries.
 //   mapP[g][r][k*N + j] = map[e][r][j] | code,  GP[g][c][r][k*N + j] = G_c(e; r, j)
 // ---------------------------------------------------------------------------
-template <int N, bool M16, class Pre = NoWait>
+template <int N, bool M16, class Pre = NoWait, bool LD = false>
 __device__ __forceinline__ void poisson_group_stored(const MapRef& mref,
                                                      const double* __restrict__ GP,
                                                      const double* __restrict__ u, int64_t g,
@@ -643,7 +648,7 @@ __device__ __forceinline__ void poisson_group_stored(const MapRef& mref,
   constexpr bool SP = N >= SEM_LDS_SPLIT_STORED_N;
   const double* gp = GP + g * (int64_t)(3 * N * LW) + lane;
   double uc[N];
-  load_map<N, M16>(mref, g, lane, in_wave, raw);
+  load_map<N, M16, LD>(mref, g, lane, in_wave, raw);
 #pragma unroll
   for (int r = 0; r < N; ++r) {
     uc[r] = u[raw[r] & GID_MASK];
@@ -837,7 +842,7 @@ __device__ __forceinline__ void nodal_laplacian(const double (&uc)[N], int j, do
 }
 
 // One group of the Poisson action with NODAL geometry (no prefetch).
-template <int N, bool M16, class Pre = NoWait>
+template <int N, bool M16, class Pre = NoWait, bool LD = false>
 __device__ __forceinline__ void poisson_group_nodal(const MapRef& mref,
                                                     const double2* __restrict__ XG,
                                                     const double* __restrict__ u, int64_t g,
@@ -849,7 +854,7 @@ __device__ __forceinline__ void poisson_group_nodal(const MapRef& mref,
                                                     double (&prev)[N], const Pre& pre = Pre()) {
   double uc[N];
   double2 xc[N];
-  load_map<N, M16>(mref, g, lane, in_wave, raw);
+  load_map<N, M16, LD>(mref, g, lane, in_wave, raw);
   gather_x<N>(XG, raw, j, xc);
 #if SEM_NODAL_EARLY_U
   gather_u<N>(u, raw, uc);
@@ -896,8 +901,8 @@ constexpr int CARRY_BUFS = 3;
 // DOT (seam plan, overwrite mode, one DOF per node): dot += u[gid] * value
 // at every STORE -- the node's one and only final value outside the seams.
 template <int N, int NC, bool PRE = false, int CW = ChainWaves<N>::value, bool SEAM = false,
-          bool DOT = false>
-__device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_t (&raw)[N],
+          bool DOT = false, bool LD = false>
+__device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_t (&raw_in)[N],
                                            double (&v)[NC][N], int lane, int wave, int rd,
                                            bool in_wave, double (*carry)[CW][NC][N],
                                            double (&rowc)[NC], int accumulate, bool round_sync,
@@ -906,6 +911,16 @@ __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_
                                            const double* __restrict__ du = nullptr,
                                            double* dot = nullptr) {
   constexpr int LW = Tile<N>::LW;
+  uint32_t raw[N];
+#pragma unroll
+  for (int p = 0; p < N; ++p) {
+    raw[p] = raw_in[p];
+    // LD: the scatter recomputes its byte offsets from the coded map entries
+    // (the compiler would otherwise keep the gather's offsets live through
+    // the whole group next to the entries themselves: a scratch spill per
+    // round at the headline's register limit)
+    if constexpr (LD) asm volatile("" : "+v"(raw[p]));
+  }
   // row carry between rounds (block layout): before any merge, row 0 takes
   // the row n-1 value this lane held back in the previous round
   const bool rc_out = (raw[N - 1] >> CODE_SHIFT) == W_ROWCARRY;
@@ -1007,7 +1022,13 @@ __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nwg) {
 // D copy, SEM_DEO_TRANSPOSED, the static register tables: n = 12 natural 126
 // VGPRs + 108 SGPRs spilled to lanes, 4-wave request 106 and none; n = 15
 // natural 118 / 4 waves, the old 5-wave request 171 / 2 waves; n = 17
-// natural 161 + 42 spilled, 3-wave request 136 and none): SEM_MW_S<n>
+// natural 161 + 42 spilled, 3-wave request 136 and none).  Measured on one
+// MI355X, kernel median ms per action, two alternating runs each
+// (profiles/r04/high_order/): p = 16 198^2 before 0.133 / 0.137, transposed
+// copy + 3-wave request 0.137 / 0.140, transposed + natural 0.131 / 0.131;
+// p = 14 227^2 0.131 / 0.131 -> 0.129 / 0.129 (natural; the old 5-wave
+// request would now give 2 waves); p = 12 263^2 0.128 / 0.124 -> 0.123 /
+// 0.124; p = 10 316^2 0.121 / 0.120 -> 0.120 / 0.116.  SEM_MW_S<n>
 // overrides the request per order (A/B builds); 0 = the default below.
 #ifndef SEM_MW_S12
 #define SEM_MW_S12 0
@@ -1025,7 +1046,7 @@ constexpr int stored_seam_mw(int n) {
   return n == 12 ? (SEM_MW_S12 ? SEM_MW_S12 : (SEM_DEO_TRANSPOSED ? 4 : 1))
        : n == 13 ? (SEM_MW_S13 ? SEM_MW_S13 : 1)
        : n == 15 ? (SEM_MW_S15 ? SEM_MW_S15 : (SEM_DEO_TRANSPOSED ? 1 : 5))
-       : n == 17 ? (SEM_MW_S17 ? SEM_MW_S17 : (SEM_DEO_TRANSPOSED ? 3 : 1))
+       : n == 17 ? (SEM_MW_S17 ? SEM_MW_S17 : 1)
                  : 1;
 }
 template <int N, bool NODAL, bool SEAM = false, bool DOT = false>
@@ -1035,6 +1056,24 @@ struct PoissonMinWaves {
                                : (!NODAL && SEAM && !DOT)            ? stored_seam_mw(N)
                                : (NODAL && N == 5 && !SEAM && !DOT)  ? 6
                                                                      : 1;
+};
+
+// RawLaunder: which column-kernel instantiations launder their map entries
+// and the wide-group lane offset (chain_emit, load_map).  Static register
+// tables (-Rpass-analysis, ScratchSize / VGPRs / waves): the headline
+// k_poisson_apply<9, NODAL, M16, SEAM> 12 B of scratch with a store and a
+// reload every round -> no scratch access in the round loop (one spill
+// before it, one reload in the rare wide-group branch); the n = 9 nodal
+// colour-launch form 12 B -> 0; n = 3 / 5 nodal 65 / 80 -> 62 / 72 VGPRs
+// (7 -> 8 / 6 -> 7 waves); n = 13 / 17 stored seams 106 / 161 -> 102 / 158.
+// Left out: the fused-dot forms (n = 9: 20 -> 36 B of scratch) and n = 11
+// (90 -> 105 VGPRs, 5 -> 4 waves).
+#ifndef SEM_RAW_LAUNDER
+#define SEM_RAW_LAUNDER 1
+#endif
+template <int N, bool DOT>
+struct RawLaunder {
+  static constexpr bool value = SEM_RAW_LAUNDER && !DOT && N != 11;
 };
 
 struct SeamPlan {
@@ -1099,15 +1138,16 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
     using Pre = typename std::conditional<SEAM, NoPrefetch, NoWait>::type;
     const Pre pre{};
     constexpr bool PRE = RmwPrefetch<N>::value > 0 && Pre::prefetch;
+    constexpr bool LD = RawLaunder<N, DOT>::value;
     if constexpr (NODAL)
-      poisson_group_nodal<N, M16>(mref, XG, u, g, lane, j, in_wave, L, LB, D, w, wj, raw, v[0],
-                                  y, accumulate, prev, pre);
+      poisson_group_nodal<N, M16, Pre, LD>(mref, XG, u, g, lane, j, in_wave, L, LB, D, w, wj, raw,
+                                           v[0], y, accumulate, prev, pre);
     else
-      poisson_group_stored<N, M16>(mref, GP, u, g, lane, j, in_wave, L, D, raw, v[0], y,
-                                   accumulate, prev, pre);
+      poisson_group_stored<N, M16, Pre, LD>(mref, GP, u, g, lane, j, in_wave, L, D, raw, v[0], y,
+                                            accumulate, prev, pre);
     SeamOut so;
     if constexpr (SEAM) so.base = sp.buf + sp.colour[chain] * sp.n_node;
-    chain_emit<N, 1, PRE, CW, SEAM, DOT>(y, raw, v, lane, wave, rd, in_wave, carry, rowc,
+    chain_emit<N, 1, PRE, CW, SEAM, DOT, LD>(y, raw, v, lane, wave, rd, in_wave, carry, rowc,
                                          accumulate, sp.round_sync, prev, so, u, &dotv);
   }
   if constexpr (DOT) {

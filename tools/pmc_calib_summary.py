@@ -17,7 +17,8 @@ import sys
 def per_dispatch(path, counter):
     rows = []
     for r in csv.DictReader(open(path)):
-        if r.get("Counter_Name") == counter:
+        # the calibration kernels only (hipMemset's fill kernel runs first)
+        if r.get("Counter_Name") == counter and "k_" in r["Kernel_Name"]:
             rows.append((int(r.get("Dispatch_Id", len(rows))), r["Kernel_Name"],
                          float(r["Counter_Value"]) * 1024.0))
     rows.sort()
