@@ -450,6 +450,13 @@ struct sem_dd {
   bool defer_zero = false;      // the interior's zero list is folded into k_dd_finish
   uint64_t fin_epoch = ~0ull;
   bool loopback = false;        // diagnostic transport (sem_dd_set_loopback)
+  // join of the side stream into the caller's stream: an event wait
+  // (default), or with SEM_DD_WAITVALUE=1 a stream memory operation (the side
+  // stream writes the step number into a signal word, the caller's stream
+  // waits until the word reaches it)
+  bool waitvalue = false;
+  uint64_t* d_flag = nullptr;
+  uint64_t step_id = 0;
   hipStream_t side = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // transport: native RCCL communicator, or caller callbacks
@@ -543,6 +550,7 @@ int build_finish(sem_dd* d) {
         }
     }
   }
+  (void)hipFree(d->d_flag);
   (void)hipFree(d->d_fidx);
   (void)hipFree(d->d_rp);
   (void)hipFree(d->d_rpos);
@@ -655,10 +663,23 @@ int dd_add(sem_dd* d, double* y, hipStream_t st) {
   return SEM_OK;
 }
 
-int dd_finish(sem_dd* d, double* y, hipStream_t st) {
-  const auto t0 = Clock::now();
+// the caller's stream waits for everything enqueued so far on the side stream
+int dd_join(sem_dd* d, hipStream_t st) {
+  if (d->waitvalue && d->d_flag) {
+    ++d->step_id;
+    HIP_TRY(hipStreamWriteValue64(d->side, d->d_flag, d->step_id, 0));
+    HIP_TRY(hipStreamWaitValue64(st, d->d_flag, d->step_id, hipStreamWaitValueGte,
+                                 ~(uint64_t)0));
+    return SEM_OK;
+  }
   HIP_TRY(hipEventRecord(d->ev1, d->side));
   HIP_TRY(hipStreamWaitEvent(st, d->ev1, 0));
+  return SEM_OK;
+}
+
+int dd_finish(sem_dd* d, double* y, hipStream_t st) {
+  const auto t0 = Clock::now();
+  SEM_TRY(dd_join(d, st));
   const int rc = dd_add(d, y, st);
   d->host_ns_finish += ns_since(t0);
   return rc;
@@ -723,8 +744,7 @@ int dd_apply_graphs(sem_dd* d, int op_kind, const double* u, double* y, hipStrea
   if (d->gS) HIP_TRY(hipGraphLaunch(d->gS, d->side));
   HIP_TRY(hipGraphLaunch(d->gM, st));
   SEM_TRY(dd_exchange(d));
-  HIP_TRY(hipEventRecord(d->ev1, d->side));
-  HIP_TRY(hipStreamWaitEvent(st, d->ev1, 0));
+  SEM_TRY(dd_join(d, st));
   if (d->gG) HIP_TRY(hipGraphLaunch(d->gG, st));
   d->n_replays++;
   return SEM_OK;
@@ -1017,6 +1037,18 @@ int sem_dd_create(sem_dd** out, sem_ctx* iface, sem_ctx* interior, int64_t ndof_
   // the device-to-device copies above may still run on the legacy stream
   if (bad(hipDeviceSynchronize())) return fail(SEM_E_HIP, "sem_dd_create: synchronize failed");
   if (const char* e = std::getenv("SEM_DD_GRAPH")) d->graphs = std::atoi(e) != 0;
+  if (const char* e = std::getenv("SEM_DD_WAITVALUE")) {
+    if (std::atoi(e) != 0) {
+      void* f = nullptr;
+      if (hipExtMallocWithFlags(&f, sizeof(uint64_t), hipMallocSignalMemory) == hipSuccess &&
+          hipMemset(f, 0, sizeof(uint64_t)) == hipSuccess && hipDeviceSynchronize() == hipSuccess) {
+        d->d_flag = static_cast<uint64_t*>(f);
+        d->waitvalue = true;
+      } else {
+        (void)hipGetLastError();  // no signal memory: the event join stays
+      }
+    }
+  }
   *out = d;
   return SEM_OK;
 }
@@ -1036,6 +1068,7 @@ void sem_dd_destroy(sem_dd* d) {
   (void)hipFree(d->d_yc);
   (void)hipFree(d->d_send);
   (void)hipFree(d->d_recv);
+  (void)hipFree(d->d_flag);
   (void)hipFree(d->d_fidx);
   (void)hipFree(d->d_rp);
   (void)hipFree(d->d_rpos);

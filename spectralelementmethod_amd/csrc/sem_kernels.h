@@ -628,6 +628,37 @@ __device__ __forceinline__ void load_map(const MapRef& m, int64_t g, int lane, b
   }
 }
 
+// Next-round map prefetch into the caches (SEM_MAP_TOUCH, column kernel with
+// the 16-bit map): the 16-bit entries of group g (N * LW * 2 bytes) and its
+// N bases, read as dwords by the wave's lanes -- no registers are held for
+// the data, only the loaded dwords until MapTouch::done, which an empty asm
+// consumes at the end of the round (a load whose value is unused would be
+// dropped; consuming it earlier would wait for it).  The next round's
+// load_map then finds its lines in L2.
+#ifndef SEM_MAP_TOUCH
+#define SEM_MAP_TOUCH 0
+#endif
+template <int N>
+struct MapTouch {
+  static constexpr int LW = Tile<N>::LW;
+  static constexpr int DW = (N * LW * 2 + 3) / 4;  // dwords of 16-bit entries
+  static constexpr int K = (DW + WAVE - 1) / WAVE;
+  uint32_t t[K + 1];
+  __device__ __forceinline__ void issue(const MapRef& m, int64_t g, int lane) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(m.p16 + g * (int64_t)(N * LW));
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int d = k * WAVE + lane;
+      t[k] = p[d < DW ? d : DW - 1];
+    }
+    t[K] = m.base[g * N + (lane < N ? lane : N - 1)];
+  }
+  __device__ __forceinline__ void done() {
+#pragma unroll
+    for (int k = 0; k <= K; ++k) asm volatile("" ::"v"(t[k]));
+  }
+};
+
 // ---------------------------------------------------------------------------
 // One group of the Poisson action with STORED factors: returns y_e[p][j]
 // (p = 0..N-1) of the lane's column j in v[], and the raw coded map entries.
@@ -1135,6 +1166,10 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
     const int64_t g = (chain * rounds + rd) * CW + wave;
     uint32_t raw[N];
     double v[1][N], prev[N];
+    constexpr bool TOUCH = SEM_MAP_TOUCH && M16 && !DOT;
+    MapTouch<N> touch;
+    if constexpr (TOUCH)
+      if (rd + 1 < rounds) touch.issue(mref, g + CW, lane);
     using Pre = typename std::conditional<SEAM, NoPrefetch, NoWait>::type;
     const Pre pre{};
     constexpr bool PRE = RmwPrefetch<N>::value > 0 && Pre::prefetch;
@@ -1149,6 +1184,8 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
     if constexpr (SEAM) so.base = sp.buf + sp.colour[chain] * sp.n_node;
     chain_emit<N, 1, PRE, CW, SEAM, DOT, LD>(y, raw, v, lane, wave, rd, in_wave, carry, rowc,
                                          accumulate, sp.round_sync, prev, so, u, &dotv);
+    if constexpr (TOUCH)
+      if (rd + 1 < rounds) touch.done();
   }
   if constexpr (DOT) {
     __shared__ double sh[CW];
