@@ -735,18 +735,16 @@ def time_rank(args):
     # the side-stream chain alone (on the caller's stream here)
     side = None
     if op.iface is not None:
+        # as sem_dd_apply's side stream runs it: the interface elements over
+        # the rank's numbering (zero list skipped), then the pack
         pl = op.plan
-        cidx = torch.from_numpy(pl.iface_dofs.view(np.int32)).to(dev)
-        pidx = torch.from_numpy(pl.peer_dofs.view(np.int32)).to(dev)
-        uc = torch.empty(cidx.numel(), dtype=torch.float64, device=dev)
-        yc = torch.empty_like(uc)
-        send = torch.empty(max(1, pidx.numel()), dtype=torch.float64, device=dev)
+        sidx = torch.from_numpy(pl.iface_dofs[pl.peer_dofs].view(np.int32)).to(dev)
+        yc = torch.empty_like(u)
+        send = torch.empty(max(1, sidx.numel()), dtype=torch.float64, device=dev)
 
         def side_chain():
-            _lib.check(lib.sem_gather(_lib.tptr(u), _lib.tptr(cidx), cidx.numel(), _lib.tptr(uc),
-                                      sp))
-            _lib.check(lib.sem_apply(op.iface._ctx, 0, _lib.tptr(uc), _lib.tptr(yc), 0, sp))
-            _lib.check(lib.sem_gather(_lib.tptr(yc), _lib.tptr(pidx), pidx.numel(),
+            _lib.check(lib.sem_apply(op.iface._ctx, 0, _lib.tptr(u), _lib.tptr(yc), 2, sp))
+            _lib.check(lib.sem_gather(_lib.tptr(yc), _lib.tptr(sidx), sidx.numel(),
                                       _lib.tptr(send), sp))
         side = timed(side_chain, K, W)
     iface_elems, interior_elems = op.n_iface_elem, op.n_interior_elem

@@ -362,9 +362,12 @@ int sem_band_lu_solve(int64_t n, int kl, int ku, const int64_t* d_rowptr, const 
  * elements are independent except for the scatter-add, so a rank owns a set
  * of elements and sums only the DOFs it shares with other ranks
  * (SURVEY.md §8(e)).  A sem_dd holds two operator contexts of one rank:
- *   iface     the elements touching a shared node, over a COMPACT numbering
- *             of their n_iface_dofs DOFs (d_iface_dofs[i] = local DOF of
- *             compact DOF i, device uint32);
+ *   iface     the elements touching a shared node, either over the rank's
+ *             own numbering (the context holds ndof_local DOFs: it reads u
+ *             directly and writes a private rank-sized vector) or over a
+ *             COMPACT numbering of their n_iface_dofs DOFs; in both cases
+ *             d_iface_dofs[i] = local DOF of compact DOF i (device uint32,
+ *             the DOFs interface elements touch);
  *   interior  every other element, over the local numbering (ndof_local
  *             DOFs); NULL when the rank has no interior element.
  * iface is NULL (n_iface_dofs = 0, no peers) on a rank that shares no node;

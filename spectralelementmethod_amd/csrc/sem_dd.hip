@@ -21,7 +21,12 @@
 // and direction, never the full vector.
 //
 //   main:  ev0 ------------- interior apply (u -> y) ------------- wait ev1, finish
-//   side:  wait ev0, u_c = u[cidx], iface apply (u_c -> y_c), pack, exchange, ev1
+//   side:  wait ev0, iface apply (u -> y_c), pack, exchange, ev1
+//
+// The interface context may number its nodes like the rank (local
+// numbering, what distributed.py builds: it reads u directly and writes a
+// rank-sized private y_c of which only its own nodes are ever read) or
+// compactly (its own n_iface_dofs; u_c = u[cidx] is gathered first).
 //
 // finish (k_dd_finish, one launch): y[cidx[j]] += y_c[j] + the neighbours'
 // values for compact DOF j, in peer order -- the unpack and the final add of
@@ -396,17 +401,19 @@ __global__ void k_csr_diag(int64_t n, const int64_t* __restrict__ rp, const int3
 // unpack launches added them), then y[i] = v (overwrite flag: a node no
 // interior element touches) or y[i] + v, i = fidx[t] & 0x7fffffff; t >= nc:
 // zero the interior's remaining zero-list DOFs (nodes no element touches)
+// (yc_local: y_c is indexed like y, by local DOF)
 __global__ void k_dd_finish(double* __restrict__ y, const uint32_t* __restrict__ fidx, int64_t nc,
-                            const double* __restrict__ yc, const int32_t* __restrict__ rp,
-                            const uint32_t* __restrict__ rpos, const double* __restrict__ recv,
-                            const uint32_t* __restrict__ fzero, int64_t nz) {
+                            const double* __restrict__ yc, int yc_local,
+                            const int32_t* __restrict__ rp, const uint32_t* __restrict__ rpos,
+                            const double* __restrict__ recv, const uint32_t* __restrict__ fzero,
+                            int64_t nz) {
   for (int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x; t < nc + nz;
        t += (int64_t)gridDim.x * BLK) {
     if (t < nc) {
-      double v = yc[t];
-      for (int32_t k = rp[t]; k < rp[t + 1]; ++k) v += recv[rpos[k]];
       const uint32_t e = fidx[t];
       const uint32_t i = e & 0x7fffffffu;
+      double v = yc[yc_local ? i : t];
+      for (int32_t k = rp[t]; k < rp[t + 1]; ++k) v += recv[rpos[k]];
       y[i] = ((e >> 31) ? 0.0 : y[i]) + v;
     } else {
       y[fzero[t - nc]] = 0.0;
@@ -438,6 +445,9 @@ struct sem_dd {
   uint8_t* d_notown = nullptr;  // local DOFs owned by another rank (global dots)
   double* d_uc = nullptr;
   double* d_yc = nullptr;
+  bool iface_local = false;      // interface context over the local numbering
+  bool iface_skip_zero = false;  // ... whose zero list it never needs (build_finish)
+  uint32_t* d_sidx = nullptr;    // local mode: y_c entry of every exchanged value
   double* d_send = nullptr;
   double* d_recv = nullptr;
   // finish tables (k_dd_finish; built by build_finish for the interior
@@ -450,13 +460,6 @@ struct sem_dd {
   bool defer_zero = false;      // the interior's zero list is folded into k_dd_finish
   uint64_t fin_epoch = ~0ull;
   bool loopback = false;        // diagnostic transport (sem_dd_set_loopback)
-  // join of the side stream into the caller's stream: an event wait
-  // (default), or with SEM_DD_WAITVALUE=1 a stream memory operation (the side
-  // stream writes the step number into a signal word, the caller's stream
-  // waits until the word reaches it)
-  bool waitvalue = false;
-  uint64_t* d_flag = nullptr;
-  uint64_t step_id = 0;
   hipStream_t side = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // transport: native RCCL communicator, or caller callbacks
@@ -508,7 +511,8 @@ inline int64_t ns_since(Clock::time_point t0) {
 // the finish tables for the interior context's current plan (see the file
 // header): rebuilt when its map changes (synchronises the device then)
 int build_finish(sem_dd* d) {
-  const uint64_t ep = d->interior ? sem::ctx_map_epoch(d->interior) : 0;
+  const uint64_t ep = (d->interior ? sem::ctx_map_epoch(d->interior) : 0) * 1000003u +
+                     (d->iface ? sem::ctx_map_epoch(d->iface) : 0);
   if (ep == d->fin_epoch && d->d_fidx) return SEM_OK;
   HIP_TRY(hipDeviceSynchronize());  // nothing in flight reads the old tables
   const int64_t nc = d->nc, ne = n_exchanged(d);
@@ -550,7 +554,7 @@ int build_finish(sem_dd* d) {
         }
     }
   }
-  (void)hipFree(d->d_flag);
+  (void)hipFree(d->d_sidx);
   (void)hipFree(d->d_fidx);
   (void)hipFree(d->d_rp);
   (void)hipFree(d->d_rpos);
@@ -571,6 +575,22 @@ int build_finish(sem_dd* d) {
                       hipMemcpyHostToDevice));
   d->n_fzero = (int64_t)fzero.size();
   d->defer_zero = defer;
+  if (d->iface_local) {
+    // pack reads y_c at the local DOF of every exchanged compact DOF; the
+    // interface context's zero list (every node no interface element
+    // touches) is never needed unless it holds atomic first writers
+    std::vector<uint32_t> sidx((size_t)std::max<int64_t>(ne, 1), 0u);
+    for (int64_t t = 0; t < ne; ++t) sidx[t] = cidx[pidx[t]];
+    (void)hipFree(d->d_sidx);
+    d->d_sidx = nullptr;
+    HIP_TRY(hipMalloc(&d->d_sidx, sidx.size() * sizeof(uint32_t)));
+    HIP_TRY(hipMemcpy(d->d_sidx, sidx.data(), sidx.size() * sizeof(uint32_t),
+                      hipMemcpyHostToDevice));
+    std::vector<uint32_t> zi;
+    bool unref = false;
+    SEM_TRY(sem::ctx_zero_list(d->iface, &zi, &unref));
+    d->iface_skip_zero = unref;
+  }
   d->fin_epoch = ep;
   return SEM_OK;
 }
@@ -581,11 +601,15 @@ int dd_side(sem_dd* d, int op_kind, bool diag, const double* u, hipStream_t sd) 
   if (!d->iface) return SEM_OK;
   if (diag) {
     SEM_TRY(sem_diag(d->iface, op_kind, d->d_yc, sd));
+  } else if (d->iface_local) {
+    SEM_TRY(sem_apply(d->iface, op_kind, u, d->d_yc, d->iface_skip_zero ? SEM_APPLY_SKIP_ZERO : 0,
+                      sd));
   } else {
     SEM_TRY(sem_gather(u, d->d_cidx, d->nc, d->d_uc, sd));
     SEM_TRY(sem_apply(d->iface, op_kind, d->d_uc, d->d_yc, 0, sd));
   }
-  return sem_gather(d->d_yc, d->d_pidx, n_exchanged(d), d->d_send, sd);
+  return sem_gather(d->d_yc, d->iface_local ? d->d_sidx : d->d_pidx, n_exchanged(d), d->d_send,
+                    sd);
 }
 
 // main-stream part: interior elements into y (their zero list deferred to
@@ -657,21 +681,17 @@ int dd_add(sem_dd* d, double* y, hipStream_t st) {
   const int64_t tot = d->nc + (d->defer_zero ? d->n_fzero : 0);
   if (!tot) return SEM_OK;
   hipLaunchKernelGGL(k_dd_finish, dim3(grid_for(tot)), dim3(BLK), 0, st, y, d->d_fidx, d->nc,
-                     d->d_yc, d->d_rp, d->d_rpos, d->d_recv, d->d_fzero,
+                     d->d_yc, d->iface_local ? 1 : 0, d->d_rp, d->d_rpos, d->d_recv, d->d_fzero,
                      d->defer_zero ? d->n_fzero : 0);
   HIP_TRY(hipGetLastError());
   return SEM_OK;
 }
 
 // the caller's stream waits for everything enqueued so far on the side stream
+// (a stream-memory-operation join, hipStreamWriteValue64 on the side stream +
+// hipStreamWaitValue64 on the caller's, hung the step on the MI355X box in
+// round 4 and was removed; the event join stays)
 int dd_join(sem_dd* d, hipStream_t st) {
-  if (d->waitvalue && d->d_flag) {
-    ++d->step_id;
-    HIP_TRY(hipStreamWriteValue64(d->side, d->d_flag, d->step_id, 0));
-    HIP_TRY(hipStreamWaitValue64(st, d->d_flag, d->step_id, hipStreamWaitValueGte,
-                                 ~(uint64_t)0));
-    return SEM_OK;
-  }
   HIP_TRY(hipEventRecord(d->ev1, d->side));
   HIP_TRY(hipStreamWaitEvent(st, d->ev1, 0));
   return SEM_OK;
@@ -984,8 +1004,9 @@ int sem_dd_create(sem_dd** out, sem_ctx* iface, sem_ctx* interior, int64_t ndof_
   if (!iface != (n_iface_dofs == 0) || (!iface && n_peers) || (iface && !d_iface_dofs))
     return fail(SEM_E_INVALID, "sem_dd_create: interface context, DOFs and peers disagree");
   if (!iface && !interior) return fail(SEM_E_INVALID, "sem_dd_create: no elements");
-  if (iface && sem::ctx_ndof(iface) != n_iface_dofs)
-    return fail(SEM_E_INVALID, "interface context must hold exactly n_iface_dofs DOFs");
+  if (iface && sem::ctx_ndof(iface) != n_iface_dofs && sem::ctx_ndof(iface) != ndof_local)
+    return fail(SEM_E_INVALID,
+                "interface context must hold n_iface_dofs (compact) or ndof_local (local) DOFs");
   if (interior && sem::ctx_ndof(interior) != ndof_local)
     return fail(SEM_E_INVALID, "interior context must hold ndof_local DOFs");
   if ((iface && sem::ctx_device(iface) != device) ||
@@ -998,6 +1019,7 @@ int sem_dd_create(sem_dd** out, sem_ctx* iface, sem_ctx* interior, int64_t ndof_
   d->interior = interior;
   d->ndof = ndof_local;
   d->nc = n_iface_dofs;
+  d->iface_local = iface && sem::ctx_ndof(iface) == ndof_local && n_iface_dofs != ndof_local;
   d->off.assign(1, 0);
   for (int k = 0; k < n_peers; ++k) {
     if (h_peer_counts[k] < 0) {
@@ -1014,9 +1036,10 @@ int sem_dd_create(sem_dd** out, sem_ctx* iface, sem_ctx* interior, int64_t ndof_
     return true;
   };
   const int64_t nc1 = std::max<int64_t>(n_iface_dofs, 1);
+  const int64_t nyc = d->iface_local ? ndof_local : nc1;
   if (bad(hipMalloc(&d->d_cidx, nc1 * sizeof(uint32_t))) ||
-      bad(hipMalloc(&d->d_uc, nc1 * sizeof(double))) ||
-      bad(hipMalloc(&d->d_yc, nc1 * sizeof(double))) ||
+      bad(hipMalloc(&d->d_uc, (d->iface_local ? 1 : nc1) * sizeof(double))) ||
+      bad(hipMalloc(&d->d_yc, nyc * sizeof(double))) ||
       bad(hipMalloc(&d->d_pidx, std::max<int64_t>(ne, 1) * sizeof(uint32_t))) ||
       bad(hipMalloc(&d->d_send, std::max<int64_t>(ne, 1) * sizeof(double))) ||
       bad(hipMalloc(&d->d_recv, std::max<int64_t>(ne, 1) * sizeof(double))) ||
@@ -1037,18 +1060,6 @@ int sem_dd_create(sem_dd** out, sem_ctx* iface, sem_ctx* interior, int64_t ndof_
   // the device-to-device copies above may still run on the legacy stream
   if (bad(hipDeviceSynchronize())) return fail(SEM_E_HIP, "sem_dd_create: synchronize failed");
   if (const char* e = std::getenv("SEM_DD_GRAPH")) d->graphs = std::atoi(e) != 0;
-  if (const char* e = std::getenv("SEM_DD_WAITVALUE")) {
-    if (std::atoi(e) != 0) {
-      void* f = nullptr;
-      if (hipExtMallocWithFlags(&f, sizeof(uint64_t), hipMallocSignalMemory) == hipSuccess &&
-          hipMemset(f, 0, sizeof(uint64_t)) == hipSuccess && hipDeviceSynchronize() == hipSuccess) {
-        d->d_flag = static_cast<uint64_t*>(f);
-        d->waitvalue = true;
-      } else {
-        (void)hipGetLastError();  // no signal memory: the event join stays
-      }
-    }
-  }
   *out = d;
   return SEM_OK;
 }
@@ -1068,7 +1079,6 @@ void sem_dd_destroy(sem_dd* d) {
   (void)hipFree(d->d_yc);
   (void)hipFree(d->d_send);
   (void)hipFree(d->d_recv);
-  (void)hipFree(d->d_flag);
   (void)hipFree(d->d_fidx);
   (void)hipFree(d->d_rp);
   (void)hipFree(d->d_rpos);

@@ -1017,9 +1017,13 @@ __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_
 // Workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8 share
 // one L2).  With SEM_XCD_SWIZZLE the chain index is remapped so that each XCD
 // works on one contiguous run of chains (neighbouring chains share node
-// columns of u / x_phys); a bijection of [0, nwg) for any nwg.
+// columns of u / x_phys and the partial 128-B lines of y at their ends); a
+// bijection of [0, nwg) for any nwg.  Headline (1024^2 p = 8, one box, three
+// alternating runs, profiles/r04/headline_ab/, pmc/): 0.632 / 0.634 / 0.646
+// against 0.644 / 0.638 / 0.639 ms per step, PMC fetch 1.99 against 2.07 GB
+// per action (round 1, on colour launches, it measured within +-1 %).
 #ifndef SEM_XCD_SWIZZLE
-#define SEM_XCD_SWIZZLE 0
+#define SEM_XCD_SWIZZLE 1
 #endif
 __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nwg) {
 #if SEM_XCD_SWIZZLE

@@ -506,7 +506,10 @@ class OverlappedOperator(object):
         else:
             self.plan = pl = DDPlan(e2n, n_node, neighbors, dofs_per_node, owned)
             self.n_iface_elem, self.n_interior_elem = pl.iface_elems.size, pl.interior_elems.size
-            self.iface = SEMOperator(p, pl.e2n_iface, nodes[:, pl.iface_nodes], **kw) \
+            # the interface elements over the rank's own numbering: they read
+            # u directly (no gather of a compact copy) and write a private
+            # rank-sized y_c (sem_dd_create's local mode)
+            self.iface = SEMOperator(p, e2n[pl.iface_elems], nodes, **kw) \
                 if pl.iface_elems.size else None
             self.interior = SEMOperator(p, e2n[pl.interior_elems], nodes, **kw) \
                 if pl.interior_elems.size else None
