@@ -653,6 +653,13 @@ def main():
             "batched_elem_matrix_1thread_dof_per_s": cb["batched_elem_matrix"]["dof_per_s"],
             "batched_sumfact_1thread_dof_per_s": cb["batched_sumfact"]["dof_per_s"],
             "batched_sumfact_sample": "256x256 p=%d (%d DOF)" % (p, cb["batched_sumfact"]["ndof"]),
+            "full_host_extrapolated": {
+                "value": fm["dof_per_s"] * (os.cpu_count() or 1) / fm["workers"],
+                "cores": os.cpu_count(),
+                "note": "the %d-process figure scaled linearly to every core of the host: an "
+                        "upper bound, not a measurement (the box's CPU share for one GPU is "
+                        "%d processes; the other cores belong to other GPUs' jobs)" % (
+                            fm["workers"], fm["workers"])},
             "faithful_setup_sec_per_elem": f1["setup_sec_per_elem"],
             "gpu_setup_sec_per_elem": t_setup / max(1, n_elem_local),
         }
@@ -727,7 +734,7 @@ def time_rank(args):
                       host_us_side=d_us["host_ns_side"], host_us_interior=d_us["host_ns_interior"],
                       host_us_finish=d_us["host_ns_finish"])
     # the interior elements alone, as sem_dd_apply launches them
-    flags = 2 if i1["zero_list_in_finish"] else 0  # SEM_APPLY_SKIP_ZERO
+    flags = 2 if i1["zero_list_in_finish"] else 0  # SEM_APPLY_SKIP_ZERO (seam sum included)
     interior = None
     if op.interior is not None:
         interior = timed(lambda: _lib.check(lib.sem_apply(op.interior._ctx, 0, _lib.tptr(u),

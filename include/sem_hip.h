@@ -429,7 +429,8 @@ int sem_copy_async(void* dst, const void* src, int64_t nbytes, void* stream);
  * synchronises with the device makes [11] the device time up to the
  * exchange), eager steps only: [12] enqueueing the side-stream part (gather,
  * interface elements, pack), [13] the interior elements, [14] the finish;
- * [15] the interior's zero list folded into the finish. */
+ * [15] bit 0: the interior's zero list folded into the finish, bit 1: the
+ * interior's seam sum fused with the finish (one launch). */
 int sem_dd_info(sem_dd* dd, int64_t* info, int n_info);
 
 /* Captured step (default off; SEM_DD_GRAPH=1 in the environment turns it

@@ -57,7 +57,10 @@ inline bool seam_auto(int n, int64_t chains_per_colour, int dpn = 1, bool blocks
   // consecutive groups 0.684 ms (profiles/r03/blocks_ab.txt)
   if (blocks && dpn == 1) return true;
   if (dpn == 2) return chains_per_colour <= 512;
-  return n >= 11 || chains_per_colour <= 1024 || (n >= 9 && chains_per_colour <= 2400);
+  // n = 7 (p = 6 at 527^2, 1,929 chains per colour; profiles/r04/p6/):
+  // nodal seams 0.099-0.100 against nodal colours 0.106-0.111 and stored
+  // colours 0.118-0.120 ms per action; stored seams 0.116-0.118
+  return n >= 11 || chains_per_colour <= 1024 || ((n >= 9 || n == 7) && chains_per_colour <= 2400);
 }
 
 struct sem_ctx {
@@ -108,6 +111,7 @@ struct sem_ctx {
   bool round_sync = true;  // a chain writes some node in two rounds (Plan::round_rmw)
   bool seam = false;
   bool seam_dot = false;    // sem_apply_dot fuses u.y into the seam plan's launches
+  bool defer_seam_sum = false;  // sem_apply leaves the seam sum to the caller (sem_dd's fused finish)
   double* d_dot = nullptr;  // u.y partials of sem_apply_dot (chains + seam-sum blocks)
   int64_t n_dot = 0;
   int seam_ns = 0;
@@ -186,7 +190,11 @@ DEO<N> make_deo(const sem_ctx* c) {
 // re-derived from x_phys per node) at p = 1, 2, 4, 5, 8, STORED at p = 3, 6,
 // 7 and above 8.  The p = 3, 5, 6 picks are within 2-3 % (one run each);
 // the clear wins are p = 2, 4, 8 (nodal) and p >= 9 (stored).
-inline bool auto_nodal_order(int n) { return n == 2 || n == 3 || n == 5 || n == 6 || n == 9; }
+// Round 4: p = 6 (n = 7) nodal -- on the seam plan 0.099-0.100 against 0.116-0.118
+// ms stored (527^2, profiles/r04/p6/).
+inline bool auto_nodal_order(int n) {
+  return n == 2 || n == 3 || n == 5 || n == 6 || n == 7 || n == 9;
+}
 
 inline bool nodal_mode(const sem_ctx* c) {
   if (c->mfma) return c->geom_mode == SEM_GEOM_NODAL;  // AUTO: stored factors

@@ -458,6 +458,13 @@ struct sem_dd {
   uint32_t* d_fzero = nullptr;  // interior zero-list DOFs outside the interface
   int64_t n_fzero = 0;
   bool defer_zero = false;      // the interior's zero list is folded into k_dd_finish
+  // the interior's seam sum fused into the finish (sem::ctx_seam_finish):
+  // compact DOF of every interior seam node (or -1), the compact DOFs off
+  // the seams; seam_deferred: this step's interior launch left its seam sum
+  bool seam_fused = false, seam_deferred = false;
+  int32_t* d_seam_cj = nullptr;
+  uint32_t* d_rest = nullptr;
+  int64_t n_rest = 0;
   uint64_t fin_epoch = ~0ull;
   bool loopback = false;        // diagnostic transport (sem_dd_set_loopback)
   hipStream_t side = nullptr;
@@ -536,6 +543,8 @@ int build_finish(sem_dd* d) {
   // interior element touches (no atomic first writers: those must be zero
   // before the interior kernel runs)
   std::vector<uint32_t> fidx(cidx), fzero;
+  std::vector<int32_t> compact((size_t)d->ndof, -1);
+  for (int64_t j = 0; j < nc; ++j) compact[cidx[j]] = (int32_t)j;
   bool defer = false;
   if (d->interior) {
     std::vector<uint32_t> z;
@@ -544,8 +553,6 @@ int build_finish(sem_dd* d) {
     defer = only_unref;
     if (defer && !z.empty()) {
       const int dpn = sem::ctx_dpn(d->interior);
-      std::vector<int32_t> compact((size_t)d->ndof, -1);
-      for (int64_t j = 0; j < nc; ++j) compact[cidx[j]] = (int32_t)j;
       for (const uint32_t node : z)
         for (int c = 0; c < dpn; ++c) {
           const uint32_t dof = node * dpn + c;
@@ -555,6 +562,8 @@ int build_finish(sem_dd* d) {
     }
   }
   (void)hipFree(d->d_sidx);
+  (void)hipFree(d->d_seam_cj);
+  (void)hipFree(d->d_rest);
   (void)hipFree(d->d_fidx);
   (void)hipFree(d->d_rp);
   (void)hipFree(d->d_rpos);
@@ -575,6 +584,35 @@ int build_finish(sem_dd* d) {
                       hipMemcpyHostToDevice));
   d->n_fzero = (int64_t)fzero.size();
   d->defer_zero = defer;
+  // the interior's seam nodes (one DOF per node: DOF = node id) and the
+  // interface DOFs the fused finish handles outside them
+  (void)hipFree(d->d_seam_cj);
+  (void)hipFree(d->d_rest);
+  d->d_seam_cj = nullptr;
+  d->d_rest = nullptr;
+  d->seam_fused = d->interior && defer && sem::ctx_seam_fusable(d->interior);
+  if (d->seam_fused) {
+    std::vector<uint32_t> sg;
+    SEM_TRY(sem::ctx_seam_gids(d->interior, &sg));
+    std::vector<int32_t> cj(sg.size());
+    std::vector<uint8_t> covered((size_t)std::max<int64_t>(nc, 1), 0);
+    for (size_t t = 0; t < sg.size(); ++t) {
+      cj[t] = compact[sg[t]];
+      if (cj[t] >= 0) covered[cj[t]] = 1;
+    }
+    std::vector<uint32_t> rest;
+    for (int64_t j = 0; j < nc; ++j)
+      if (!covered[j]) rest.push_back((uint32_t)j);
+    HIP_TRY(hipMalloc(&d->d_seam_cj, std::max<size_t>(cj.size(), 1) * sizeof(int32_t)));
+    HIP_TRY(hipMalloc(&d->d_rest, std::max<size_t>(rest.size(), 1) * sizeof(uint32_t)));
+    if (!cj.empty())
+      HIP_TRY(hipMemcpy(d->d_seam_cj, cj.data(), cj.size() * sizeof(int32_t),
+                        hipMemcpyHostToDevice));
+    if (!rest.empty())
+      HIP_TRY(hipMemcpy(d->d_rest, rest.data(), rest.size() * sizeof(uint32_t),
+                        hipMemcpyHostToDevice));
+    d->n_rest = (int64_t)rest.size();
+  }
   if (d->iface_local) {
     // pack reads y_c at the local DOF of every exchanged compact DOF; the
     // interface context's zero list (every node no interface element
@@ -615,9 +653,16 @@ int dd_side(sem_dd* d, int op_kind, bool diag, const double* u, hipStream_t sd) 
 // main-stream part: interior elements into y (their zero list deferred to
 // the finish when build_finish allowed it)
 int dd_main(sem_dd* d, int op_kind, bool diag, const double* u, double* y, hipStream_t st) {
+  d->seam_deferred = false;
   if (d->interior) {
     if (diag) return sem_diag(d->interior, op_kind, y, st);
-    return sem_apply(d->interior, op_kind, u, y, d->defer_zero ? SEM_APPLY_SKIP_ZERO : 0, st);
+    const int flags = d->defer_zero ? SEM_APPLY_SKIP_ZERO : 0;
+    if (!d->seam_fused) return sem_apply(d->interior, op_kind, u, y, flags, st);
+    sem::ctx_set_defer_seam_sum(d->interior, true);  // summed by the fused finish
+    const int rc = sem_apply(d->interior, op_kind, u, y, flags, st);
+    sem::ctx_set_defer_seam_sum(d->interior, false);
+    d->seam_deferred = rc == SEM_OK;
+    return rc;
   }
   HIP_TRY(hipMemsetAsync(y, 0, d->ndof * sizeof(double), st));
   return SEM_OK;
@@ -676,8 +721,25 @@ int dd_exchange_impl(sem_dd* d) {
   return fail(SEM_E_STATE, "no transport: call sem_dd_init_rccl or sem_dd_set_transport");
 }
 
-// unpack + final add + deferred zero list in one launch on `st`
+// unpack + final add + deferred zero list in one launch on `st` (with the
+// interior's seam sum when it was deferred)
 int dd_add(sem_dd* d, double* y, hipStream_t st) {
+  if (d->seam_deferred) {
+    sem::DDFinish f{};
+    f.fidx = d->d_fidx;
+    f.nc = d->nc;
+    f.yc = d->d_yc;
+    f.yc_local = d->iface_local ? 1 : 0;
+    f.rp = d->d_rp;
+    f.rpos = d->d_rpos;
+    f.recv = d->d_recv;
+    f.fzero = d->d_fzero;
+    f.nz = d->defer_zero ? d->n_fzero : 0;
+    f.seam_cj = d->d_seam_cj;
+    f.rest = d->d_rest;
+    f.n_rest = d->n_rest;
+    return sem::ctx_seam_finish(d->interior, y, f, st);
+  }
   const int64_t tot = d->nc + (d->defer_zero ? d->n_fzero : 0);
   if (!tot) return SEM_OK;
   hipLaunchKernelGGL(k_dd_finish, dim3(grid_for(tot)), dim3(BLK), 0, st, y, d->d_fidx, d->nc,
@@ -1148,7 +1210,7 @@ int sem_dd_info(sem_dd* d, int64_t* info, int n_info) {
                          d->graphs ? 1 : 0, d->n_captures, d->n_replays,
                          d->host_steps, d->host_ns, d->host_ns_transport,
                          d->host_ns_side, d->host_ns_main, d->host_ns_finish,
-                         d->defer_zero ? 1 : 0};
+                         (d->defer_zero ? 1 : 0) | (d->seam_fused ? 2 : 0)};
   for (int i = 0; i < n_info && i < 16; ++i) info[i] = v[i];
   return SEM_OK;
 }

@@ -167,6 +167,17 @@ int ctx_device(const sem_ctx* c) { return c->device; }
 uint64_t ctx_epoch(const sem_ctx* c) { return c->epoch; }
 int ctx_dpn(const sem_ctx* c) { return c->dpn; }
 uint64_t ctx_map_epoch(const sem_ctx* c) { return c->map_epoch; }
+bool ctx_seam_fusable(const sem_ctx* c) {
+  return c->seam && c->n_seam > 0 && c->dpn == 1 && c->seam_ns >= 1 && c->seam_ns <= 8;
+}
+int ctx_seam_gids(const sem_ctx* c, std::vector<uint32_t>* gids) {
+  gids->assign((size_t)c->n_seam, 0u);
+  if (c->n_seam)
+    HIP_TRY(hipMemcpy(gids->data(), c->d_seam_gid, c->n_seam * sizeof(uint32_t),
+                      hipMemcpyDeviceToHost));
+  return SEM_OK;
+}
+void ctx_set_defer_seam_sum(sem_ctx* c, bool defer) { c->defer_seam_sum = defer; }
 int ctx_zero_list(const sem_ctx* c, std::vector<uint32_t>* nodes, bool* only_unreferenced) {
   nodes->assign((size_t)c->n_zero, 0u);
   *only_unreferenced = c->n_atomic_groups == 0;
@@ -1622,3 +1633,25 @@ int sem_det_inv_2x2(int64_t n, const double* d_mat, double* d_det, double* d_inv
 }
 
 }  // extern "C"
+
+namespace sem {
+int ctx_seam_finish(sem_ctx* c, double* y, const DDFinish& f, hipStream_t st) {
+  const int64_t tot = c->n_seam + f.n_rest + f.nz;
+  if (!tot) return SEM_OK;
+  const dim3 g(semd::grid_for(tot)), b(BLOCK);
+  switch (c->seam_ns) {
+#define SEAM_FIN(K)                                                                         \
+  case K:                                                                                 \
+    hipLaunchKernelGGL(k_seam_dd_finish<K>, g, b, 0, st, y, c->d_seam_gid, c->d_seam_mask, \
+                       c->n_seam, c->d_seam_buf, c->n_node, f);                           \
+    break;
+    SEAM_FIN(1) SEAM_FIN(2) SEAM_FIN(3) SEAM_FIN(4) SEAM_FIN(5) SEAM_FIN(6) SEAM_FIN(7)
+    SEAM_FIN(8)
+#undef SEAM_FIN
+    default:
+      return fail(SEM_E_STATE, "seam plan with more than 8 colours");
+  }
+  HIP_TRY(hipGetLastError());
+  return SEM_OK;
+}
+}  // namespace sem

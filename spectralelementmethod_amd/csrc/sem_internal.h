@@ -5,6 +5,8 @@
 #include <string>
 #include <vector>
 
+#include <hip/hip_runtime.h>
+
 #include "../../include/sem_hip.h"
 
 #define SEM_MAX_ORDER 16
@@ -42,4 +44,30 @@ int ctx_zero_list(const sem_ctx* c, std::vector<uint32_t>* nodes, bool* only_unr
 int ctx_dpn(const sem_ctx* c);
 // bumped by sem_set_map_shared only (the plan, hence the zero list, changed)
 uint64_t ctx_map_epoch(const sem_ctx* c);
+
+// The decomposition's finish fused with the interior context's seam sum
+// (sem_dd.hip): one launch that writes every seam node of the interior
+// (y[g] = its colour slots, as k_seam_sum) plus, for a seam node the
+// interface also touches, the interface value and the neighbours' values;
+// then the remaining interface DOFs and the deferred zero list as k_dd_finish.
+struct DDFinish {
+  const uint32_t* fidx;  // [nc] local DOF | overwrite << 31
+  int64_t nc;
+  const double* yc;      // interface values (indexed like y when yc_local)
+  int yc_local;
+  const int32_t* rp;     // [nc + 1] received values of compact DOF j at rpos[rp[j]..)
+  const uint32_t* rpos;
+  const double* recv;
+  const uint32_t* fzero;  // DOFs to zero
+  int64_t nz;
+  const int32_t* seam_cj;  // [n_seam] compact DOF of the seam node, or -1
+  const uint32_t* rest;    // compact DOFs that are not seam nodes
+  int64_t n_rest;
+};
+// seam plan of a one-DOF-per-node context: true when sem_apply can leave its
+// seam sum to ctx_seam_finish; the seam nodes' ids copied to the host
+bool ctx_seam_fusable(const sem_ctx* c);
+int ctx_seam_gids(const sem_ctx* c, std::vector<uint32_t>* gids);
+void ctx_set_defer_seam_sum(sem_ctx* c, bool defer);
+int ctx_seam_finish(sem_ctx* c, double* y, const DDFinish& f, hipStream_t st);
 }  // namespace sem

@@ -37,6 +37,8 @@
 #include <cstdint>
 #include <type_traits>
 
+#include "sem_internal.h"
+
 namespace semk {
 
 constexpr int WAVE = 64;
@@ -1018,12 +1020,14 @@ __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_
 // one L2).  With SEM_XCD_SWIZZLE the chain index is remapped so that each XCD
 // works on one contiguous run of chains (neighbouring chains share node
 // columns of u / x_phys and the partial 128-B lines of y at their ends); a
-// bijection of [0, nwg) for any nwg.  Headline (1024^2 p = 8, one box, three
-// alternating runs, profiles/r04/headline_ab/, pmc/): 0.632 / 0.634 / 0.646
-// against 0.644 / 0.638 / 0.639 ms per step, PMC fetch 1.99 against 2.07 GB
-// per action (round 1, on colour launches, it measured within +-1 %).
+// bijection of [0, nwg) for any nwg.  Measured on one MI355X
+// (profiles/r04/xcd/, kernel median ms per action, swizzled / dealt): cfg2
+// 256^2 (2,341 chains) 0.042 / 0.044; the headline 1024^2 (9,472) 0.623 -
+// 0.630 / 0.619 with 0.08 GB less PMC fetch; p = 2 / 4 / 6 / 10 / 16 at 1e7
+// DOF 2-6 % slower.  Off: a run-time choice (a kernel argument) costs the
+// headline kernel, at its register limit, a scratch spill per round.
 #ifndef SEM_XCD_SWIZZLE
-#define SEM_XCD_SWIZZLE 1
+#define SEM_XCD_SWIZZLE 0
 #endif
 __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nwg) {
 #if SEM_XCD_SWIZZLE
@@ -1298,6 +1302,66 @@ __global__ void __launch_bounds__(BLOCK)
     __shared__ double sh[BLOCK / WAVE];
     const double t = block_sum_fixed<BLOCK / WAVE>(dotv, sh);
     if (threadIdx.x == 0) dot[blockIdx.x] = t;
+  }
+}
+
+// The decomposition's finish fused with the interior's seam sum
+// (sem::ctx_seam_finish, sem_dd.hip).  t < n: seam node g, s = its slots in
+// colour order as k_seam_sum, plus -- when the interface also touches g --
+// v = y_c + the neighbours' values in peer order (the order of the unfused
+// seam sum, then y = y + v); then the interface DOFs off the seams and the
+// deferred zero list as k_dd_finish.  Bitwise equal to the two launches.
+template <int NS>
+__global__ void __launch_bounds__(BLOCK)
+    k_seam_dd_finish(double* __restrict__ y, const uint32_t* __restrict__ gid,
+                     const uint16_t* __restrict__ mask, int64_t n, const double* __restrict__ buf,
+                     int64_t n_node, const sem::DDFinish f) {
+  auto iface_value = [&](int64_t j, uint32_t i) {
+    double v = f.yc[f.yc_local ? i : j];
+    for (int32_t k = f.rp[j]; k < f.rp[j + 1]; ++k) v += f.recv[f.rpos[k]];
+    return v;
+  };
+  // one buffer resource per colour plane, slot loads issued together
+  // (predicated: an unused slot reads past the range, 0 and no traffic), as
+  // in k_seam_sum
+  __amdgpu_buffer_rsrc_t rb[NS];
+#pragma unroll
+  for (int c = 0; c < NS; ++c)
+    rb[c] = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(buf + c * n_node), 0, 0x80000000,
+                                              0x00020000);
+  const int64_t tot = n + f.n_rest + f.nz;
+  for (int64_t t = blockIdx.x * (int64_t)BLOCK + threadIdx.x; t < tot;
+       t += (int64_t)gridDim.x * BLOCK) {
+    if (t < n) {
+      const uint32_t g = gid[t];
+      const uint32_t m = mask[t];
+      const bool prior = (m & 0x100u) != 0;
+      double b[NS];
+#pragma unroll
+      for (int c = 0; c < NS; ++c) {
+        const uint32_t off = (m & (1u << c)) ? g * 8u : 0x80000000u;
+        b[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rb[c], off, 0, CPOL_NT));
+      }
+      double s = prior ? y[g] : 0.0;
+      bool first = !prior;
+#pragma unroll
+      for (int c = 0; c < NS; ++c)
+        if (m & (1u << c)) {
+          s = first ? b[c] : s + b[c];
+          first = false;
+        }
+      const int32_t j = f.seam_cj[t];
+      if (j >= 0) s = s + iface_value(j, g);
+      y[g] = s;
+    } else if (t < n + f.n_rest) {
+      const uint32_t j = f.rest[t - n];
+      const uint32_t e = f.fidx[j];
+      const uint32_t i = e & 0x7fffffffu;
+      const double v = iface_value(j, i);
+      y[i] = ((e >> 31) ? 0.0 : y[i]) + v;
+    } else {
+      y[f.fzero[t - n - f.n_rest]] = 0.0;
+    }
   }
 }
 

@@ -3,6 +3,8 @@
 // this file once per range, in parallel; spectralelementmethod_amd/_build.py).
 #include "sem_ctx.h"
 
+#include <cstdlib>
+
 #ifndef SEM_N_LO
 #define SEM_N_LO 2
 #endif
@@ -125,6 +127,7 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
     // dot_out: u.y fused into the two launches (partials, then a fixed-order sum)
     double* part = dot_out ? c->d_dot : nullptr;
     launch_chains<N, true>(c, op_kind, nodal, u, y, acc, lin, c0, c1, D, w, st, part);
+    if (c->defer_seam_sum && !dot_out) return SEM_OK;  // the caller's fused finish sums them
     const int rc = launch_seam_sum(c, y, acc, st, dot_out ? u : nullptr,
                                    part ? part + (c1 - c0) : nullptr);
     if (rc || !dot_out) return rc;

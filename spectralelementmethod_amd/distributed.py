@@ -591,7 +591,8 @@ class OverlappedOperator(object):
                     host_us_per_apply_excl_transport=(v[10] - v[11]) / steps / 1e3,
                     host_ns_side=v[12], host_ns_interior=v[13], host_ns_finish=v[14],
                     host_us_side=v[12] / steps / 1e3, host_us_interior=v[13] / steps / 1e3,
-                    host_us_finish=v[14] / steps / 1e3, zero_list_in_finish=bool(v[15]))
+                    host_us_finish=v[14] / steps / 1e3, zero_list_in_finish=bool(v[15] & 1),
+                    seam_sum_in_finish=bool(v[15] & 2))
 
     def set_graphs(self, enable):
         """Captured step on / off (sem_dd_set_graphs)."""
