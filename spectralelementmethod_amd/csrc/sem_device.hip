@@ -319,6 +319,63 @@ struct Plan {
   bool seam_failed = false;
 };
 
+// Workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8 share
+// one L2).  For a seam-plan launch of at most SEM_CHAIN_SWIZZLE_MAX chains
+// (default 2,400) the planner reorders the chains so that workgroup b runs
+// chain q(b) = x * (nch / 8) + min(x, nch % 8) + b / 8 (x = b % 8): each XCD
+// then works on one contiguous run of chains, which share node columns of u
+// and x_phys and the partial lines of y at their ends.  A permutation of the
+// chain blocks of the packed arrays (slots, element positions, chain
+// colours); node-indexed data and the seam sums are untouched, so results
+// are bitwise those of the unpermuted plan.  Measured as a kernel-side
+// remap (profiles/r04/xcd/, kernel median ms per action): cfg2 256^2 (2,341
+// chains) 0.042 against 0.044; on the larger launches (4,993 - 9,472 chains)
+// neutral to 6 % slower, hence the bound.  (Done in the kernel, as a
+// run-time choice, it cost the headline kernel a scratch spill per round.)
+int64_t chain_swizzle_max() {
+  const char* e = std::getenv("SEM_CHAIN_SWIZZLE_MAX");
+  return e ? (int64_t)std::atoll(e) : (int64_t)2400;
+}
+
+void chain_swizzle(Plan& P, int n, int rounds) {
+  if (P.colour_start.size() != 2) return;
+  const int64_t nch = P.colour_start[1] - P.colour_start[0];
+  if (nch < 16 || nch > chain_swizzle_max()) return;
+  const int64_t spc = (int64_t)rounds * chain_waves_of(n);  // slots per chain
+  if (P.n_slots != nch * spc) return;
+  constexpr int64_t NX = 8;
+  const int64_t q = nch / NX, r = nch % NX;
+  std::vector<int64_t> perm(nch), inv(nch);  // new position b <- old chain perm[b]
+  for (int64_t b = 0; b < nch; ++b) {
+    const int64_t x = b % NX, k = b / NX;
+    perm[b] = x * q + (x < r ? x : r) + k;
+    inv[perm[b]] = b;
+  }
+  const size_t per_slot = P.mapP.size() / (size_t)P.n_slots;
+  std::vector<uint32_t> mp(P.mapP.size());
+  std::vector<uint8_t> fill(P.slot_fill.size());
+  for (int64_t b = 0; b < nch; ++b) {
+    std::copy(P.mapP.begin() + perm[b] * spc * per_slot,
+              P.mapP.begin() + (perm[b] + 1) * spc * per_slot, mp.begin() + b * spc * per_slot);
+    std::copy(P.slot_fill.begin() + perm[b] * spc, P.slot_fill.begin() + (perm[b] + 1) * spc,
+              fill.begin() + b * spc);
+  }
+  P.mapP.swap(mp);
+  P.slot_fill.swap(fill);
+  const int epw = epw_of(n);
+  for (int& ep : P.epos) {
+    if (ep < 0) continue;
+    const int64_t slot = ep / epw, k = ep % epw;
+    const int64_t ch = slot / spc, within = slot % spc;
+    ep = (int)((inv[ch] * spc + within) * epw + k);
+  }
+  if ((int64_t)P.chain_colour.size() == nch) {
+    std::vector<uint8_t> cc(nch);
+    for (int64_t b = 0; b < nch; ++b) cc[b] = P.chain_colour[perm[b]];
+    P.chain_colour.swap(cc);
+  }
+}
+
 // groups of EPW consecutive elements, chains of CH consecutive groups
 void groups_consecutive(int64_t n_elem, int epw, int CH, std::vector<int64_t>& gel) {
   const int64_t n_groups = (n_elem + epw - 1) / epw;
@@ -1201,6 +1258,8 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
   }
   if (rc) return rc;
   if (P.blocks) rounds = P.block_rounds;
+  // XCD-contiguous chain order for small seam-plan launches (chain_swizzle)
+  if (!mfma && P.seam) chain_swizzle(P, n, rounds);
   // element-coloured fallback for orders that defeat the chain patterns
   // (SEM_PLAN=1 forces it, SEM_PLAN=0 forbids it)
   const char* penv = std::getenv("SEM_PLAN");
