@@ -590,7 +590,11 @@ int build_finish(sem_dd* d) {
   (void)hipFree(d->d_rest);
   d->d_seam_cj = nullptr;
   d->d_rest = nullptr;
-  d->seam_fused = d->interior && defer && sem::ctx_seam_fusable(d->interior);
+  // SEM_DD_FUSE_SEAM=0: the interior's own seam-sum launch, then k_dd_finish
+  // (A/B and the bitwise test of the fused form)
+  const char* fe = std::getenv("SEM_DD_FUSE_SEAM");
+  d->seam_fused = d->interior && defer && sem::ctx_seam_fusable(d->interior) &&
+                  !(fe && std::atoi(fe) == 0);
   if (d->seam_fused) {
     std::vector<uint32_t> sg;
     SEM_TRY(sem::ctx_seam_gids(d->interior, &sg));

@@ -601,11 +601,22 @@ __device__ __forceinline__ void load_map(const MapRef& m, int64_t g, int lane, b
     const uint16_t* mp = m.p16 + g * (int64_t)(N * LW) + (in_wave ? lane : LW - 1);
     const uint32_t* bp = m.base + g * N;  // g is wave-uniform: scalar loads
     uint32_t o[N], b[N];
+#if SEM_DIAG_NO_MAP16_LOAD
+    // DIAGNOSTIC (timing only, wrong results): the 16-bit entries are not
+    // read; canonical structured offsets, every entry a plain store
+    (void)mp;
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      const int kk = lane / N, jj = lane - kk * N;
+      o[r] = in_wave ? (uint32_t)(kk * (N - 1) + jj) : (W_SKIP << M16_CODE_SHIFT);
+    }
+#else
 #pragma unroll
     for (int r = 0; r < N; ++r) {
       const uint32_t t = mp[r * LW];
       o[r] = in_wave ? t : (W_SKIP << M16_CODE_SHIFT);
     }
+#endif
 #pragma unroll
     for (int r = 0; r < N; ++r) b[r] = bp[r];
 #pragma unroll

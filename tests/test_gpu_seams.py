@@ -151,3 +151,50 @@ def test_mfma17_seams_match_colour_launches(gpu, gll, monkeypatch, nex, ney):
     ref, ext = _oracle(gll, nodes, e2n, p, u)
     y = ys.cpu().numpy()
     assert rel_l2(y, ext) <= max(1.5 * rel_l2(ref, ext), TOL)
+
+
+@pytest.mark.parametrize("geometry", ["nodal", "stored"])
+def test_chain_swizzle_is_bitwise_neutral(gpu, monkeypatch, geometry):
+    """The planner's XCD-contiguous chain order (chain_swizzle in
+    csrc/sem_device.hip, seam launches of <= 2,400 chains) only permutes the
+    chain blocks of the packed arrays: the action equals the unpermuted
+    plan's bit for bit, with nodal and with stored (packed by element
+    position) factors."""
+    from spectralelementmethod_amd import meshgen
+    from spectralelementmethod_amd.operators import SEMOperator
+    nodes, e2n = meshgen.structured_square(20, 112, 8, warp=0.05)  # whole chains per column
+    u = torch.from_numpy(np.random.default_rng(4).standard_normal(nodes.shape[1])).to(gpu)
+    monkeypatch.setenv("SEM_SEAM", "1")
+    monkeypatch.setenv("SEM_CHAIN_SWIZZLE_MAX", "0")
+    ref = SEMOperator(8, e2n, nodes, device=gpu, kernel="column", geometry=geometry)
+    monkeypatch.setenv("SEM_CHAIN_SWIZZLE_MAX", "100000")
+    swz = SEMOperator(8, e2n, nodes, device=gpu, kernel="column", geometry=geometry)
+    assert swz.plan_info()["plan"] == "chains-seams"
+    assert torch.equal(ref.apply(u), swz.apply(u))
+
+
+@pytest.mark.parametrize("rank", [0, 2])
+def test_dd_fused_seam_finish_is_bitwise(gpu, monkeypatch, rank):
+    """sem_dd's finish fused with the interior's seam sum (one launch) equals
+    the interior's own seam sum followed by k_dd_finish bit for bit, on one
+    rank of a 4-strip split with the loopback transport (both peers'
+    exchanges exercised; the values are not the global action, the same in
+    both forms)."""
+    from spectralelementmethod_amd.distributed import OverlappedOperator, StripPartition
+    part = StripPartition(24, 112, 8, 4, rank)  # whole chains per element column
+    nodes, e2n = part.local_mesh(0.05)
+    u = torch.from_numpy(np.random.default_rng(5).standard_normal(nodes.shape[1])).to(gpu)
+    monkeypatch.setenv("SEM_SEAM", "1")
+    out = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("SEM_DD_FUSE_SEAM", fuse)
+        op = OverlappedOperator(8, nodes, e2n, part.neighbors, 1, gpu, owned=part.owned,
+                                transport="loopback", world=1, rank=0, decompose=True)
+        y = torch.full_like(u, 7.0)
+        op.step(u, y)
+        op.step(u, y)
+        torch.cuda.synchronize()
+        out[fuse] = (y.clone(), op.dd_info())
+        op.close()
+    assert out["1"][1]["seam_sum_in_finish"] and not out["0"][1]["seam_sum_in_finish"]
+    assert torch.equal(out["1"][0], out["0"][0])
