@@ -150,7 +150,12 @@ int sem_set_map_shared(sem_ctx* ctx, const uint32_t* d_e2n, const uint8_t* d_nod
  * stacked lines of elements, and the node row between two rounds is carried
  * in registers; SEM_BLOCK_ROUNDS=R in the environment forces R rounds, 0
  * turns it off), [24] the packed map entries so carried.
- * Writes min(n_info, 25) values. */
+ * [25] 1 when the Poisson column kernels take D as compile-time constants:
+ * sem_set_basis found the context's D equal to the baked standard GLL D
+ * bit for bit (csrc/deo_const.h; 16-bit maps) at an order where that is
+ * measured faster; SEM_CONST_D=0 / 1 in the environment
+ * turns it off / on at every order.
+ * Writes min(n_info, 26) values. */
 int sem_plan_info(sem_ctx* ctx, int64_t* info, int n_info);
 
 /* How the Poisson action obtains its geometric factors.

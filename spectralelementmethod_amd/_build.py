@@ -16,7 +16,15 @@ SOURCES = ["sem_device.hip", "sem_dd.hip", "sem_sc.hip", "sem_basis.cpp"]
 # (lo, hi) order ranges of sem_launch.hip, balanced by compile time (the
 # unrolled column kernels grow with n)
 LAUNCH_RANGES = [(2, 5), (6, 8), (9, 9), (10, 11), (12, 13), (14, 15), (16, 16), (17, 17)]
-DEPS = SOURCES + ["sem_launch.hip", "sem_internal.h", "sem_kernels.h", "sem_ctx.h", "gll_table.h"]
+# the constant-D Poisson launches (sem_launch_cd.hip), per range with extra
+# compiler flags: machine LICM off where hoisting the materialised
+# coefficients out of the round loop costs registers / occupancy
+# (profiles/r04/const_d/)
+NO_LICM = ("-mllvm", "-disable-machine-licm")
+LAUNCH_CD_RANGES = [((2, 5), ()), ((6, 8), ()), ((9, 9), ()), ((10, 11), ()), ((12, 13), ()),
+                    ((14, 15), ()), ((16, 16), ()), ((17, 17), NO_LICM)]
+DEPS = SOURCES + ["sem_launch.hip", "sem_launch_cd.hip", "sem_internal.h", "sem_kernels.h", "sem_ctx.h", "gll_table.h",
+                  "deo_const.h"]
 ARCH = os.environ.get("SEM_OFFLOAD_ARCH", "gfx950")
 
 
@@ -45,7 +53,8 @@ def _jobs():
 
 def build(force=False, verbose=True, out=None, defines=(), orders=None):
     """Compile the library (``out`` and ``defines`` build diagnostic
-    variants, e.g. for A/B timing in one process; ``orders`` = (lo, hi)
+    variants, e.g. for A/B timing in one process; a ``defines`` entry that
+    starts with "-" is passed to hipcc as is; ``orders`` = (lo, hi)
     restricts the kernel instantiations to those orders)."""
     out = out or LIB_PATH
     if not force and out == LIB_PATH and not needs_rebuild():
@@ -55,12 +64,19 @@ def build(force=False, verbose=True, out=None, defines=(), orders=None):
     common = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17",
               "-munsafe-fp-atomics", "-Wall", "-Wno-unused-result",
               "-Wno-pass-failed",  # occupancy requests the allocator meets lower (PoissonMinWaves)
-              *["-D" + d for d in defines]]
+              *[d if d.startswith("-") else "-D" + d for d in defines]]
     units = [(s, [], os.path.join(objdir, s + ".o")) for s in SOURCES]
     ranges = [orders] if orders else LAUNCH_RANGES
     for lo, hi in ranges:
         units.append(("sem_launch.hip", ["-DSEM_N_LO=%d" % lo, "-DSEM_N_HI=%d" % hi],
                       os.path.join(objdir, "sem_launch_%d_%d.o" % (lo, hi))))
+    for (lo, hi), flags in LAUNCH_CD_RANGES:
+        if orders and (hi < orders[0] or lo > orders[1]):
+            continue
+        lo, hi = (max(lo, orders[0]), min(hi, orders[1])) if orders else (lo, hi)
+        units.append(("sem_launch_cd.hip", ["-DSEM_N_LO=%d" % lo, "-DSEM_N_HI=%d" % hi,
+                                            *flags],
+                      os.path.join(objdir, "sem_launch_cd_%d_%d.o" % (lo, hi))))
 
     headers = [os.path.join(CSRC, d) for d in DEPS if d.endswith(".h")]
     headers.append(os.path.join(os.path.dirname(PKG_DIR), "include", "sem_hip.h"))

@@ -99,6 +99,9 @@ struct sem_ctx {
   // need different plans and packed layouts)
   int kernel = SEM_KERNEL_AUTO;
   bool mfma = false;
+  // D is the standard GLL D of deo_const.h bit for bit: the Poisson column
+  // kernels take it as compile-time constants (SEM_CONST_D=0 disables)
+  bool const_d = false;
   bool ecol = false;  // column kernel on the element-coloured plan
   double2* d_XG = nullptr;
   uint32_t* d_owner = nullptr;
@@ -196,6 +199,11 @@ inline bool auto_nodal_order(int n) {
   return n == 2 || n == 3 || n == 5 || n == 6 || n == 7 || n == 9;
 }
 
+// Orders whose Poisson column kernels run with D as compile-time constants
+// when the basis is the standard GLL one (sem_set_basis):
+// measured per order on MI355X at ~1e7 DOF (profiles/r04/const_d/).
+inline bool const_d_order(int n) { return n >= 11; }
+
 inline bool nodal_mode(const sem_ctx* c) {
   if (c->mfma) return c->geom_mode == SEM_GEOM_NODAL;  // AUTO: stored factors
   return c->geom_mode == SEM_GEOM_NODAL ||
@@ -255,6 +263,24 @@ int launch_geom_n(sem_ctx* c, const double* nodes, int op_kind, double* GP, doub
                   const double2* XGin, hipStream_t st);
 template <int N>
 int upload_deo(sem_ctx* c);
+// one launch of the Poisson column kernel with D as compile-time constants
+// (16-bit map; sem_launch_cd.hip, a translation unit of its own so that its
+// compiler flags are chosen per order, csrc/../_build.py)
+struct PoissonLaunch {
+  dim3 g, b;
+  hipStream_t st;
+  MapRef mr;
+  const double* GP;
+  const double2* XG;
+  const double* u;
+  double* y;
+  int64_t c0, c1;
+  int rounds, acc;
+  SeamPlan sp;
+};
+template <int N>
+void launch_poisson_const_d(const PoissonLaunch& L, bool nodal, bool seam, bool dot,
+                            const WVec<N>& w);
 // the seam sums of the seam plan (sem_device.hip); du / dot: also the u.y
 // partials of the seam nodes, one per block of seam_sum_blocks(c)
 int launch_seam_sum(sem_ctx* c, double* y, int acc, hipStream_t st, const double* du = nullptr,

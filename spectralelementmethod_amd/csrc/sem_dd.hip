@@ -306,26 +306,39 @@ __global__ void __launch_bounds__(BLK)
   write_partials(s0, s1, partial);
 }
 
-// the rest of the iteration in one pass: x += alpha p with the p of this
-// iteration, then p = z + beta p with z = r / diag (0 on Dirichlet DOFs:
-// dinv is 0 there); beta = rz_new / rz_old on the device
-template <int V>
+// the rest of the iteration in one pass, with z = r / diag (0 on Dirichlet
+// DOFs: dinv is 0 there) and beta = rz_new / rz_old on the device.
+//   STEP_NOW:   x += alpha p, then p = z + beta p (in place);
+//   STEP_DEFER: pout = z + beta p, x untouched; alpha saved to *alpha_io;
+//   STEP_PAIR:  x += alpha' pout + alpha p (alpha' = *alpha_io, pout = the
+//               previous iteration's p), then pout = z + beta p.
+// DEFER / PAIR alternate (SEM_PCG_X_PAIRS, default): x is read and written
+// every second iteration, 40 instead of 44 bytes per DOF and iteration over
+// the two, and x = fma(alpha, p, fma(alpha', p', x)) is bitwise the two
+// single updates in order.
+enum { STEP_NOW = 0, STEP_DEFER = 1, STEP_PAIR = 2 };
+template <int V, int MODE>
 __global__ void __launch_bounds__(BLK)
-    k_cg_step(double* __restrict__ x, double* __restrict__ p, const double* __restrict__ r,
-              const dinv_t* __restrict__ dinv, const double* __restrict__ rz_new,
-              const double* __restrict__ rz_old, const double* __restrict__ pq, int64_t n) {
+    k_cg_step(double* __restrict__ x, double* __restrict__ p, double* __restrict__ pout,
+              const double* __restrict__ r, const dinv_t* __restrict__ dinv,
+              const double* __restrict__ rz_new, const double* __restrict__ rz_old,
+              const double* __restrict__ pq, double* __restrict__ alpha_io, int64_t n) {
   constexpr int U = UNR / V;
   const double alpha = cg_alpha(rz_old, pq);
+  const double alpha_prev = MODE == STEP_PAIR ? *alpha_io : 0.0;
   const double den = *rz_old;
   const double beta = den != 0.0 ? *rz_new / den : 0.0;
+  if (MODE == STEP_DEFER && blockIdx.x == 0 && threadIdx.x == 0) *alpha_io = alpha;
+  double* dst = MODE == STEP_NOW ? p : pout;
   const int64_t nv = n / V, st = (int64_t)gridDim.x * BLK;
   for (int64_t i0 = blockIdx.x * (int64_t)BLK + threadIdx.x; i0 < nv; i0 += U * st) {
-    double xv[U][V], pv[U][V], rv[U][V];
+    double xv[U][V], pv[U][V], rv[U][V], av[U][V];
     dinv_t dv[U][V];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t i = i0 + u * st < nv ? i0 + u * st : 0;
-      ldv<V>(x, i, xv[u]);
+      if (MODE != STEP_DEFER) ldv<V>(x, i, xv[u]);
+      if (MODE == STEP_PAIR) ldv<V>(pout, i, av[u]);
       ldv<V>(p, i, pv[u]);
       ldv<V>(r, i, rv[u]);
       ldv<V>(dinv, i, dv[u]);
@@ -335,18 +348,30 @@ __global__ void __launch_bounds__(BLK)
       if (i0 + u * st >= nv) continue;
 #pragma unroll
       for (int e = 0; e < V; ++e) {
-        xv[u][e] = fma(alpha, pv[u][e], xv[u][e]);
+        if (MODE == STEP_PAIR) xv[u][e] = fma(alpha_prev, av[u][e], xv[u][e]);
+        if (MODE != STEP_DEFER) xv[u][e] = fma(alpha, pv[u][e], xv[u][e]);
         pv[u][e] = fma(beta, pv[u][e], pc_z(rv[u][e], dv[u][e]));
       }
-      stv<V>(x, i0 + u * st, xv[u]);
-      stv<V>(p, i0 + u * st, pv[u]);
+      if (MODE != STEP_DEFER) stv<V>(x, i0 + u * st, xv[u]);
+      stv<V>(dst, i0 + u * st, pv[u]);
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0)
     for (int64_t t = nv * V; t < n; ++t) {
-      x[t] = fma(alpha, p[t], x[t]);
-      p[t] = fma(beta, p[t], pc_z(r[t], dinv[t]));
+      double xt = MODE != STEP_DEFER ? x[t] : 0.0;
+      if (MODE == STEP_PAIR) xt = fma(alpha_prev, pout[t], xt);
+      if (MODE != STEP_DEFER) x[t] = fma(alpha, p[t], xt);
+      dst[t] = fma(beta, p[t], pc_z(r[t], dinv[t]));
     }
+}
+
+// the update of x still owed after a STEP_DEFER iteration: x += alpha' p'
+__global__ void __launch_bounds__(BLK)
+    k_cg_flush_x(double* __restrict__ x, const double* __restrict__ pp,
+                 const double* __restrict__ alpha_io, int64_t n) {
+  const double a = *alpha_io;
+  for (int64_t t = blockIdx.x * (int64_t)BLK + threadIdx.x; t < n; t += (int64_t)gridDim.x * BLK)
+    x[t] = fma(a, pp[t], x[t]);
 }
 
 // fixed-order sum of the partials: out[0..nd) (deterministic run to run);
@@ -913,6 +938,13 @@ struct PcgScratch {
 const bool g_sync_each = std::getenv("SEM_PCG_SYNC_EACH") != nullptr;  // diagnostic
 // SEM_PCG_SEPARATE_PQ=1: the p.q pass after the action even on one GPU (A/B)
 const bool g_separate_pq = std::getenv("SEM_PCG_SEPARATE_PQ") != nullptr;
+// SEM_PCG_X_EVERY=1: x updated every iteration (STEP_NOW; A/B against the
+// default pairs, bitwise the same x)
+// (read per solve)
+bool pcg_x_pairs() {
+  const char* e = std::getenv("SEM_PCG_X_EVERY");
+  return !(e && std::atoi(e) == 1);
+}
 
 int pcg_run(const PcgOp& op, int kind, const double* b, double* x, const uint8_t* dir,
             const uint8_t* notown, double rtol, int max_iter, int check, int* iters,
@@ -925,9 +957,11 @@ int pcg_run(const PcgOp& op, int kind, const double* b, double* x, const uint8_t
   DeviceGuard g(op.device);
   const int64_t n = op.n;
   PcgScratch s;
-  // r, p, q, 1/diag; rows padded to 32 doubles (16-byte vector accesses)
+  const bool g_x_pairs = pcg_x_pairs();
+  // r, p, q, 1/diag, the second p buffer (x updated every second iteration);
+  // rows padded to 32 doubles (16-byte vector accesses)
   const int64_t nn = (n + 31) / 32 * 32;
-  HIP_TRY(hipMalloc(&s.base, 4 * nn * sizeof(double)));
+  HIP_TRY(hipMalloc(&s.base, (g_x_pairs ? 5 : 4) * nn * sizeof(double)));
   HIP_TRY(hipMalloc(&s.flags, n));
   HIP_TRY(hipMalloc(&s.pc, nn * sizeof(dinv_t)));
   // partials [2][RED_BLOCKS], then scalars: T0 = (rz, rr), T1 = (rz, rr), pq
@@ -938,11 +972,14 @@ int pcg_run(const PcgOp& op, int kind, const double* b, double* x, const uint8_t
   double* p = r + nn;
   double* q = p + nn;
   double* dg = q + nn;
+  double* p_alt = g_x_pairs ? dg + nn : nullptr;  // the other p buffer
   // x is the caller's: 16-byte aligned -> the paired kernels
   const bool v2 = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
   double* partial = s.red;
   double* T[2] = {s.red + 2 * RED_BLOCKS, s.red + 2 * RED_BLOCKS + 2};
   double* pq = s.red + 2 * RED_BLOCKS + 4;
+  double* alpha_saved = s.red + 2 * RED_BLOCKS + 5;  // alpha of a STEP_DEFER iteration
+  bool x_owed = false;  // x += alpha_saved * p_alt still to do
   const int gb = grid_for(n, RED_BLOCKS);
   const bool multi = op.dd && op.dd->world > 1;  // dots need an all-reduce
   hipLaunchKernelGGL(k_cg_flags, dim3(grid_for(n)), dim3(BLK), 0, st, dir, notown, n, s.flags);
@@ -984,12 +1021,27 @@ int pcg_run(const PcgOp& op, int kind, const double* b, double* x, const uint8_t
         SEM_TRY(dd_allreduce(op.dd, T[nw], 2, st));
         hipLaunchKernelGGL(k_cg_record, dim3(1), dim3(WV), 0, st, T[nw] + 1, s.hist + it + 1);
       }
-      if (v2)
-        hipLaunchKernelGGL(k_cg_step<2>, dim3(gb), dim3(BLK), 0, st, x, p, r, s.pc, T[nw], T[o], pq,
-                           n);
-      else
-        hipLaunchKernelGGL(k_cg_step<1>, dim3(gb), dim3(BLK), 0, st, x, p, r, s.pc, T[nw], T[o], pq,
-                           n);
+      if (!g_x_pairs) {
+        if (v2)
+          hipLaunchKernelGGL((k_cg_step<2, STEP_NOW>), dim3(gb), dim3(BLK), 0, st, x, p, nullptr, r,
+                             s.pc, T[nw], T[o], pq, nullptr, n);
+        else
+          hipLaunchKernelGGL((k_cg_step<1, STEP_NOW>), dim3(gb), dim3(BLK), 0, st, x, p, nullptr, r,
+                             s.pc, T[nw], T[o], pq, nullptr, n);
+      } else if (!x_owed) {  // p_alt = z + beta p; x waits for the next iteration
+        hipLaunchKernelGGL((k_cg_step<2, STEP_DEFER>), dim3(gb), dim3(BLK), 0, st, x, p, p_alt, r,
+                           s.pc, T[nw], T[o], pq, alpha_saved, n);
+      } else if (v2) {  // x += alpha' p_alt + alpha p; p_alt = z + beta p
+        hipLaunchKernelGGL((k_cg_step<2, STEP_PAIR>), dim3(gb), dim3(BLK), 0, st, x, p, p_alt, r,
+                           s.pc, T[nw], T[o], pq, alpha_saved, n);
+      } else {
+        hipLaunchKernelGGL((k_cg_step<1, STEP_PAIR>), dim3(gb), dim3(BLK), 0, st, x, p, p_alt, r,
+                           s.pc, T[nw], T[o], pq, alpha_saved, n);
+      }
+      if (g_x_pairs) {  // the new p is in p_alt; the old one is the owed update's
+        std::swap(p, p_alt);
+        x_owed = !x_owed;
+      }
       HIP_TRY(hipGetLastError());
       if (g_sync_each) HIP_TRY(hipDeviceSynchronize());  // diagnostic
       ++it;
@@ -1002,6 +1054,10 @@ int pcg_run(const PcgOp& op, int kind, const double* b, double* x, const uint8_t
       if (!std::isfinite(rr_last)) return fail(SEM_E_INVALID, "PCG: non-finite residual");
       if (rr_last <= tol2) done = true;
     }
+  }
+  if (x_owed) {
+    hipLaunchKernelGGL(k_cg_flush_x, dim3(grid_for(n)), dim3(BLK), 0, st, x, p_alt, alpha_saved, n);
+    HIP_TRY(hipGetLastError());
   }
   if (iters) *iters = it;
   if (relres) *relres = rr0 > 0.0 ? std::sqrt(rr_last / rr0) : 0.0;

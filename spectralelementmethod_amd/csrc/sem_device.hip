@@ -1197,6 +1197,14 @@ int sem_set_basis(sem_ctx* c, const double* hD, const double* hw) {
   c->epoch++;
   std::memcpy(c->hD, hD, sizeof(double) * n * n);
   std::memcpy(c->hw, hw, sizeof(double) * n);
+  {
+    const double* kd = sem_deo_const_d(n);
+    // SEM_CONST_D: unset = the per-order choice (const_d_order), 0 = never,
+    // 1 = wherever D matches
+    const char* e = std::getenv("SEM_CONST_D");
+    const bool want = e ? e[0] == '1' : const_d_order(n);
+    c->const_d = want && kd && std::memcmp(kd, hD, sizeof(double) * n * n) == 0;
+  }
   HIP_TRY(hipMemcpy(c->d_D, hD, sizeof(double) * n * n, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(c->d_w, hw, sizeof(double) * n, hipMemcpyHostToDevice));
   int rc = SEM_OK;
@@ -1381,29 +1389,30 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
 int sem_plan_info(sem_ctx* c, int64_t* info, int n_info) {
   if (!c || !info || n_info < 1) return fail(SEM_E_INVALID, "bad arguments");
   const int64_t nc = c->colour_start.empty() ? 0 : (int64_t)c->colour_start.size() - 1;
-  constexpr int NV = 8 + MAX_COLOURS + 1 + 1 + 1 + 1 + 1 + 1 + 1 + 2;
+  constexpr int NV = 8 + MAX_COLOURS + 1 + 1 + 1 + 1 + 1 + 1 + 1 + 2 + 1;
   int64_t vals[NV] = {c->n_groups, c->n_zero, c->n_atomic_groups, c->conforming ? 1 : 0,
                       c->epw,      nc,        c->rounds,          c->n_slots};
   for (int64_t q = 0; q < nc && q <= MAX_COLOURS; ++q)
     vals[8 + q] = c->colour_start[q + 1] - c->colour_start[q];
-  vals[NV - 8] = c->mfma ? SEM_KERNEL_MFMA : SEM_KERNEL_COLUMN;
-  vals[NV - 7] = c->map16 ? 2 : 4;  // bytes per packed map entry
+  vals[NV - 9] = c->mfma ? SEM_KERNEL_MFMA : SEM_KERNEL_COLUMN;
+  vals[NV - 8] = c->map16 ? 2 : 4;  // bytes per packed map entry
   // the geometry the Poisson action actually uses: nodal only once x_phys
   // per node exists (sem_set_geom installs stored factors); before any
   // geometry, the mode sem_geom_from_nodes will resolve to
   const bool eff_nodal = c->xg_valid ? true : (c->d_GP[0] ? false : nodal_mode(c));
-  vals[NV - 6] = eff_nodal ? SEM_GEOM_NODAL : SEM_GEOM_STORED;
+  vals[NV - 7] = eff_nodal ? SEM_GEOM_NODAL : SEM_GEOM_STORED;
   // plan: 0 chains (colour launches), 1 element-coloured chains, 2 elements
   // (MFMA kernel), 4 chains + seam sums (3 was the retired one-launch plan),
   // 5 elements + seam sums (n = 17 MFMA kernel)
-  vals[NV - 5] = c->mfma ? (c->seam ? 5 : 2) : (c->ecol ? 1 : (c->seam ? 4 : 0));
+  vals[NV - 6] = c->mfma ? (c->seam ? 5 : 2) : (c->ecol ? 1 : (c->seam ? 4 : 0));
   // the same for the axisymmetric Stokes block (dofs_per_node = 2)
   const bool axi_nodal =
       c->xg_axi ? true : (c->d_GP[1] ? false : nodal_mode_op(c, SEM_OP_AXISYM_STOKES));
-  vals[NV - 4] = c->dpn == 2 ? (axi_nodal ? SEM_GEOM_NODAL : SEM_GEOM_STORED) : 0;
-  vals[NV - 3] = c->seam ? c->n_seam : 0;  // seam nodes
-  vals[NV - 2] = c->blocks ? 1 : 0;          // block layout
-  vals[NV - 1] = c->row_carries;             // entries carried between rounds
+  vals[NV - 5] = c->dpn == 2 ? (axi_nodal ? SEM_GEOM_NODAL : SEM_GEOM_STORED) : 0;
+  vals[NV - 4] = c->seam ? c->n_seam : 0;  // seam nodes
+  vals[NV - 3] = c->blocks ? 1 : 0;          // block layout
+  vals[NV - 2] = c->row_carries;             // entries carried between rounds
+  vals[NV - 1] = c->const_d && c->map16 && !c->mfma ? 1 : 0;  // Poisson: D as constants
   for (int i = 0; i < n_info && i < NV; ++i) info[i] = vals[i];
   return SEM_OK;
 }

@@ -36,6 +36,7 @@
 
 #include <cstdint>
 #include <type_traits>
+#include <utility>
 
 #include "sem_internal.h"
 
@@ -165,9 +166,46 @@ struct DEO<N, true> {
   }
 };
 
-// v = D x
+// D of the standard GLL basis as compile-time constants (csrc/deo_const.h,
+// generated by tools/gen_deo_const.py from the library's own D): the
+// coefficients become literal operands materialised by scalar moves where
+// they are used, so they hold no registers across the round loop (the
+// kernel-argument form keeps 80 SGPRs live and the allocator spills the
+// excess to VGPR lanes, read back with v_readlane in every round).  Used
+// only when the context's D equals the table bit for bit (sem_set_basis,
+// DESIGN.md §4.1); any other basis runs the argument form.
 template <int N>
-__device__ __forceinline__ void deo_apply(const DEO<N>& D, const double (&x)[N],
+struct DEOConstData {
+  static constexpr bool available = false;
+};
+}  // namespace semk
+#include "deo_const.h"
+namespace semk {
+template <int N>
+struct DEOConst {};  // tag: the contractions below read DEOConstData<N> at compile time
+
+// compile-time loop: f(std::integral_constant<int, i>) for i = 0..K-1
+template <class F, int... I>
+__device__ __forceinline__ void sfor_(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>()), ...);
+}
+template <int K, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+  sfor_(f, std::make_integer_sequence<int, K>());
+}
+
+// the kernel's view of D: the constant table (CD) or the argument
+template <int N, bool CD>
+__device__ __forceinline__ auto deo_view(const DEO<N>& D) {
+  if constexpr (CD)
+    return DEOConst<N>();
+  else
+    return D;
+}
+
+// v = D x
+template <int N, class DT>
+__device__ __forceinline__ void deo_apply(const DT& D, const double (&x)[N],
                                           double (&v)[N]) {
   constexpr int H = N / 2;
   double e[H], o[H];
@@ -199,8 +237,8 @@ __device__ __forceinline__ void deo_apply(const DEO<N>& D, const double (&x)[N],
 }
 
 // v = D^T x  (the transpose is centro-antisymmetric with P^T <-> Q^T swapped)
-template <int N>
-__device__ __forceinline__ void deo_apply_t(const DEO<N>& D, const double (&x)[N],
+template <int N, class DT>
+__device__ __forceinline__ void deo_apply_t(const DT& D, const double (&x)[N],
                                             double (&v)[N]) {
   constexpr int H = N / 2;
   double e[H], o[H];
@@ -235,8 +273,8 @@ __device__ __forceinline__ void deo_apply_t(const DEO<N>& D, const double (&x)[N
 // pair as the even-odd sums complete (a row pass stores into the lane's own
 // LDS row): only e, o and one output pair are live, not the whole output
 // column -- the register peak of the high-order column kernels
-template <int N, bool TR>
-__device__ __forceinline__ void deo_apply_to(const DEO<N>& D, const double (&x)[N], double* out) {
+template <int N, bool TR, class DT>
+__device__ __forceinline__ void deo_apply_to(const DT& D, const double (&x)[N], double* out) {
   constexpr int H = N / 2;
   double e[H], o[H];
 #pragma unroll
@@ -264,6 +302,67 @@ __device__ __forceinline__ void deo_apply_to(const DEO<N>& D, const double (&x)[
     for (int r = 0; r < H; ++r) a = fma(TR ? E->cc[r] : E->rr[r], o[r], a);
     out[H] = a;
   }
+}
+
+// the same three contractions with D from the compile-time table: every
+// coefficient is a constant expression (a literal operand where it is used)
+template <int N>
+__device__ __forceinline__ void deo_const_rows(const double (&x)[N], double (&e)[N / 2],
+                                               double (&o)[N / 2]) {
+#pragma unroll
+  for (int r = 0; r < N / 2; ++r) {
+    e[r] = x[r] + x[N - 1 - r];
+    o[r] = x[r] - x[N - 1 - r];
+  }
+}
+// TR false: out[m] = (D x)[m]; TR true: (D^T x)[m]; Store(m, value)
+template <int N, bool TR, class Store>
+__device__ __forceinline__ void deo_const_apply(const double (&x)[N], Store&& st) {
+  using K = DEOConstData<N>;
+  constexpr int H = N / 2;
+  double e[H], o[H];
+  deo_const_rows<N>(x, e, o);
+  sfor<H>([&](auto mI) {
+    constexpr int m = decltype(mI)::value;
+    double sp = 0.0, tp = 0.0;
+    if constexpr (N % 2) {
+      constexpr double c = TR ? K::rr[m] : K::cc[m];
+      tp = c * x[H];
+    }
+    sfor<H>([&](auto rI) {
+      constexpr int r = decltype(rI)::value;
+      constexpr double a = TR ? K::Q[r * H + m] : K::P[m * H + r];
+      constexpr double b = TR ? K::P[r * H + m] : K::Q[m * H + r];
+      sp = fma(a, o[r], sp);
+      tp = fma(b, e[r], tp);
+    });
+    st(m, sp + tp);
+    st(N - 1 - m, sp - tp);
+  });
+  if constexpr (N % 2) {
+    double a = 0.0;
+    sfor<H>([&](auto rI) {
+      constexpr int r = decltype(rI)::value;
+      constexpr double c = TR ? K::cc[r] : K::rr[r];
+      a = fma(c, o[r], a);
+    });
+    st(H, a);
+  }
+}
+template <int N>
+__device__ __forceinline__ void deo_apply(const DEOConst<N>&, const double (&x)[N],
+                                          double (&v)[N]) {
+  deo_const_apply<N, false>(x, [&](int m, double t) { v[m] = t; });
+}
+template <int N>
+__device__ __forceinline__ void deo_apply_t(const DEOConst<N>&, const double (&x)[N],
+                                            double (&v)[N]) {
+  deo_const_apply<N, true>(x, [&](int m, double t) { v[m] = t; });
+}
+template <int N, bool TR>
+__device__ __forceinline__ void deo_apply_to(const DEOConst<N>&, const double (&x)[N],
+                                             double* out) {
+  deo_const_apply<N, TR>(x, [&](int m, double t) { out[m] = t; });
 }
 
 template <int N>
@@ -549,8 +648,9 @@ struct WLTile {
 #ifndef SEM_ROW_STORE_PAIRS_N
 #define SEM_ROW_STORE_PAIRS_N 17  // orders from which row passes store output pairs directly
 #endif
-template <int N, int RS, bool TR, bool REL, int RL = RS, int JUNK = 0, bool SPLIT = false>
-__device__ __forceinline__ void row_pass(double* L, int j, const DEO<N>& D, bool active = true) {
+template <int N, int RS, bool TR, bool REL, int RL = RS, int JUNK = 0, bool SPLIT = false,
+          class DT = DEO<N>>
+__device__ __forceinline__ void row_pass(double* L, int j, const DT& D, bool active = true) {
   double r[RL], x[N];
   load_row<N, RS, RL, SPLIT>(L, j, r);
 #pragma unroll
@@ -601,22 +701,11 @@ __device__ __forceinline__ void load_map(const MapRef& m, int64_t g, int lane, b
     const uint16_t* mp = m.p16 + g * (int64_t)(N * LW) + (in_wave ? lane : LW - 1);
     const uint32_t* bp = m.base + g * N;  // g is wave-uniform: scalar loads
     uint32_t o[N], b[N];
-#if SEM_DIAG_NO_MAP16_LOAD
-    // DIAGNOSTIC (timing only, wrong results): the 16-bit entries are not
-    // read; canonical structured offsets, every entry a plain store
-    (void)mp;
-#pragma unroll
-    for (int r = 0; r < N; ++r) {
-      const int kk = lane / N, jj = lane - kk * N;
-      o[r] = in_wave ? (uint32_t)(kk * (N - 1) + jj) : (W_SKIP << M16_CODE_SHIFT);
-    }
-#else
 #pragma unroll
     for (int r = 0; r < N; ++r) {
       const uint32_t t = mp[r * LW];
       o[r] = in_wave ? t : (W_SKIP << M16_CODE_SHIFT);
     }
-#endif
 #pragma unroll
     for (int r = 0; r < N; ++r) b[r] = bp[r];
 #pragma unroll
@@ -677,12 +766,12 @@ struct MapTouch {
 // (p = 0..N-1) of the lane's column j in v[], and the raw coded map entries.
 //   mapP[g][r][k*N + j] = map[e][r][j] | code,  GP[g][c][r][k*N + j] = G_c(e; r, j)
 // ---------------------------------------------------------------------------
-template <int N, bool M16, class Pre = NoWait, bool LD = false>
+template <int N, bool M16, class Pre = NoWait, bool LD = false, class DT = DEO<N>>
 __device__ __forceinline__ void poisson_group_stored(const MapRef& mref,
                                                      const double* __restrict__ GP,
                                                      const double* __restrict__ u, int64_t g,
                                                      int lane, int j, bool in_wave, double* L,
-                                                     const DEO<N>& D, uint32_t (&raw)[N],
+                                                     const DT& D, uint32_t (&raw)[N],
                                                      double (&v)[N], const double* __restrict__ y,
                                                      int accumulate, double (&prev)[N],
                                                      const Pre& pre = Pre()) {
@@ -791,9 +880,9 @@ struct NodalTile {
   static constexpr bool split = SEM_LDS_SPLIT;
 };
 
-template <int N>
+template <int N, class DT>
 __device__ __forceinline__ void nodal_geometry(const double2 (&xc)[N], int j, double* A, double* B,
-                                               const DEO<N>& D, const WVec<N>& w, double wj,
+                                               const DT& D, const WVec<N>& w, double wj,
                                                double (&g00)[N], double (&g01)[N], bool in_wave) {
   constexpr int RS = NodalTile<N>::RS;
   constexpr int RL = NodalTile<N>::RL;
@@ -846,9 +935,9 @@ __device__ __forceinline__ void nodal_geometry(const double2 (&xc)[N], int j, do
 }
 
 // the Laplacian of the group on tile A with G00/G01 in registers, G11 in B
-template <int N, class Pre = NoWait>
+template <int N, class Pre = NoWait, class DT = DEO<N>>
 __device__ __forceinline__ void nodal_laplacian(const double (&uc)[N], int j, double* A,
-                                                const double* B, const DEO<N>& D,
+                                                const double* B, const DT& D,
                                                 const double (&g00)[N], const double (&g01)[N],
                                                 double (&v)[N], const double* __restrict__ y,
                                                 const uint32_t (&raw)[N], int accumulate,
@@ -886,12 +975,12 @@ __device__ __forceinline__ void nodal_laplacian(const double (&uc)[N], int j, do
 }
 
 // One group of the Poisson action with NODAL geometry (no prefetch).
-template <int N, bool M16, class Pre = NoWait, bool LD = false>
+template <int N, bool M16, class Pre = NoWait, bool LD = false, class DT = DEO<N>>
 __device__ __forceinline__ void poisson_group_nodal(const MapRef& mref,
                                                     const double2* __restrict__ XG,
                                                     const double* __restrict__ u, int64_t g,
                                                     int lane, int j, bool in_wave, double* A,
-                                                    double* B, const DEO<N>& D,
+                                                    double* B, const DT& D,
                                                     const WVec<N>& w, double wj,
                                                     uint32_t (&raw)[N], double (&v)[N],
                                                     const double* __restrict__ y, int accumulate,
@@ -1149,12 +1238,13 @@ __device__ __forceinline__ double block_sum_fixed(double v, double* sh) {
   return s;
 }
 
-template <int N, bool NODAL, bool M16, bool SEAM = false, bool DOT = false>
+template <int N, bool NODAL, bool M16, bool SEAM = false, bool DOT = false, bool CD = false>
 __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODAL, SEAM, DOT>::value))
     k_poisson_apply(const MapRef mref, const double* __restrict__ GP,
                     const double2* __restrict__ XG, const double* __restrict__ u,
                     double* __restrict__ y, int64_t c0, int64_t c1, int rounds, int accumulate,
-                    const DEO<N> D, const WVec<N> w, const SeamPlan sp) {
+                    const DEO<N> Darg, const WVec<N> w, const SeamPlan sp) {
+  const auto D = deo_view<N, CD>(Darg);
   using T = Tile<N, NODAL ? SEM_TILE_PAD_NODAL : SEM_TILE_PAD_STORED>;
   constexpr int NT = NODAL ? 2 : 1;  // tiles per element slot
   constexpr int CW = ChainWaves<N>::value;
@@ -1378,7 +1468,7 @@ __global__ void __launch_bounds__(BLOCK)
 
 // fixed-order sum of the DOT partials of an action: na chain partials, then
 // nb seam-sum partials -> *out
-static __global__ void __launch_bounds__(BLOCK)
+[[maybe_unused]] static __global__ void __launch_bounds__(BLOCK)
     k_dot_finish(const double* __restrict__ a, int64_t na, const double* __restrict__ b,
                  int64_t nb, double* __restrict__ out) {
   double v = 0.0;

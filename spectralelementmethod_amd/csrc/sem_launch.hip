@@ -25,6 +25,14 @@ void launch_chains(sem_ctx* c, int op_kind, bool nodal, const double* u, double*
   SeamPlan sp{c->d_ccol, c->d_seam_buf, c->n_node};
   sp.dot = dot_part;
   sp.round_sync = c->round_sync ? 1 : 0;
+  // the standard GLL D as compile-time constants (16-bit maps: the
+  // structured meshes; sem_ctx::const_d)
+  if (c->const_d && c->map16 && op_kind == SEM_OP_POISSON) {
+    const PoissonLaunch L{g,  b,  st, mr, nodal ? nullptr : c->d_GP[0], nodal ? c->d_XG : nullptr,
+                          u,  y,  c0, c1, R, acc, sp};
+    launch_poisson_const_d<N>(L, nodal, SEAM, SEAM && dot_part, w);
+    return;
+  }
   if constexpr (SEAM) {
     if (dot_part) {  // Poisson, one DOF per node, overwrite: u.y partials per chain
       const double* GP = nodal ? nullptr : c->d_GP[0];

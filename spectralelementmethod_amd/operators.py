@@ -189,8 +189,8 @@ class SEMOperator(object):
 
     def plan_info(self):
         """Setup plan of the scatter (see include/sem_hip.h sem_plan_info)."""
-        info = (C.c_int64 * 25)()
-        _lib.check(self._lib.sem_plan_info(self._ctx, info, 25))
+        info = (C.c_int64 * 26)()
+        _lib.check(self._lib.sem_plan_info(self._ctx, info, 26))
         v = list(info)
         counts = [x for x in v[8:8 + v[5]]]
         while counts and counts[-1] == 0:
@@ -206,7 +206,7 @@ class SEMOperator(object):
                     geometry_axisym=(None if self.dpn != 2 else
                                      "nodal" if v[21] == _lib.GEOM_NODAL else "stored"),
                     seam_nodes=v[22] if v[20] in (4, 5) else 0, blocks=bool(v[23]),
-                    row_carries=v[24])
+                    row_carries=v[24], const_d=bool(v[25]))
 
     # ------------------------------------------------------------------
     def compute_geometry(self, kind=POISSON, stream=None):

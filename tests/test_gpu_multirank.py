@@ -204,6 +204,31 @@ def test_pcg_fixed_iterations_and_errors(gpu):
     assert rel <= 1e-12 and ((x - xs).norm() / xs.norm()).item() < 1e-9
 
 
+@pytest.mark.parametrize("iters", [1, 36, 37])
+def test_pcg_x_pairs_bitwise(gpu, monkeypatch, iters):
+    """x updated every second iteration (default: x += a' p' + a p as two
+    fused multiply-adds in order, a flush after an odd count) is bitwise the
+    x of the every-iteration update (SEM_PCG_X_EVERY=1), read per solve."""
+    from spectralelementmethod_amd import meshgen
+    from spectralelementmethod_amd.operators import SEMOperator
+    nodes, e2n = meshgen.structured_square(16, 16, 4, warp=0.05)
+    op = SEMOperator(4, e2n, nodes, device=gpu)
+    xs, on = _manufactured(nodes, gpu)
+    b = op.apply(xs)
+    x0 = torch.where(on, xs, torch.zeros_like(xs))
+    out = {}
+    for every in ("1", "0"):
+        monkeypatch.setenv("SEM_PCG_X_EVERY", every)
+        out[every] = op.pcg_solve(b, x0.clone(), on, rtol=0.0, max_iter=iters)
+    assert out["1"][1] == out["0"][1] == iters
+    assert torch.equal(out["1"][0], out["0"][0])
+    assert out["1"][2] == out["0"][2]
+    # and a converged solve with the default
+    monkeypatch.delenv("SEM_PCG_X_EVERY")
+    x, its, rel = op.pcg_solve(b, x0.clone(), on, rtol=1e-12)
+    assert rel <= 1e-12 and ((x - xs).norm() / xs.norm()).item() < 1e-9
+
+
 def _native_rccl_worker(q):
     """One rank through the bench's process-group setup and the native RCCL
     transport of sem_dd (communicator init, ncclAllReduce in the PCG; no peer

@@ -4,7 +4,9 @@
   python tools/build_variants.py NAME:DEF1,DEF2 [NAME:...]
 
 writes build_variants/NAME/libsem_hip.so compiled with -DDEF1 -DDEF2 (every
-order); select one at run time with SEM_LIB_PATH=build_variants/NAME/libsem_hip.so."""
+order; an entry starting with "-" is a raw compiler flag, e.g.
+nolicm:-mllvm,-disable-machine-licm); select one at run time with
+SEM_LIB_PATH=build_variants/NAME/libsem_hip.so."""
 import os
 import sys
 
