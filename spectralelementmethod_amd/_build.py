@@ -21,7 +21,7 @@ LAUNCH_RANGES = [(2, 5), (6, 8), (9, 9), (10, 11), (12, 13), (14, 15), (16, 16),
 # coefficients out of the round loop costs registers / occupancy
 # (profiles/r04/const_d/)
 NO_LICM = ("-mllvm", "-disable-machine-licm")
-LAUNCH_CD_RANGES = [((2, 5), ()), ((6, 8), ()), ((9, 9), ()), ((10, 11), ()), ((12, 13), ()),
+LAUNCH_CD_RANGES = [((2, 6), ()), ((7, 7), NO_LICM), ((8, 10), ()), ((11, 13), ()),
                     ((14, 15), ()), ((16, 16), ()), ((17, 17), NO_LICM)]
 DEPS = SOURCES + ["sem_launch.hip", "sem_launch_cd.hip", "sem_internal.h", "sem_kernels.h", "sem_ctx.h", "gll_table.h",
                   "deo_const.h"]

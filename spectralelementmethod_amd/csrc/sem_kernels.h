@@ -178,6 +178,11 @@ template <int N>
 struct DEOConstData {
   static constexpr bool available = false;
 };
+// SEM_CONST_D_PIN: each constant is materialised at its use (an empty asm on
+// its SGPR pair), never hoisted out of the round loop
+#ifndef SEM_CONST_D_PIN
+#define SEM_CONST_D_PIN 0
+#endif
 }  // namespace semk
 #include "deo_const.h"
 namespace semk {
@@ -326,13 +331,18 @@ __device__ __forceinline__ void deo_const_apply(const double (&x)[N], Store&& st
     constexpr int m = decltype(mI)::value;
     double sp = 0.0, tp = 0.0;
     if constexpr (N % 2) {
-      constexpr double c = TR ? K::rr[m] : K::cc[m];
+      double c = TR ? K::rr[m] : K::cc[m];
+      if constexpr (SEM_CONST_D_PIN) asm volatile("" : "+s"(c));
       tp = c * x[H];
     }
     sfor<H>([&](auto rI) {
       constexpr int r = decltype(rI)::value;
-      constexpr double a = TR ? K::Q[r * H + m] : K::P[m * H + r];
-      constexpr double b = TR ? K::P[r * H + m] : K::Q[m * H + r];
+      double a = TR ? K::Q[r * H + m] : K::P[m * H + r];
+      double b = TR ? K::P[r * H + m] : K::Q[m * H + r];
+      if constexpr (SEM_CONST_D_PIN) {  // materialised here, never hoisted
+        asm volatile("" : "+s"(a));
+        asm volatile("" : "+s"(b));
+      }
       sp = fma(a, o[r], sp);
       tp = fma(b, e[r], tp);
     });
@@ -343,7 +353,8 @@ __device__ __forceinline__ void deo_const_apply(const double (&x)[N], Store&& st
     double a = 0.0;
     sfor<H>([&](auto rI) {
       constexpr int r = decltype(rI)::value;
-      constexpr double c = TR ? K::cc[r] : K::rr[r];
+      double c = TR ? K::cc[r] : K::rr[r];
+      if constexpr (SEM_CONST_D_PIN) asm volatile("" : "+s"(c));
       a = fma(c, o[r], a);
     });
     st(H, a);
@@ -880,10 +891,29 @@ struct NodalTile {
   static constexpr bool split = SEM_LDS_SPLIT;
 };
 
+// SEM_W_SCALAR_LOAD: the nodal geometry reads w_m with scalar loads from the
+// device copy once per round (pointer laundered, so neither hoisted nor kept)
+// instead of holding the 2n SGPRs of the kernel argument for the whole launch
+#ifndef SEM_W_SCALAR_LOAD
+#define SEM_W_SCALAR_LOAD 0
+#endif
+using CWPtr = const __attribute__((address_space(4))) double*;
+__device__ __forceinline__ CWPtr wrow(const double* wp) {
+  CWPtr q = (CWPtr)wp;
+  if constexpr (SEM_W_SCALAR_LOAD) asm volatile("" : "+s"(q));
+  return q;
+}
+template <int N>
+__device__ __forceinline__ double wsel(const WVec<N>& w, CWPtr q, int m) {
+  if constexpr (SEM_W_SCALAR_LOAD)
+    return q[m];
+  else
+    return w.v[m];
+}
 template <int N, class DT>
 __device__ __forceinline__ void nodal_geometry(const double2 (&xc)[N], int j, double* A, double* B,
                                                const DT& D, const WVec<N>& w, double wj,
-                                               double (&g00)[N], double (&g01)[N], bool in_wave) {
+                                               double (&g00)[N], double (&g01)[N], bool in_wave, const double* wp = nullptr) {
   constexpr int RS = NodalTile<N>::RS;
   constexpr int RL = NodalTile<N>::RL;
   double jr0[N], jr1[N];
@@ -919,6 +949,7 @@ __device__ __forceinline__ void nodal_geometry(const double2 (&xc)[N], int j, do
     store_row<N, RS, NodalTile<N>::JUNK>(B, j, tb, in_wave || !NodalTile<N>::wl);
   }
   wave_sync();
+  const auto wq = wrow(wp);
 #pragma unroll
   for (int m = 0; m < N; ++m) {
     constexpr bool SP = NodalTile<N>::split;
@@ -926,7 +957,7 @@ __device__ __forceinline__ void nodal_geometry(const double2 (&xc)[N], int j, do
     const double det = jr0[m] * js1 - js0 * jr1[m];
     // (w_m w_j) / det, associated so that no loop-invariant w_m w_j array
     // is hoisted out of the round loop (9 doubles spilled at 4 waves/SIMD)
-    const double sc = w.v[m] * (wj * fast_rcp(det));
+    const double sc = wsel<N>(w, wq, m) * (wj * fast_rcp(det));
     g00[m] = sc * fma(js1, js1, js0 * js0);
     g01[m] = -sc * fma(js1, jr1[m], js0 * jr0[m]);
     B[m * RS + j] = sc * fma(jr1[m], jr1[m], jr0[m] * jr0[m]);  // G11, own slot
@@ -984,7 +1015,7 @@ __device__ __forceinline__ void poisson_group_nodal(const MapRef& mref,
                                                     const WVec<N>& w, double wj,
                                                     uint32_t (&raw)[N], double (&v)[N],
                                                     const double* __restrict__ y, int accumulate,
-                                                    double (&prev)[N], const Pre& pre = Pre()) {
+                                                    double (&prev)[N], const Pre& pre = Pre(), const double* wp = nullptr) {
   double uc[N];
   double2 xc[N];
   load_map<N, M16, LD>(mref, g, lane, in_wave, raw);
@@ -993,7 +1024,7 @@ __device__ __forceinline__ void poisson_group_nodal(const MapRef& mref,
   gather_u<N>(u, raw, uc);
 #endif
   double g00[N], g01[N];
-  nodal_geometry<N>(xc, j, A, B, D, w, wj, g00, g01, in_wave);
+  nodal_geometry<N>(xc, j, A, B, D, w, wj, g00, g01, in_wave, wp);
 #if !SEM_NODAL_EARLY_U
   gather_u<N>(u, raw, uc);
 #endif
@@ -1027,6 +1058,9 @@ __device__ __forceinline__ double lane_next(double x) {
 #define SEM_ROUND_SYNC_ALWAYS 0
 #endif
 constexpr int CARRY_BUFS = 3;
+#ifndef SEM_LANE_RECOMPUTE
+#define SEM_LANE_RECOMPUTE 0
+#endif
 
 // Scatter of one group's column values through the coded map, with the
 // in-group merge (next lane) and the chain carry (previous group) applied.
@@ -1071,6 +1105,10 @@ __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_
       if ((raw[p] >> CODE_SHIFT) & W_MERGE) v[c][p] += vn;
     }
   // hand the last lane's column to the next group of the chain
+  // SEM_LANE_RECOMPUTE: the lane tests are re-evaluated every round (the
+  // lane id laundered) instead of kept as loop-invariant SGPR masks, which
+  // the allocator spills to VGPR lanes at the register limit
+  if constexpr (SEM_LANE_RECOMPUTE) asm volatile("" : "+v"(lane));
   if (lane == LW - 1) {
 #pragma unroll
     for (int c = 0; c < NC; ++c)
@@ -1188,9 +1226,24 @@ constexpr int stored_seam_mw(int n) {
        : n == 17 ? (SEM_MW_S17 ? SEM_MW_S17 : 1)
                  : 1;
 }
-template <int N, bool NODAL, bool SEAM = false, bool DOT = false>
+// the stored seam kernels with D as constants (CD): p = 12 (n = 13) with a
+// 5-wave request (96 VGPRs, 16 B of scratch) measured 0.109-0.110 against
+// 0.123-0.124 ms per action (natural 4 waves; profiles/r04/const_d/l_*);
+// the same request at n = 11 0.117 against 0.108.  SEM_MW_CD_N / _W
+// override one order (A/B builds).
+#ifndef SEM_MW_CD_N
+#define SEM_MW_CD_N 0
+#endif
+#ifndef SEM_MW_CD_W
+#define SEM_MW_CD_W 0
+#endif
+constexpr int cd_seam_mw(int n) {
+  return n == SEM_MW_CD_N ? SEM_MW_CD_W : n == 13 ? 5 : stored_seam_mw(n);
+}
+template <int N, bool NODAL, bool SEAM = false, bool DOT = false, bool CD = false>
 struct PoissonMinWaves {
   static constexpr int value = SEM_POISSON_MIN_WAVES > 0             ? SEM_POISSON_MIN_WAVES
+                               : (CD && !NODAL && SEAM && !DOT)      ? cd_seam_mw(N)
                                : (NODAL && N == 9)                   ? 4
                                : (!NODAL && SEAM && !DOT)            ? stored_seam_mw(N)
                                : (NODAL && N == 5 && !SEAM && !DOT)  ? 6
@@ -1221,6 +1274,7 @@ struct SeamPlan {
   int64_t n_node;
   double* dot = nullptr;  // DOT kernels: one partial of u.y per workgroup
   int round_sync = 1;     // a chain writes some node in two rounds: order the rounds
+  const double* w = nullptr;  // device copy of the weights (SEM_W_SCALAR_LOAD)
 };
 
 // sum of one value per thread over the workgroup, in a fixed order (wave
@@ -1239,7 +1293,7 @@ __device__ __forceinline__ double block_sum_fixed(double v, double* sh) {
 }
 
 template <int N, bool NODAL, bool M16, bool SEAM = false, bool DOT = false, bool CD = false>
-__global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODAL, SEAM, DOT>::value))
+__global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODAL, SEAM, DOT, CD>::value))
     k_poisson_apply(const MapRef mref, const double* __restrict__ GP,
                     const double2* __restrict__ XG, const double* __restrict__ u,
                     double* __restrict__ y, int64_t c0, int64_t c1, int rounds, int accumulate,
@@ -1285,7 +1339,7 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
     constexpr bool LD = RawLaunder<N, DOT>::value;
     if constexpr (NODAL)
       poisson_group_nodal<N, M16, Pre, LD>(mref, XG, u, g, lane, j, in_wave, L, LB, D, w, wj, raw,
-                                           v[0], y, accumulate, prev, pre);
+                                           v[0], y, accumulate, prev, pre, sp.w);
     else
       poisson_group_stored<N, M16, Pre, LD>(mref, GP, u, g, lane, j, in_wave, L, D, raw, v[0], y,
                                             accumulate, prev, pre);

@@ -25,6 +25,7 @@ void launch_chains(sem_ctx* c, int op_kind, bool nodal, const double* u, double*
   SeamPlan sp{c->d_ccol, c->d_seam_buf, c->n_node};
   sp.dot = dot_part;
   sp.round_sync = c->round_sync ? 1 : 0;
+  sp.w = c->d_w;
   // the standard GLL D as compile-time constants (16-bit maps: the
   // structured meshes; sem_ctx::const_d)
   if (c->const_d && c->map16 && op_kind == SEM_OP_POISSON) {
