@@ -602,10 +602,11 @@ class OverlappedOperator(object):
 
     def step(self, u, y, events=None):
         """y = K u on this rank's DOFs, shared DOFs summed over all ranks.
-        ``events`` (start, end) bracket the step on the caller's stream."""
+        ``events`` (start, end) bracket the step on the caller's stream
+        (either may be None)."""
         main = torch.cuda.current_stream(self.device)
         sp = _lib.stream_ptr(main)
-        if events is not None:
+        if events is not None and events[0] is not None:
             events[0].record(main)
         if self.dd:
             self._check(self._lib.sem_dd_apply(self.dd, self.kind, _lib.tptr(u), _lib.tptr(y),
@@ -613,7 +614,7 @@ class OverlappedOperator(object):
         else:
             _lib.check(self._lib.sem_apply(self.ops[0]._ctx, self.kind, _lib.tptr(u),
                                            _lib.tptr(y), 0, sp))
-        if events is not None:
+        if events is not None and events[1] is not None:
             events[1].record(main)
         return y
 
