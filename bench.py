@@ -385,6 +385,8 @@ def main():
     ap.add_argument("--step-events", choices=["each", "region"], default="each",
                     help="HIP events around every timed action, or one pair around the "
                          "timed region (per-action quartiles then from an untimed pass)")
+    ap.add_argument("--kernel-series", action="store_true",
+                    help="also write every timed action's HIP-event time into the JSON")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the parity spot check (timing-only diagnostic builds)")
@@ -619,6 +621,8 @@ def main():
             "step_events": args.step_events,
             "kernel_ms_quartiles": [float(q) for q in np.percentile(kern_ms, [25, 50, 75])],
             "kernel_ms_max": float(np.max(kern_ms)),
+            "kernel_ms_series": [round(float(x), 5) for x in kern_ms] if args.kernel_series
+            else None,
             "host_enqueue_ms_per_step": t_enqueue / args.steps * 1e3,
             "decomposition": op.dd_info(),
             "gflops_kernel": F / kern_avg_s / 1e9,

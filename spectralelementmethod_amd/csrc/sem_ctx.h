@@ -205,9 +205,10 @@ inline bool auto_nodal_order(int n) {
 // median ms per action, argument form -> constants): p = 10 0.119 -> 0.108,
 // 12 0.126 -> 0.123, 14 0.131 -> 0.123, 16 0.140 -> 0.122 (machine LICM
 // off for that unit), every order from p = 10 2-13 % faster; p = 6 (LICM
-// off) 0.102-0.105 -> 0.099; p = 4 and p = 8 (nodal) 17-19 % slower (the
-// hoisted constants spill), the other low orders within 1-2 %.
-inline bool const_d_order(int n) { return n == 7 || n >= 11; }
+// off) 0.102-0.105 -> 0.099; p = 9 with a 5-wave request 0.114 -> 0.112;
+// p = 4 and p = 8 (nodal) 17-19 % slower (the hoisted constants spill), the
+// other low orders within 1-2 %.
+inline bool const_d_order(int n) { return n == 7 || n >= 10; }
 
 inline bool nodal_mode(const sem_ctx* c) {
   if (c->mfma) return c->geom_mode == SEM_GEOM_NODAL;  // AUTO: stored factors

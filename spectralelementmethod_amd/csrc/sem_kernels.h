@@ -1229,8 +1229,10 @@ constexpr int stored_seam_mw(int n) {
 // the stored seam kernels with D as constants (CD): p = 12 (n = 13) with a
 // 5-wave request (96 VGPRs, 16 B of scratch) measured 0.109-0.110 against
 // 0.123-0.124 ms per action (natural 4 waves; profiles/r04/const_d/l_*);
-// the same request at n = 11 0.117 against 0.108.  SEM_MW_CD_N / _W
-// override one order (A/B builds).
+// the same request at n = 11 0.117 against 0.108, at n = 15 no change;
+// p = 9 (n = 10) with constants and 5 waves 0.1123-0.1125 against
+// 0.1141 for the argument form (call N).  SEM_MW_CD_N / _W override one
+// order (A/B builds).
 #ifndef SEM_MW_CD_N
 #define SEM_MW_CD_N 0
 #endif
@@ -1238,7 +1240,7 @@ constexpr int stored_seam_mw(int n) {
 #define SEM_MW_CD_W 0
 #endif
 constexpr int cd_seam_mw(int n) {
-  return n == SEM_MW_CD_N ? SEM_MW_CD_W : n == 13 ? 5 : stored_seam_mw(n);
+  return n == SEM_MW_CD_N ? SEM_MW_CD_W : (n == 13 || n == 10) ? 5 : stored_seam_mw(n);
 }
 template <int N, bool NODAL, bool SEAM = false, bool DOT = false, bool CD = false>
 struct PoissonMinWaves {
