@@ -608,6 +608,9 @@ __device__ __forceinline__ void store_row(double* L, int i, const double (&t)[N]
 #ifndef SEM_TILE_PAD_STORED
 #define SEM_TILE_PAD_STORED 1
 #endif
+// per order: p = 14 (n = 15) unpadded, 0.1209-0.1211 against 0.1234-0.1248
+// ms per action (profiles/r04/knobs_high/, call P; p = 12 / 16 unchanged)
+constexpr bool stored_pad(int n) { return SEM_TILE_PAD_STORED && n != 15; }
 #ifndef SEM_TILE_PAD_NODAL
 #define SEM_TILE_PAD_NODAL 0
 #endif
@@ -786,7 +789,7 @@ __device__ __forceinline__ void poisson_group_stored(const MapRef& mref,
                                                      double (&v)[N], const double* __restrict__ y,
                                                      int accumulate, double (&prev)[N],
                                                      const Pre& pre = Pre()) {
-  using T = Tile<N, SEM_TILE_PAD_STORED>;
+  using T = Tile<N, stored_pad(N)>;
   constexpr int LW = T::LW;
   constexpr int RS = T::RS;
   constexpr bool SP = N >= SEM_LDS_SPLIT_STORED_N;
@@ -1301,7 +1304,7 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
                     double* __restrict__ y, int64_t c0, int64_t c1, int rounds, int accumulate,
                     const DEO<N> Darg, const WVec<N> w, const SeamPlan sp) {
   const auto D = deo_view<N, CD>(Darg);
-  using T = Tile<N, NODAL ? SEM_TILE_PAD_NODAL : SEM_TILE_PAD_STORED>;
+  using T = Tile<N, NODAL ? SEM_TILE_PAD_NODAL : stored_pad(N)>;
   constexpr int NT = NODAL ? 2 : 1;  // tiles per element slot
   constexpr int CW = ChainWaves<N>::value;
   constexpr bool WL = NODAL && NodalTile<N>::wl;
