@@ -115,7 +115,9 @@ def _rank_worker(rank, world, port, mode, p, nex, ney, q):
 
 @pytest.mark.parametrize("world,mode,p,nex,ney", [(2, "strip", 8, 12, 6), (3, "strip", 4, 10, 5),
                                                   (3, "generic", 3, 7, 6),
-                                                  (4, "sfc", 4, 6, 5)])
+                                                  (4, "sfc", 4, 6, 5),
+                                                  # constant-D kernels on both contexts
+                                                  (2, "strip", 12, 8, 6)])
 def test_overlapped_operator_ranks_on_one_gpu(gpu, world, mode, p, nex, ney):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
