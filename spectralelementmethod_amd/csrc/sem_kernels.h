@@ -1046,9 +1046,15 @@ __device__ __forceinline__ void poisson_group_nodal(const MapRef& mref,
 #ifndef SEM_DPP_SHIFT
 #define SEM_DPP_SHIFT 1
 #endif
-template <int N>
+#ifndef SEM_DPP_SHIFT_MAX_N
+#define SEM_DPP_SHIFT_MAX_N 17
+#endif
+// DPP17: the DPP form at n = 17 as well (the constant-D kernels: 128 VGPRs
+// either way there, 17 fewer LDS round trips per round; p = 16 0.1196-0.1226
+// against 0.1225-0.1253 ms per action, profiles/r04/knobs_high/u_*)
+template <int N, bool DPP17 = false>
 __device__ __forceinline__ double lane_next(double x) {
-  if constexpr (SEM_DPP_SHIFT && N < 17) {
+  if constexpr (SEM_DPP_SHIFT && (N < SEM_DPP_SHIFT_MAX_N || DPP17)) {
     constexpr int WAVE_SHL1 = 0x130;
     const int lo = __double2loint(x), hi = __double2hiint(x);
     return __hiloint2double(__builtin_amdgcn_update_dpp(hi, hi, WAVE_SHL1, 0xF, 0xF, false),
@@ -1072,7 +1078,7 @@ constexpr int CARRY_BUFS = 3;
 // DOT (seam plan, overwrite mode, one DOF per node): dot += u[gid] * value
 // at every STORE -- the node's one and only final value outside the seams.
 template <int N, int NC, bool PRE = false, int CW = ChainWaves<N>::value, bool SEAM = false,
-          bool DOT = false, bool LD = false>
+          bool DOT = false, bool LD = false, bool DPP17 = false>
 __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_t (&raw_in)[N],
                                            double (&v)[NC][N], int lane, int wave, int rd,
                                            bool in_wave, double (*carry)[CW][NC][N],
@@ -1105,7 +1111,7 @@ __device__ __forceinline__ void chain_emit(double* __restrict__ y, const uint32_
   for (int c = 0; c < NC; ++c)
 #pragma unroll
     for (int p = 0; p < N; ++p) {
-      const double vn = lane_next<N>(v[c][p]);
+      const double vn = lane_next<N, DPP17>(v[c][p]);
       if ((raw[p] >> CODE_SHIFT) & W_MERGE) v[c][p] += vn;
     }
   // hand the last lane's column to the next group of the chain
@@ -1351,7 +1357,7 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
                                             accumulate, prev, pre);
     SeamOut so;
     if constexpr (SEAM) so.base = sp.buf + sp.colour[chain] * sp.n_node;
-    chain_emit<N, 1, PRE, CW, SEAM, DOT, LD>(y, raw, v, lane, wave, rd, in_wave, carry, rowc,
+    chain_emit<N, 1, PRE, CW, SEAM, DOT, LD, CD>(y, raw, v, lane, wave, rd, in_wave, carry, rowc,
                                          accumulate, sp.round_sync, prev, so, u, &dotv);
     if constexpr (TOUCH)
       if (rd + 1 < rounds) touch.done();
