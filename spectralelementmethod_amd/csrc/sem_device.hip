@@ -192,25 +192,36 @@ int ctx_zero_list(const sem_ctx* c, std::vector<uint32_t>* nodes, bool* only_unr
 namespace semd {
 // second launch of the seam plan (k_seam_sum / k_seam_sum2 over the seam
 // nodes, one instantiation per colour count)
+int seam_ilp_of(const sem_ctx* c) { return c->n == 17 ? SEAM_ILP_17 : SEAM_ILP; }
+
 int64_t seam_sum_blocks(const sem_ctx* c) {
-  return c->n_seam ? grid_for(c->n_seam, BLOCK * SEAM_ILP) : 0;
+  return c->n_seam ? grid_for(c->n_seam, BLOCK * seam_ilp_of(c)) : 0;
 }
 
 int launch_seam_sum(sem_ctx* c, double* y, int acc, hipStream_t st, const double* du,
                     double* dot) {
   if (!c->n_seam) return SEM_OK;
   const dim3 g(c->dpn == 2 ? grid_for(c->n_seam) : (int)seam_sum_blocks(c)), b(BLOCK);
+  const bool ilp2 = seam_ilp_of(c) == 2;
+  static_assert(SEAM_ILP == 1 || SEAM_ILP == 2, "seam-sum ILP 1 or 2");
   switch (c->seam_ns) {
 #define SEAM_NS(K)                                                                           \
   case K:                                                                                  \
     if (c->dpn == 2)                                                                       \
       hipLaunchKernelGGL(k_seam_sum2<K>, g, b, 0, st, y, c->d_seam_gid, c->d_seam_mask,    \
                          c->n_seam, c->d_seam_buf, c->n_node, acc);                        \
-    else if (dot)                                                                          \
-      hipLaunchKernelGGL((k_seam_sum<K, true>), g, b, 0, st, y, c->d_seam_gid,             \
+    else if (dot && ilp2)                                                                  \
+      hipLaunchKernelGGL((k_seam_sum<K, true, 2>), g, b, 0, st, y, c->d_seam_gid,          \
                          c->d_seam_mask, c->n_seam, c->d_seam_buf, c->n_node, acc, du, dot);\
+    else if (dot)                                                                          \
+      hipLaunchKernelGGL((k_seam_sum<K, true, 1>), g, b, 0, st, y, c->d_seam_gid,          \
+                         c->d_seam_mask, c->n_seam, c->d_seam_buf, c->n_node, acc, du, dot);\
+    else if (ilp2)                                                                         \
+      hipLaunchKernelGGL((k_seam_sum<K, false, 2>), g, b, 0, st, y, c->d_seam_gid,         \
+                         c->d_seam_mask, c->n_seam, c->d_seam_buf, c->n_node, acc, nullptr, \
+                         nullptr);                                                         \
     else                                                                                   \
-      hipLaunchKernelGGL((k_seam_sum<K, false>), g, b, 0, st, y, c->d_seam_gid,            \
+      hipLaunchKernelGGL((k_seam_sum<K, false, 1>), g, b, 0, st, y, c->d_seam_gid,         \
                          c->d_seam_mask, c->n_seam, c->d_seam_buf, c->n_node, acc, nullptr, \
                          nullptr);                                                         \
     break;

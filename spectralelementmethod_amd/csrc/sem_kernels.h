@@ -1381,7 +1381,13 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
 #ifndef SEAM_ILP
 #define SEAM_ILP 1
 #endif
-template <int NS, bool DOT = false>
+// per context (seam_ilp_of): 2 at n = 17, where it measured faster per
+// action with the constant-D kernel: 0.1270-0.1275 against 0.1277-0.1288 ms
+// per step, three runs alternating (profiles/r04/knobs_high/x_*, u_*)
+#ifndef SEAM_ILP_17
+#define SEAM_ILP_17 2
+#endif
+template <int NS, bool DOT = false, int ILP = SEAM_ILP>
 __global__ void __launch_bounds__(BLOCK)
     k_seam_sum(double* __restrict__ y, const uint32_t* __restrict__ gid,
                const uint16_t* __restrict__ mask, int64_t n, const double* __restrict__ buf,
@@ -1411,13 +1417,13 @@ __global__ void k_seam_sum2(double* __restrict__ y, const uint32_t* __restrict__
   }
 }
 
-template <int NS, bool DOT>
+template <int NS, bool DOT, int ILP>
 __global__ void __launch_bounds__(BLOCK)
     k_seam_sum(double* __restrict__ y, const uint32_t* __restrict__ gid,
                const uint16_t* __restrict__ mask, int64_t n, const double* __restrict__ buf,
                int64_t n_node, int accumulate, const double* __restrict__ du,
                double* __restrict__ dot) {
-  // SEAM_ILP nodes per thread per pass (a block covers SEAM_ILP * BLOCK
+  // ILP nodes per thread per pass (a block covers ILP * BLOCK
   // consecutive seam nodes): their index, slot and y loads are in flight
   // together instead of one dependent chain per node
   double dotv = 0.0;
@@ -1427,19 +1433,19 @@ __global__ void __launch_bounds__(BLOCK)
   for (int c = 0; c < NS; ++c)
     rb[c] = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(buf + c * n_node), 0, 0x80000000,
                                               0x00020000);
-  for (int64_t b0 = (int64_t)blockIdx.x * (SEAM_ILP * BLOCK); b0 < n;
-       b0 += (int64_t)gridDim.x * (SEAM_ILP * BLOCK)) {
-    uint32_t g[SEAM_ILP], m[SEAM_ILP];
+  for (int64_t b0 = (int64_t)blockIdx.x * (ILP * BLOCK); b0 < n;
+       b0 += (int64_t)gridDim.x * (ILP * BLOCK)) {
+    uint32_t g[ILP], m[ILP];
 #pragma unroll
-    for (int q = 0; q < SEAM_ILP; ++q) {
+    for (int q = 0; q < ILP; ++q) {
       const int64_t i = b0 + q * BLOCK + threadIdx.x;
       const bool in = i < n;
       g[q] = in ? gid[i] : 0u;
       m[q] = in ? (uint32_t)mask[i] : 0u;
     }
-    double y0[SEAM_ILP], b[SEAM_ILP][NS];
+    double y0[ILP], b[ILP][NS];
 #pragma unroll
-    for (int q = 0; q < SEAM_ILP; ++q) {
+    for (int q = 0; q < ILP; ++q) {
       const bool prior = m[q] && (accumulate || (m[q] & 0x100u));
       y0[q] = prior ? y[g[q]] : 0.0;
 #pragma unroll
@@ -1450,7 +1456,7 @@ __global__ void __launch_bounds__(BLOCK)
       }
     }
 #pragma unroll
-    for (int q = 0; q < SEAM_ILP; ++q) {
+    for (int q = 0; q < ILP; ++q) {
       if (!m[q]) continue;  // past the end
       const bool prior = accumulate || (m[q] & 0x100u);
       double s = y0[q];
