@@ -654,6 +654,8 @@ struct WLTile {
   __device__ static int base(int wave, int k) { return wave * WS + k * N; }
 };
 
+
+
 // Row pass on a wave-private tile: the lane's row j (written column-wise by
 // the wave and synchronised) is contracted with D (or D^T when TR) and
 // written back, so the tile again holds the result in column layout.  REL
@@ -663,6 +665,20 @@ struct WLTile {
 #ifndef SEM_ROW_STORE_PAIRS_N
 #define SEM_ROW_STORE_PAIRS_N 17  // orders from which row passes store output pairs directly
 #endif
+// the stored-factor kernel's tile: wave-linear from order
+// SEM_TILE_WL_STORED_N (conflict-free column and row accesses, §4.6; rows
+// of 8-byte reads instead of 16-byte pairs), below the orders whose row
+// passes store output pairs directly (their padding lanes have no junk row)
+#ifndef SEM_TILE_WL_STORED_N
+#define SEM_TILE_WL_STORED_N 99
+#endif
+template <int N>
+struct StoredTile {
+  static constexpr bool wl = N >= SEM_TILE_WL_STORED_N && N < SEM_ROW_STORE_PAIRS_N;
+  static constexpr int RS = wl ? WL_RS : Tile<N, stored_pad(N)>::RS;
+  static constexpr int RL = wl ? N : RS;  // doubles loaded per row
+  static constexpr int JUNK = wl ? WLTile<N>::JUNK : 0;
+};
 template <int N, int RS, bool TR, bool REL, int RL = RS, int JUNK = 0, bool SPLIT = false,
           class DT = DEO<N>>
 __device__ __forceinline__ void row_pass(double* L, int j, const DT& D, bool active = true) {
@@ -792,7 +808,10 @@ __device__ __forceinline__ void poisson_group_stored(const MapRef& mref,
                                                      const Pre& pre = Pre()) {
   using T = Tile<N, stored_pad(N)>;
   constexpr int LW = T::LW;
-  constexpr int RS = T::RS;
+  constexpr int RS = StoredTile<N>::RS;
+  constexpr int RL = StoredTile<N>::RL;
+  constexpr int JUNK = StoredTile<N>::JUNK;
+  const bool act = in_wave || !StoredTile<N>::wl;
   constexpr bool SP = N >= SEM_LDS_SPLIT_STORED_N;
   const double* gp = GP + g * (int64_t)(3 * N * LW) + lane;
   double uc[N];
@@ -808,7 +827,7 @@ __device__ __forceinline__ void poisson_group_stored(const MapRef& mref,
   for (int r = 0; r < N; ++r) L[r * RS + j] = uc[r];
   wave_sync();
   // row i = j: d1[i][q] = sum_s D[q][s] u[i][s]     (TensorProduct.deriv dim 1)
-  row_pass<N, RS, false, false>(L, j, D);
+  row_pass<N, RS, false, false, RL, JUNK>(L, j, D, act);
   // column j: w0/w1, and ya = D^T w0 along xi0 (kept in v); w1 -> tile
   {
     double w0[N];
@@ -829,7 +848,7 @@ __device__ __forceinline__ void poisson_group_stored(const MapRef& mref,
   }
   wave_sync();
   // row i = j: yb[i][q] = sum_n D[n][q] w1[i][n]
-  row_pass<N, RS, true, false>(L, j, D);
+  row_pass<N, RS, true, false, RL, JUNK>(L, j, D, act);
 #pragma unroll
   for (int p = 0; p < N; ++p) v[p] += lds_ld<SP>(L + p * RS + j);
   wave_sync();  // the tile is rewritten by the next group of this wave
@@ -1314,7 +1333,7 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
   using T = Tile<N, NODAL ? SEM_TILE_PAD_NODAL : stored_pad(N)>;
   constexpr int NT = NODAL ? 2 : 1;  // tiles per element slot
   constexpr int CW = ChainWaves<N>::value;
-  constexpr bool WL = NODAL && NodalTile<N>::wl;
+  constexpr bool WL = NODAL ? NodalTile<N>::wl : StoredTile<N>::wl;
   constexpr int PLANE = WL ? CW * WLTile<N>::WS : T::TILE_SLOTS * T::ES;  // doubles per tile plane
   __shared__ __attribute__((aligned(16))) double lds[PLANE * NT];
   __shared__ double carry[CARRY_BUFS][CW][1][N];
