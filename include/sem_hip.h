@@ -93,6 +93,33 @@ typedef struct sem_ctx sem_ctx;
 int sem_ctx_create(sem_ctx** out, int p, int64_t n_elem, int64_t n_node, int dpn, int device);
 void sem_ctx_destroy(sem_ctx* ctx);
 
+/* The same for a mesh of dimension ndim: 2 = quadrilaterals (sem_ctx_create),
+ * 3 = hexahedra.  The reference's basis layer is N-dimensional
+ * (TensorProduct.deriv / gradient, compute_coeffs_grid_eq,
+ * sem/basis_functions.py:599-650; TensorQuadratureRule.xweight,
+ * sem/quadratures.py:268-275; NCube, sem/geometry.py:32-216); only its 2x2
+ * Jacobian inverse stops at 2-D (sem/mapping.py:110-111).  On a hexahedral
+ * context (1 <= p <= 11, dpn = 1, Poisson):
+ *   - element-local arrays are [n][n][n] in lexicographic (xi0, xi1, xi2)
+ *     order, xi2 fastest; the map is uint32 [n_elem][n][n][n];
+ *   - sem_geom_from_nodes takes nodes float64 [3][n_node] and stores the 6
+ *     factors G_kl = detJxW sum_j invJ[k][j] invJ[l][j] per node;
+ *     sem_geom_fields writes x_phys [E][3][n][n][n], J / invJ
+ *     [E][3][3][n][n][n] (J[c][d] = d x_c / d xi_d, invJ = J^-1), detJ and
+ *     detJxW [E][n][n][n]; sem_set_geom takes [E][6][n][n][n] in the order
+ *     (00, 01, 02, 11, 12, 22);
+ *   - sem_apply / sem_apply_dot / sem_diag / sem_assemble / sem_zero_shared /
+ *     sem_pcg_solve work as on quadrilaterals (stored geometry, column kernel;
+ *     SEM_GEOM_NODAL, SEM_KERNEL_MFMA, node states and the axisymmetric kinds
+ *     return SEM_E_NOTIMPL);
+ *   - sem_plan_info: [0] workgroups, [1] zero list, [2] 0, [3] 1, [4]
+ *     element slots per workgroup, [5] chains along xi0, [6] sub-chain length
+ *     cap, [7] launch positions, [8] sub-chains, [9] seam nodes, [10] slotted
+ *     writes, [11] plain stores, [12] threads per workgroup, [13] 3, [14]
+ *     geometry ready. */
+int sem_ctx_create_nd(sem_ctx** out, int ndim, int p, int64_t n_elem, int64_t n_node, int dpn,
+                      int device);
+
 /* Basis of the operator: D (n*n, host) and 1-D quadrature weights w (n,
  * host): TensorProductQS.get_D1_matrices() / quad_rule.weights
  * (sem/basis_functions.py:156-162, sem/quadratures.py:246-252). */

@@ -12,7 +12,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_NAME = "libsem_hip.so"
 LIB_PATH = os.environ.get("SEM_LIB_PATH", os.path.join(PKG_DIR, LIB_NAME))
-SOURCES = ["sem_device.hip", "sem_dd.hip", "sem_sc.hip", "sem_basis.cpp"]
+SOURCES = ["sem_device.hip", "sem_dd.hip", "sem_sc.hip", "sem_basis.cpp", "sem_hex.hip"]
 # (lo, hi) order ranges of sem_launch.hip, balanced by compile time (the
 # unrolled column kernels grow with n)
 LAUNCH_RANGES = [(2, 5), (6, 8), (9, 9), (10, 11), (12, 13), (14, 15), (16, 16), (17, 17)]
@@ -23,7 +23,7 @@ LAUNCH_RANGES = [(2, 5), (6, 8), (9, 9), (10, 11), (12, 13), (14, 15), (16, 16),
 NO_LICM = ("-mllvm", "-disable-machine-licm")
 LAUNCH_CD_RANGES = [((2, 6), ()), ((7, 7), NO_LICM), ((8, 10), ()), ((11, 13), ()),
                     ((14, 15), ()), ((16, 16), ()), ((17, 17), NO_LICM)]
-DEPS = SOURCES + ["sem_launch.hip", "sem_launch_cd.hip", "sem_internal.h", "sem_kernels.h", "sem_ctx.h", "gll_table.h",
+DEPS = SOURCES + ["sem_launch.hip", "sem_launch_cd.hip", "sem_internal.h", "sem_kernels.h", "sem_ctx.h", "sem_hex.h", "gll_table.h",
                   "deo_const.h"]
 ARCH = os.environ.get("SEM_OFFLOAD_ARCH", "gfx950")
 

@@ -52,6 +52,8 @@ SIGNATURES = {
     "sem_legeval": (C.c_double, [C.c_double, C.c_uint]),
     "sem_barycentric_lagrange": (C.c_double, [_dp, C.c_uint, C.c_double]),
     "sem_ctx_create": (C.c_int, [C.POINTER(_vp), C.c_int, _i64, _i64, C.c_int, C.c_int]),
+    "sem_ctx_create_nd": (C.c_int, [C.POINTER(_vp), C.c_int, C.c_int, _i64, _i64, C.c_int,
+                                    C.c_int]),
     "sem_ctx_destroy": (None, [_vp]),
     "sem_set_basis": (C.c_int, [_vp, _dp, _dp]),
     "sem_set_map": (C.c_int, [_vp, _vp, _vp]),

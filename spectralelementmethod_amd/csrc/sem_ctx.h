@@ -63,8 +63,12 @@ inline bool seam_auto(int n, int64_t chains_per_colour, int dpn = 1, bool blocks
   return n >= 11 || chains_per_colour <= 1024 || ((n >= 9 || n == 7) && chains_per_colour <= 2400);
 }
 
+struct HexState;  // the 3-D (hexahedral) path, sem_hex.hip
+
 struct sem_ctx {
   int p = 0, n = 0, dpn = 1, device = 0;
+  int ndim = 2;              // 3: hexahedra, every entry point forwards to semh::
+  HexState* hex = nullptr;
   int64_t n_elem = 0, n_node = 0;
   int epw = 0, lw = 0;
   int64_t n_groups = 0;
@@ -315,3 +319,21 @@ int64_t seam_sum_blocks(const sem_ctx* c);
   }
 
 }  // namespace semd
+
+// the hexahedral (ndim = 3) halves of the C ABI entry points (sem_hex.hip)
+namespace semh {
+int ctx_init(sem_ctx* c);
+void ctx_free(sem_ctx* c);
+int set_map(sem_ctx* c, const uint32_t* d_e2n, hipStream_t st);
+int geom_from_nodes(sem_ctx* c, const double* d_nodes, int op_kind, int64_t* n_bad,
+                    hipStream_t st);
+int geom_fields(sem_ctx* c, const double* d_nodes, double* x_phys, double* J, double* invJ,
+                double* detJ, double* detJxW, hipStream_t st);
+int set_geom(sem_ctx* c, const double* d_G, int op_kind, hipStream_t st);
+int apply(sem_ctx* c, int op_kind, const double* u, double* y, int flags, hipStream_t st);
+int diag(sem_ctx* c, int op_kind, double* d, hipStream_t st);
+int zero_shared(sem_ctx* c, double* y, hipStream_t st);
+int plan_info(const sem_ctx* c, int64_t* info, int n_info);
+int zero_list(const sem_ctx* c, std::vector<uint32_t>* nodes, bool* only_unreferenced);
+int assemble(sem_ctx* c, const double* vals, double* out, int accumulate, hipStream_t st);
+}  // namespace semh

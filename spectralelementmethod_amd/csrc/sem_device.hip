@@ -179,6 +179,7 @@ int ctx_seam_gids(const sem_ctx* c, std::vector<uint32_t>* gids) {
 }
 void ctx_set_defer_seam_sum(sem_ctx* c, bool defer) { c->defer_seam_sum = defer; }
 int ctx_zero_list(const sem_ctx* c, std::vector<uint32_t>* nodes, bool* only_unreferenced) {
+  if (c->ndim == 3) return semh::zero_list(c, nodes, only_unreferenced);
   nodes->assign((size_t)c->n_zero, 0u);
   *only_unreferenced = c->n_atomic_groups == 0;
   if (c->n_zero) {
@@ -1122,16 +1123,25 @@ int build_plan_ecol(const std::vector<uint32_t>& e2n, int64_t n_elem, int64_t n_
 extern "C" {
 
 int sem_ctx_create(sem_ctx** out, int p, int64_t n_elem, int64_t n_node, int dpn, int device) {
+  return sem_ctx_create_nd(out, 2, p, n_elem, n_node, dpn, device);
+}
+
+int sem_ctx_create_nd(sem_ctx** out, int ndim, int p, int64_t n_elem, int64_t n_node, int dpn,
+                      int device) {
   if (!out) return fail(SEM_E_INVALID, "null ctx pointer");
   *out = nullptr;
+  if (ndim != 2 && ndim != 3)
+    return fail(SEM_E_NOTIMPL, "operators on quadrilaterals (ndim 2) and hexahedra (ndim 3) only");
   if (p < 1) return fail(SEM_E_INVALID, "Must specify an order of 1 or greater.");
   if (p > SEM_MAX_ORDER)
     return fail(SEM_E_NOTIMPL, "operator kernels built for orders 1.." +
                                    std::to_string(SEM_MAX_ORDER));
   if (n_elem < 1 || n_node < 1 || dpn < 1 || dpn > 2)
     return fail(SEM_E_INVALID, "bad sizes (n_elem, n_node >= 1, dpn in {1,2})");
-  if (n_node > (int64_t)GID_MASK)
-    return fail(SEM_E_INVALID, "n_node exceeds the per-GPU limit of 2^29 - 1 nodes");
+  if (ndim == 2 && n_node > (int64_t)GID_MASK)
+    return fail(SEM_E_INVALID, "n_node exceeds the per-GPU limit of 2^28 - 1 nodes");
+  if (n_node > (int64_t)0xFFFFFFFFll)
+    return fail(SEM_E_INVALID, "n_node exceeds the uint32 element map");
   DeviceGuard g(device);
   sem_ctx* c = new sem_ctx();
   c->p = p;
@@ -1158,6 +1168,13 @@ int sem_ctx_create(sem_ctx** out, int p, int64_t n_elem, int64_t n_node, int dpn
     sem_ctx_destroy(c);
     return fail(SEM_E_HIP, "hipMalloc failed in sem_ctx_create");
   }
+  if (ndim == 3) {
+    c->ndim = 3;
+    if (const int rc = semh::ctx_init(c)) {
+      sem_ctx_destroy(c);
+      return rc;
+    }
+  }
   *out = c;
   return SEM_OK;
 }
@@ -1165,6 +1182,7 @@ int sem_ctx_create(sem_ctx** out, int p, int64_t n_elem, int64_t n_node, int dpn
 void sem_ctx_destroy(sem_ctx* c) {
   if (!c) return;
   DeviceGuard g(c->device);
+  semh::ctx_free(c);
   (void)hipFree(c->d_D);
   (void)hipFree(c->d_w);
   (void)hipFree(c->d_Vinv);
@@ -1233,6 +1251,11 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
                        void* stream) {
   if (!c || !d_e2n) return fail(SEM_E_INVALID, "null argument");
   DeviceGuard g(c->device);
+  if (c->ndim == 3) {
+    if (d_node_state)
+      return fail(SEM_E_NOTIMPL, "sem_set_map_shared: node states on hexahedra are not supported");
+    return semh::set_map(c, d_e2n, S(stream));
+  }
   c->epoch++;
   c->map_epoch++;
   hipStream_t st = S(stream);
@@ -1399,6 +1422,7 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
 
 int sem_plan_info(sem_ctx* c, int64_t* info, int n_info) {
   if (!c || !info || n_info < 1) return fail(SEM_E_INVALID, "bad arguments");
+  if (c->ndim == 3) return semh::plan_info(c, info, n_info);
   const int64_t nc = c->colour_start.empty() ? 0 : (int64_t)c->colour_start.size() - 1;
   constexpr int NV = 8 + MAX_COLOURS + 1 + 1 + 1 + 1 + 1 + 1 + 1 + 2 + 1;
   int64_t vals[NV] = {c->n_groups, c->n_zero, c->n_atomic_groups, c->conforming ? 1 : 0,
@@ -1440,6 +1464,8 @@ int sem_set_geom_mode(sem_ctx* c, int mode) {
   if (!c) return fail(SEM_E_INVALID, "null ctx");
   if (mode != SEM_GEOM_STORED && mode != SEM_GEOM_NODAL && mode != SEM_GEOM_AUTO)
     return fail(SEM_E_INVALID, "unknown geometry mode " + std::to_string(mode));
+  if (c->ndim == 3 && mode == SEM_GEOM_NODAL)
+    return fail(SEM_E_NOTIMPL, "hexahedra: stored geometric factors only");
   c->geom_mode = mode;
   c->epoch++;
   return SEM_OK;
@@ -1458,6 +1484,8 @@ int sem_set_kernel(sem_ctx* c, int kernel) {
   if (!c) return fail(SEM_E_INVALID, "null ctx");
   if (kernel != SEM_KERNEL_COLUMN && kernel != SEM_KERNEL_MFMA && kernel != SEM_KERNEL_AUTO)
     return fail(SEM_E_INVALID, "unknown kernel " + std::to_string(kernel));
+  if (kernel == SEM_KERNEL_MFMA && c->ndim == 3)
+    return fail(SEM_E_NOTIMPL, "hexahedra: column kernel only");
   if (kernel == SEM_KERNEL_MFMA && (c->dpn != 1 || c->n > 17))
     return fail(SEM_E_NOTIMPL, "the MFMA kernel needs dofs_per_node == 1 and p <= 16");
   c->kernel = kernel;
@@ -1472,6 +1500,7 @@ int sem_geom_from_nodes(sem_ctx* c, const double* d_nodes, const double* h_Vinv,
   int rc = geom_common(c, d_nodes, h_Vinv);
   if (rc) return rc;
   if ((rc = check_op(c, op_kind))) return rc;
+  if (c->ndim == 3) return semh::geom_from_nodes(c, d_nodes, op_kind, n_bad_nodes, S(stream));
   const bool nodal = nodal_mode_op(c, op_kind);
   c->epoch++;
   double* GP = nullptr;
@@ -1511,6 +1540,7 @@ int sem_geom_fields(sem_ctx* c, const double* d_nodes, const double* h_Vinv, dou
   int rc = geom_common(c, d_nodes, h_Vinv);
   if (rc) return rc;
   hipStream_t st = S(stream);
+  if (c->ndim == 3) return semh::geom_fields(c, d_nodes, x_phys, J, invJ, detJ, detJxW, st);
   HIP_TRY(hipMemsetAsync(c->d_bad, 0, sizeof(unsigned long long), st));
   SEM_DISPATCH_N(rc, c->n, launch_geom_n, c, d_nodes, SEM_OP_POISSON, nullptr, x_phys, J, invJ,
                  detJ, detJxW, nullptr, nullptr, st);
@@ -1522,6 +1552,10 @@ int sem_geom_fields(sem_ctx* c, const double* d_nodes, const double* h_Vinv, dou
 
 int sem_set_geom(sem_ctx* c, const double* d_G, int op_kind, void* stream) {
   if (!c || !d_G) return fail(SEM_E_INVALID, "null argument");
+  if (c->ndim == 3) {
+    DeviceGuard g(c->device);
+    return semh::set_geom(c, d_G, op_kind, S(stream));
+  }
   if (!c->d_epos) return fail(SEM_E_STATE, "sem_set_map must precede sem_set_geom");
   DeviceGuard g(c->device);
   int rc;
@@ -1540,6 +1574,10 @@ int sem_set_geom(sem_ctx* c, const double* d_G, int op_kind, void* stream) {
 
 int sem_zero_shared(sem_ctx* c, double* y, void* stream) {
   if (!c || !y) return fail(SEM_E_INVALID, "null argument");
+  if (c->ndim == 3) {
+    DeviceGuard g(c->device);
+    return semh::zero_shared(c, y, S(stream));
+  }
   if (!c->d_mapP) return fail(SEM_E_STATE, "map must be set");
   DeviceGuard g(c->device);
   if (c->n_zero)
@@ -1560,6 +1598,10 @@ int sem_apply(sem_ctx* c, int op_kind, const double* u, double* y, int flags, vo
     return fail(SEM_E_INVALID, "unknown sem_apply flags");
   int rc;
   if ((rc = check_op(c, op_kind))) return rc;
+  if (c->ndim == 3) {
+    DeviceGuard g(c->device);
+    return semh::apply(c, op_kind, u, y, flags, S(stream));
+  }
   if (!c->have_basis || !c->d_mapP) return fail(SEM_E_STATE, "basis and map must be set");
   if (!use_nodal(c, op_kind) && !c->d_GP[gp_slot(op_kind)])
     return fail(SEM_E_STATE, "geometry for this operator has not been computed");
@@ -1635,6 +1677,10 @@ int sem_diag(sem_ctx* c, int op_kind, double* d_diag, void* stream) {
   if (op_kind != SEM_OP_POISSON) return fail(SEM_E_NOTIMPL, "sem_diag: Poisson only");
   int rc;
   if ((rc = check_op(c, op_kind))) return rc;
+  if (c->ndim == 3) {
+    DeviceGuard g(c->device);
+    return semh::diag(c, op_kind, d_diag, S(stream));
+  }
   if (!c->d_mapP || !(c->d_GP[0] || use_nodal(c, op_kind)))
     return fail(SEM_E_STATE, "geometry/map not set");
   DeviceGuard g(c->device);
@@ -1655,6 +1701,10 @@ int sem_diag(sem_ctx* c, int op_kind, double* d_diag, void* stream) {
 
 int sem_assemble(sem_ctx* c, const double* vals, double* out, int accumulate, void* stream) {
   if (!c || !vals || !out) return fail(SEM_E_INVALID, "null argument");
+  if (c->ndim == 3) {
+    DeviceGuard g(c->device);
+    return semh::assemble(c, vals, out, accumulate, S(stream));
+  }
   if (!c->d_e2n) return fail(SEM_E_STATE, "sem_set_map must precede sem_assemble");
   if (c->dpn != 1) return fail(SEM_E_INVALID, "sem_assemble: dofs_per_node == 1 only");
   DeviceGuard g(c->device);

@@ -1,0 +1,458 @@
+// Hexahedral (3-D) kernels of libsem_hip.so (included by sem_hex.hip only).
+//
+// The reference's tensor-product layer is N-dimensional: TensorProduct.deriv
+// / gradient apply D along any axis of an [..., n, n, n] coefficient array
+// (sem/basis_functions.py:626-650), compute_coeffs_grid_eq solves V_eq along
+// each axis (:599-624) and TensorQuadratureRule.xweight multiplies by the
+// tensor weights (sem/quadratures.py:268-275); only the 2x2 Jacobian inverse
+// (sem/mapping.py:110-111) and the quad-only example stop it at 2-D.  These
+// kernels run the same per-element algebra on hexahedra: local node (a, b, c)
+// <-> (xi0, xi1, xi2), C-contiguous, xi2 fastest, as the reference lays out
+// an [n, n, n] coefficient block.
+//
+//   u_e = u[map[e]]                                      (gather)
+//   d_k = D along xi_k of u_e,  k = 0, 1, 2              (D(x)I(x)I, I(x)D(x)I, I(x)I(x)D)
+//   w_k = sum_l G_kl d_l,  G = detJxW invJ invJ^T        (6 factors per node)
+//   y_e = sum_k D^T along xi_k of w_k                    (transposed pass)
+//   y[map[e]] += y_e                                     (scatter, no atomics)
+//
+// CDNA4 mapping:
+//  * one element = an n x n tile of threads, thread (b, c) owns the element
+//    COLUMN of nodes (0..n-1, b, c) along xi0 in registers; a 256-thread
+//    workgroup holds S = floor(256 / n^2) such tiles ("slots").  The xi0
+//    contractions run in registers; the xi1 / xi2 ones read the other
+//    threads' columns from LDS (three n^3 buffers per slot: u, w1, w2, so an
+//    element costs two workgroup barriers).
+//  * each slot walks a CHAIN of elements along xi0 (consecutive elements of a
+//    chain share their xi0 face with identical (b, c) ordering): the node row
+//    a = n-1 of one element IS row a = 0 of the next, held by the same
+//    thread, so that face is summed in a register and written once.
+//  * every other node shared by several writers (element edges / faces
+//    between chains, chain ends) is written into a per-writer SLOT and summed
+//    in a fixed order by a second launch (k_hex_seam_sum): deterministic, no
+//    atomics; nodes with one writer are plain stores.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace semh {
+
+constexpr int HEX_MIN_N = 2;
+constexpr int HEX_MAX_N = 12;  // p <= 11
+
+// element slots per workgroup: as many n x n thread tiles as fit in 256 threads
+constexpr int hex_slots(int n) { return 256 / (n * n) > 0 ? 256 / (n * n) : 1; }
+constexpr int hex_threads(int n) { return (hex_slots(n) * n * n + 63) / 64 * 64; }
+// boundary columns of an element: b or c on the element boundary
+constexpr int hex_nbc(int n) { return 4 * (n - 1); }
+
+// launch tables of the hex plan (device pointers; sem_hex.hip builds them)
+struct HexLaunch {
+  const int* wg_off;                // [n_wg] first launch position of workgroup w
+  const int* wg_len;                // [n_wg] chain length of workgroup w
+  const int* elist;                 // [pos] element at position wg_off + k*S + s, -1 = empty slot
+  const unsigned long long* cmask;  // [pos] boundary columns written into slots
+  const uint8_t* cflag;             // [n_wg*S] bit 0: chain head face slotted, bit 1: tail face
+  double* slot;                     // column slots [pos][n][NBC], then face slots [n_wg*S][2][n^2]
+  int64_t face_base;
+};
+
+enum { HEX_SET = 0, HEX_ACC = 1, HEX_DIAG = 2 };
+
+// boundary-column index of (b, c) in [0, 4(n-1)), -1 for an interior column
+template <int N>
+__device__ __forceinline__ int hex_bcol(int b, int c) {
+  if (b == 0) return c;
+  if (b == N - 1) return 3 * N - 4 + c;
+  if (c == 0) return N + 2 * (b - 1);
+  if (c == N - 1) return N + 2 * (b - 1) + 1;
+  return -1;
+}
+
+// Poisson stiffness action on hexahedra (MODE HEX_SET / HEX_ACC), or the
+// diagonal of the assembled operator (HEX_DIAG; u unused).  G: stored factors
+// [E][a][6][b*n + c], components (00, 01, 02, 11, 12, 22).
+#ifndef SEM_HEX_MIN_WAVES
+#define SEM_HEX_MIN_WAVES 4
+#endif
+template <int N, int MODE>
+__global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
+    k_hex_poisson(const double* __restrict__ u, double* __restrict__ y,
+                  const uint32_t* __restrict__ map, const double* __restrict__ G,
+                  const double* __restrict__ gD, HexLaunch P) {
+  constexpr int N2 = N * N, N3 = N2 * N, S = hex_slots(N), T = hex_threads(N), NBC = hex_nbc(N);
+  __shared__ double sD[N2];
+  __shared__ double sU[S * N3];
+  __shared__ double sA[S * N3];
+  __shared__ double sB[S * N3];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < N2; i += T) sD[i] = gD[i];
+  const int w = blockIdx.x;
+  const int L = P.wg_len[w];
+  const int base = P.wg_off[w];
+  const int s = tid / N2;
+  const int bc = tid - s * N2;
+  const int b = bc / N, c = bc - b * N;
+  const bool active = s < S && P.elist[base + s] >= 0;
+  const int sl = active ? s : 0;
+  double* const su = sU + sl * N3;
+  double* const sa = sA + sl * N3;
+  double* const sb = sB + sl * N3;
+  const int bcol = hex_bcol<N>(b, c);
+  const uint8_t cf = active ? P.cflag[w * S + s] : 0;
+  double* const face = P.slot + P.face_base + (int64_t)(w * S + sl) * 2 * N2 + bc;
+  __syncthreads();  // sD
+  double carry = 0.0;
+#pragma unroll 1
+  for (int k = 0; k < L; ++k) {
+    const int pos = base + k * S + s;
+    const int e = active ? P.elist[pos] : 0;
+    uint32_t m[N];
+    const double* g = G + (int64_t)e * 6 * N3 + bc;
+    if (active) {
+      const uint32_t* me = map + (int64_t)e * N3 + bc;
+#pragma unroll
+      for (int a = 0; a < N; ++a) m[a] = me[a * N2];
+      if constexpr (MODE != HEX_DIAG) {
+        double uc[N];
+#pragma unroll
+        for (int a = 0; a < N; ++a) uc[a] = u[m[a]];
+#pragma unroll
+        for (int a = 0; a < N; ++a) su[a * N2 + bc] = uc[a];
+      } else {
+        // diagonal: G00 of this column, G11 / G22 of the other threads' nodes
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+          su[a * N2 + bc] = g[(a * 6 + 0) * N2];
+          sa[a * N2 + bc] = g[(a * 6 + 3) * N2];
+          sb[a * N2 + bc] = g[(a * 6 + 5) * N2];
+        }
+      }
+    }
+    __syncthreads();
+    // The contractions run with the summation index outermost and NOT
+    // unrolled, the node row a unrolled inside: every register array is
+    // indexed by a compile-time a, and a step holds only its own operands
+    // (a fully unrolled a x r nest lets the scheduler hoist the LDS and G
+    // reads of later rows: 256+ VGPRs and spills from n = 6 on).
+    double yv[N];
+#pragma unroll
+    for (int a = 0; a < N; ++a) yv[a] = 0.0;
+    if constexpr (MODE != HEX_DIAG) {
+      double w0[N];
+      if (active) {
+        double d0[N], d1[N], d2[N];
+#pragma unroll
+        for (int a = 0; a < N; ++a) d0[a] = d1[a] = d2[a] = 0.0;
+#pragma unroll 1
+        for (int r = 0; r < N; ++r) {
+          const double ur = su[r * N2 + bc];
+          const double dbr = sD[b * N + r], dcr = sD[c * N + r];
+#pragma unroll
+          for (int a = 0; a < N; ++a) {
+            d0[a] = fma(sD[a * N + r], ur, d0[a]);
+            d1[a] = fma(dbr, su[a * N2 + r * N + c], d1[a]);
+            d2[a] = fma(dcr, su[a * N2 + b * N + r], d2[a]);
+          }
+        }
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+          const double* ga = g + a * 6 * N2;
+          const double g00 = ga[0], g01 = ga[N2], g02 = ga[2 * N2], g11 = ga[3 * N2],
+                       g12 = ga[4 * N2], g22 = ga[5 * N2];
+          w0[a] = g00 * d0[a] + g01 * d1[a] + g02 * d2[a];
+          sa[a * N2 + bc] = g01 * d0[a] + g11 * d1[a] + g12 * d2[a];
+          sb[a * N2 + bc] = g02 * d0[a] + g12 * d1[a] + g22 * d2[a];
+        }
+      }
+      __syncthreads();
+      if (active) {
+        // w0 into this thread's own column of su (no other thread reads it
+        // until the next element's first barrier)
+#pragma unroll
+        for (int a = 0; a < N; ++a) su[a * N2 + bc] = w0[a];
+#pragma unroll 1
+        for (int q = 0; q < N; ++q) {
+          const double wq = su[q * N2 + bc];
+          const double dqb = sD[q * N + b], dqc = sD[q * N + c];
+#pragma unroll
+          for (int a = 0; a < N; ++a) {
+            yv[a] = fma(sD[q * N + a], wq, yv[a]);
+            yv[a] = fma(dqb, sa[a * N2 + q * N + c], yv[a]);
+            yv[a] = fma(dqc, sb[a * N2 + b * N + q], yv[a]);
+          }
+        }
+      }
+    } else {
+      if (active) {
+        // K_ii = sum_q D[q][a]^2 G00[q,b,c] + D[q][b]^2 G11[a,q,c] + D[q][c]^2 G22[a,b,q]
+        //        + 2 (D[a][a] D[b][b] G01 + D[a][a] D[c][c] G02 + D[b][b] D[c][c] G12)[a,b,c]
+        const double dbb = sD[b * N + b], dcc = sD[c * N + c];
+#pragma unroll 1
+        for (int q = 0; q < N; ++q) {
+          const double g0 = su[q * N2 + bc];
+          const double db = sD[q * N + b], dc = sD[q * N + c];
+#pragma unroll
+          for (int a = 0; a < N; ++a) {
+            const double da = sD[q * N + a];
+            yv[a] = fma(da * da, g0, yv[a]);
+            yv[a] = fma(db * db, sa[a * N2 + q * N + c], yv[a]);
+            yv[a] = fma(dc * dc, sb[a * N2 + b * N + q], yv[a]);
+          }
+        }
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+          const double* ga = g + a * 6 * N2;
+          const double daa = sD[a * N + a];
+          yv[a] += 2.0 * (daa * dbb * ga[N2] + daa * dcc * ga[2 * N2] + dbb * dcc * ga[4 * N2]);
+        }
+      }
+      __syncthreads();  // su / sa / sb are rewritten by the next element
+    }
+    if (active) {
+      if (k > 0) yv[0] += carry;
+      const bool last = k == L - 1;
+      if (!last) carry = yv[N - 1];
+      const bool colslot = bcol >= 0 && ((P.cmask[pos] >> bcol) & 1ull);
+      double* const cs = P.slot + ((int64_t)pos * N) * NBC + bcol;
+#pragma unroll
+      for (int a = 0; a < N; ++a) {
+        if (a == N - 1 && !last) continue;  // carried into the next element's row 0
+        const double v = yv[a];
+        if (a == 0 && k == 0 && (cf & 1)) {
+          face[0] = v;
+        } else if (a == N - 1 && last && (cf & 2)) {
+          face[N2] = v;
+        } else if (colslot) {
+          cs[a * NBC] = v;
+        } else {
+          if constexpr (MODE == HEX_ACC)
+            y[m[a]] += v;
+          else
+            y[m[a]] = v;
+        }
+      }
+    }
+  }
+}
+
+// y[gid[i]] (=|+=) sum of the slot values of seam node i, in plan order
+template <bool ACC>
+__global__ void k_hex_seam_sum(double* __restrict__ y, const uint32_t* __restrict__ gid,
+                               const uint32_t* __restrict__ ptr, const uint32_t* __restrict__ idx,
+                               int64_t n, const double* __restrict__ slot) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t j0 = ptr[i], j1 = ptr[i + 1];
+    double v = 0.0;
+    for (uint32_t j = j0; j < j1; ++j) v += slot[idx[j]];
+    if (ACC)
+      y[gid[i]] += v;
+    else
+      y[gid[i]] = v;
+  }
+}
+
+// Geometry of hexahedra from equispaced element nodes (d_nodes [3][n_node]):
+//   x_phys = (V^-1 (x) V^-1 (x) V^-1) X       TensorProduct.compute_coeffs_grid_eq
+//                                             (sem/basis_functions.py:599-624) in 3-D
+//   J[c][d] = d x_c / d xi_d                  gradient(x_phys).swapaxes(0, 1)
+//                                             (sem/mapping.py:113-114)
+//   det, invJ = J^-1 (cofactors)              the 3x3 twin of det_inv_2x2 (sem/linalg.py:105-115)
+//   detJxW = ((det w_a) w_b) w_c              TensorQuadratureRule.xweight (sem/quadratures.py:268-275)
+//   G_kl = detJxW sum_j invJ[k][j] invJ[l][j]
+// The transforms act on coordinates relative to the element's node (0,0,0)
+// (the constant is added back to x_phys) to keep the rounding of V^-1's
+// large alternating entries off the absolute position.  Outputs may be null:
+// GP [E][a][6][n^2] (the action's layout), x_phys [E][3][n^3], J / invJ
+// [E][3][3][n^3], detJ / detJxW [E][n^3].  bad counts nodes with detJ <= 0.
+template <int N>
+__global__ void __launch_bounds__(hex_threads(N))
+    k_hex_geom(const double* __restrict__ nodes, int64_t n_node, const uint32_t* __restrict__ map,
+               int64_t n_elem, const double* __restrict__ gV, const double* __restrict__ gD,
+               const double* __restrict__ gw, double* __restrict__ GP, double* __restrict__ xph,
+               double* __restrict__ Jo, double* __restrict__ iJo, double* __restrict__ dJo,
+               double* __restrict__ dJWo, unsigned long long* __restrict__ bad) {
+  constexpr int N2 = N * N, N3 = N2 * N, S = hex_slots(N), T = hex_threads(N);
+  __shared__ double sV[N2], sD[N2], sw[N];
+  __shared__ double sX[3][S * N3];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < N2; i += T) {
+    sV[i] = gV[i];
+    sD[i] = gD[i];
+  }
+  for (int i = tid; i < N; i += T) sw[i] = gw[i];
+  const int s = tid / N2;
+  const int bc = tid - s * N2;
+  const int b = bc / N, c = bc - b * N;
+  const int sl = s < S ? s : 0;
+  unsigned long long nbad = 0;
+  __syncthreads();
+#pragma unroll 1
+  for (int64_t e0 = (int64_t)blockIdx.x * S; e0 < n_elem; e0 += (int64_t)gridDim.x * S) {
+    const int64_t e = e0 + s;
+    const bool active = s < S && e < n_elem;
+    double x[3][N];
+    double xr[3] = {0.0, 0.0, 0.0};
+    double* const sx0 = sX[0] + sl * N3;
+    double* const sx1 = sX[1] + sl * N3;
+    double* const sx2 = sX[2] + sl * N3;
+    double* const sxk[3] = {sx0, sx1, sx2};
+    if (active) {
+      const uint32_t* me = map + e * N3;
+      const uint32_t g0 = me[0];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) xr[k] = nodes[k * n_node + g0];
+      double xe[3][N];
+#pragma unroll
+      for (int a = 0; a < N; ++a) {
+        const uint32_t gi = me[a * N2 + bc];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) xe[k][a] = nodes[k * n_node + gi] - xr[k];
+      }
+      // xi0: registers
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+          double v = 0.0;
+#pragma unroll
+          for (int r = 0; r < N; ++r) v = fma(sV[a * N + r], xe[k][r], v);
+          sxk[k][a * N2 + bc] = v;
+        }
+    }
+    __syncthreads();
+    if (active) {  // xi1
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+          double v = 0.0;
+#pragma unroll
+          for (int r = 0; r < N; ++r) v = fma(sV[b * N + r], sxk[k][a * N2 + r * N + c], v);
+          x[k][a] = v;
+        }
+    }
+    __syncthreads();
+    if (active)
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int a = 0; a < N; ++a) sxk[k][a * N2 + bc] = x[k][a];
+    __syncthreads();
+    if (active) {  // xi2
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+          double v = 0.0;
+#pragma unroll
+          for (int r = 0; r < N; ++r) v = fma(sV[c * N + r], sxk[k][a * N2 + b * N + r], v);
+          x[k][a] = v;  // x_phys relative to node (0,0,0)
+        }
+    }
+    __syncthreads();
+    if (active)
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int a = 0; a < N; ++a) sxk[k][a * N2 + bc] = x[k][a];
+    __syncthreads();
+    if (active) {
+#pragma unroll
+      for (int a = 0; a < N; ++a) {
+        double J[3][3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          double j0 = 0.0, j1 = 0.0, j2 = 0.0;
+#pragma unroll
+          for (int r = 0; r < N; ++r) {
+            j0 = fma(sD[a * N + r], x[k][r], j0);
+            j1 = fma(sD[b * N + r], sxk[k][a * N2 + r * N + c], j1);
+            j2 = fma(sD[c * N + r], sxk[k][a * N2 + b * N + r], j2);
+          }
+          J[k][0] = j0;
+          J[k][1] = j1;
+          J[k][2] = j2;
+        }
+        const double c00 = J[1][1] * J[2][2] - J[1][2] * J[2][1];
+        const double c01 = J[1][2] * J[2][0] - J[1][0] * J[2][2];
+        const double c02 = J[1][0] * J[2][1] - J[1][1] * J[2][0];
+        const double det = J[0][0] * c00 + J[0][1] * c01 + J[0][2] * c02;
+        const double r = 1.0 / det;
+        double iJ[3][3];
+        iJ[0][0] = c00 * r;
+        iJ[1][0] = c01 * r;
+        iJ[2][0] = c02 * r;
+        iJ[0][1] = (J[0][2] * J[2][1] - J[0][1] * J[2][2]) * r;
+        iJ[1][1] = (J[0][0] * J[2][2] - J[0][2] * J[2][0]) * r;
+        iJ[2][1] = (J[0][1] * J[2][0] - J[0][0] * J[2][1]) * r;
+        iJ[0][2] = (J[0][1] * J[1][2] - J[0][2] * J[1][1]) * r;
+        iJ[1][2] = (J[0][2] * J[1][0] - J[0][0] * J[1][2]) * r;
+        iJ[2][2] = (J[0][0] * J[1][1] - J[0][1] * J[1][0]) * r;
+        if (!(det > 0.0)) ++nbad;
+        const double W = ((det * sw[a]) * sw[b]) * sw[c];
+        const int64_t node = e * N3 + a * N2 + bc;
+        if (GP) {
+          double* gp = GP + (e * N + a) * 6 * N2 + bc;
+          gp[0] = W * (iJ[0][0] * iJ[0][0] + iJ[0][1] * iJ[0][1] + iJ[0][2] * iJ[0][2]);
+          gp[N2] = W * (iJ[0][0] * iJ[1][0] + iJ[0][1] * iJ[1][1] + iJ[0][2] * iJ[1][2]);
+          gp[2 * N2] = W * (iJ[0][0] * iJ[2][0] + iJ[0][1] * iJ[2][1] + iJ[0][2] * iJ[2][2]);
+          gp[3 * N2] = W * (iJ[1][0] * iJ[1][0] + iJ[1][1] * iJ[1][1] + iJ[1][2] * iJ[1][2]);
+          gp[4 * N2] = W * (iJ[1][0] * iJ[2][0] + iJ[1][1] * iJ[2][1] + iJ[1][2] * iJ[2][2]);
+          gp[5 * N2] = W * (iJ[2][0] * iJ[2][0] + iJ[2][1] * iJ[2][1] + iJ[2][2] * iJ[2][2]);
+        }
+        if (xph)
+#pragma unroll
+          for (int k = 0; k < 3; ++k) xph[(e * 3 + k) * N3 + a * N2 + bc] = x[k][a] + xr[k];
+        if (Jo)
+#pragma unroll
+          for (int k = 0; k < 3; ++k)
+#pragma unroll
+            for (int d = 0; d < 3; ++d) Jo[((e * 3 + k) * 3 + d) * N3 + a * N2 + bc] = J[k][d];
+        if (iJo)
+#pragma unroll
+          for (int k = 0; k < 3; ++k)
+#pragma unroll
+            for (int d = 0; d < 3; ++d) iJo[((e * 3 + k) * 3 + d) * N3 + a * N2 + bc] = iJ[k][d];
+        if (dJo) dJo[node] = det;
+        if (dJWo) dJWo[node] = W;
+      }
+    }
+    __syncthreads();  // sX is rewritten by the next element
+  }
+  if (nbad) atomicAdd(bad, nbad);
+}
+
+__global__ void k_hex_zero(double* __restrict__ y, const uint32_t* __restrict__ idx, int64_t n) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n;
+       t += (int64_t)gridDim.x * blockDim.x)
+    y[idx[t]] = 0.0;
+}
+
+// out[map[e][a][b][c]] += vals[e][a][b][c] (setup-time assembly, e.g. load vectors)
+__global__ void k_hex_assemble(const uint32_t* __restrict__ e2n, const double* __restrict__ vals,
+                               int64_t total, double* __restrict__ out) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x)
+    unsafeAtomicAdd(out + e2n[t], vals[t]);
+}
+
+// user factors [E][6][n^3] -> the action's layout [E][a][6][n^2]
+__global__ void k_hex_pack_geom(const double* __restrict__ G, int64_t n_elem, int n,
+                                double* __restrict__ GP) {
+  const int64_t n2 = (int64_t)n * n, n3 = n2 * n;
+  const int64_t total = n_elem * 6 * n3;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = t / (6 * n3);
+    const int64_t rem = t - e * 6 * n3;
+    const int comp = (int)(rem / n3);
+    const int64_t node = rem - comp * n3;
+    const int64_t a = node / n2, bc = node - a * n2;
+    GP[((e * n + a) * 6 + comp) * n2 + bc] = G[t];
+  }
+}
+
+}  // namespace semh

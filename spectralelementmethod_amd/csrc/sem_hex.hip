@@ -1,0 +1,610 @@
+// Hexahedral (3-D) operator path of libsem_hip.so: the scatter planner (host,
+// once per map), the per-order launches of sem_hex.h and the 3-D halves of
+// the C ABI entry points (sem_device.hip forwards a context created with
+// ndim = 3 here).  DESIGN.md §4.9 / §5.3.
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <numeric>
+#include <unordered_map>
+
+#include "sem_ctx.h"
+#include "sem_hex.h"
+
+using sem::fail;
+using semd::DeviceGuard;
+using semd::grid_for;
+
+struct HexState {
+  int N = 0, slots = 0, threads = 0, nbc = 0;
+  // launch tables (HexLaunch)
+  int64_t n_wg = 0, n_pos = 0;
+  int* d_wg_off = nullptr;
+  int* d_wg_len = nullptr;
+  int* d_elist = nullptr;
+  unsigned long long* d_cmask = nullptr;
+  uint8_t* d_cflag = nullptr;
+  double* d_slot = nullptr;
+  int64_t face_base = 0, n_slot = 0;
+  // seam sums: seam node i = gid[i] sums slot[idx[ptr[i] .. ptr[i+1])]
+  uint32_t* d_seam_gid = nullptr;
+  uint32_t* d_seam_ptr = nullptr;
+  uint32_t* d_seam_idx = nullptr;
+  int64_t n_seam = 0, n_seam_writes = 0;
+  uint32_t* d_zero = nullptr;  // unreferenced nodes (overwrite mode zeroes them)
+  int64_t n_zero = 0;
+  uint32_t* d_map = nullptr;   // the library's copy of the caller's map [E][n][n][n]
+  double* d_G = nullptr;       // stored factors [E][a][6][n^2]
+  bool have_G = false;
+  // diagnostics (sem_plan_info)
+  int64_t n_chains = 0, n_subchains = 0, chain_len = 0, n_direct = 0;
+
+  void free_plan() {
+    for (void* p : {(void*)d_wg_off, (void*)d_wg_len, (void*)d_elist, (void*)d_cmask,
+                    (void*)d_cflag, (void*)d_slot, (void*)d_seam_gid, (void*)d_seam_ptr,
+                    (void*)d_seam_idx, (void*)d_zero})
+      (void)hipFree(p);
+    d_wg_off = d_wg_len = d_elist = nullptr;
+    d_cmask = nullptr;
+    d_cflag = nullptr;
+    d_slot = nullptr;
+    d_seam_gid = d_seam_ptr = d_seam_idx = d_zero = nullptr;
+    n_wg = n_pos = n_slot = n_seam = n_seam_writes = n_zero = 0;
+  }
+};
+
+namespace {
+
+int hex_check_order(int n) {
+  if (n < semh::HEX_MIN_N || n > semh::HEX_MAX_N)
+    return fail(SEM_E_NOTIMPL, "hexahedral kernels are built for orders 1.." +
+                                   std::to_string(semh::HEX_MAX_N - 1));
+  return SEM_OK;
+}
+
+template <typename T>
+int upload(T** dst, const std::vector<T>& v) {
+  (void)hipFree(*dst);
+  *dst = nullptr;
+  if (v.empty()) return SEM_OK;
+  HIP_TRY(hipMalloc(dst, v.size() * sizeof(T)));
+  HIP_TRY(hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  return SEM_OK;
+}
+
+uint64_t face_hash(const uint32_t* f, int n2) {
+  uint64_t h = 0x9E3779B97F4A7C15ull;
+  for (int j = 0; j < n2; ++j) {
+    h ^= f[j] + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+    h *= 0xBF58476D1CE4E5B9ull;
+  }
+  return h ^ (h >> 31);
+}
+
+// ---------------------------------------------------------------------------
+// Planner.  Chains follow xi0: element e' succeeds e when e's face a = n-1 is
+// e''s face a = 0 node for node (same (b, c) order), so one thread holds the
+// shared node row of both.  Chains are cut into sub-chains of <= Lc elements
+// so that the launch has enough workgroups; a workgroup runs S sub-chains of
+// equal length in lockstep (slot s of step k = launch position
+// wg_off + k*S + s).
+//
+// Every (element, node) the kernel writes is a write EVENT, except row
+// a = n-1 of a non-last chain element (carried).  A node with one event is a
+// plain store.  A node with several events is a SEAM node: each of its events
+// goes to a slot of its own and k_hex_seam_sum adds them.  The kernel decides
+// per thread and element from two small masks: a boundary column (b or c on
+// the element boundary) is slotted as a whole when any of its events is on a
+// seam node (cmask bit), a chain's first / last face likewise (cflag).  The
+// planner replays exactly that rule, checks that every plain store hits a
+// one-event node (conforming mesh) and lists the slots of each seam node.
+struct HexPlanHost {
+  std::vector<int> wg_off, wg_len, elist;
+  std::vector<unsigned long long> cmask;
+  std::vector<uint8_t> cflag;
+  std::vector<uint32_t> seam_gid, seam_ptr, seam_idx, zero;
+  int64_t n_slot = 0, face_base = 0, n_chains = 0, n_sub = 0, lc = 0, n_direct = 0;
+};
+
+int hex_build_plan(const std::vector<uint32_t>& h, int64_t E, int64_t n_node, int N,
+                   int64_t target_wgs, HexPlanHost& P) {
+  const int N2 = N * N;
+  const int64_t N3 = (int64_t)N2 * N;
+  const int S = semh::hex_slots(N), NBC = semh::hex_nbc(N);
+  for (size_t i = 0; i < h.size(); ++i)
+    if (h[i] >= (uint64_t)n_node) return fail(SEM_E_INVALID, "element map entry >= n_node");
+  // 1. successors along xi0
+  std::vector<int64_t> succ(E, -1), pred(E, -1);
+  {
+    std::unordered_map<uint64_t, int64_t> first;
+    first.reserve((size_t)E * 2);
+    for (int64_t e = 0; e < E; ++e) {
+      auto it = first.emplace(face_hash(&h[e * N3], N2), e);
+      if (!it.second) it.first->second = -1;  // ambiguous: never chained
+    }
+    for (int64_t e = 0; e < E; ++e) {
+      const uint32_t* fl = &h[e * N3 + (int64_t)(N - 1) * N2];
+      auto it = first.find(face_hash(fl, N2));
+      if (it == first.end() || it->second < 0 || it->second == e) continue;
+      const int64_t e2 = it->second;
+      if (std::memcmp(fl, &h[e2 * N3], sizeof(uint32_t) * N2) != 0) continue;
+      if (pred[e2] >= 0) continue;
+      succ[e] = e2;
+      pred[e2] = e;
+    }
+  }
+  // 2. maximal chains (heads without predecessor; then any cycle, cut anywhere)
+  std::vector<int64_t> order;
+  std::vector<int64_t> chain_start;
+  order.reserve(E);
+  {
+    std::vector<uint8_t> seen(E, 0);
+    auto walk = [&](int64_t e) {
+      chain_start.push_back((int64_t)order.size());
+      while (e >= 0 && !seen[e]) {
+        seen[e] = 1;
+        order.push_back(e);
+        e = succ[e];
+      }
+    };
+    for (int64_t e = 0; e < E; ++e)
+      if (pred[e] < 0) walk(e);
+    for (int64_t e = 0; e < E; ++e)
+      if (!seen[e]) walk(e);
+    chain_start.push_back((int64_t)order.size());
+  }
+  const int64_t n_chains = (int64_t)chain_start.size() - 1;
+  // 3. sub-chains of near-equal length <= lc
+  int64_t lc = E / std::max<int64_t>(1, (int64_t)S * target_wgs);
+  lc = std::max<int64_t>(1, std::min<int64_t>(lc, 16));
+  if (const char* s = std::getenv("SEM_HEX_CHAIN")) lc = std::max(1, std::atoi(s));
+  struct Sub {
+    int64_t start, len;
+  };
+  std::vector<Sub> sub;
+  for (int64_t ch = 0; ch < n_chains; ++ch) {
+    const int64_t a0 = chain_start[ch], M = chain_start[ch + 1] - a0;
+    const int64_t parts = (M + lc - 1) / lc;
+    const int64_t q = M / parts, r = M % parts;
+    int64_t off = a0;
+    for (int64_t k = 0; k < parts; ++k) {
+      const int64_t len = q + (k < r ? 1 : 0);
+      sub.push_back({off, len});
+      off += len;
+    }
+  }
+  // 4. longest first, then by head element (neighbouring sub-chains share
+  //    faces: they run in the same or adjacent workgroups)
+  std::stable_sort(sub.begin(), sub.end(), [&](const Sub& x, const Sub& y) {
+    if (x.len != y.len) return x.len > y.len;
+    return order[x.start] < order[y.start];
+  });
+  // 5. workgroups of S equal-length sub-chains
+  std::vector<int64_t> sub_wg(sub.size()), sub_slot(sub.size());
+  int64_t pos = 0;
+  for (size_t i = 0; i < sub.size();) {
+    const int64_t len = sub[i].len;
+    size_t j = i;
+    while (j < sub.size() && j - i < (size_t)S && sub[j].len == len) ++j;
+    const int64_t w = (int64_t)P.wg_off.size();
+    if (pos > 0x7FFFFFFFll - len * S) return fail(SEM_E_INVALID, "hex plan: too many elements");
+    P.wg_off.push_back((int)pos);
+    P.wg_len.push_back((int)len);
+    for (int64_t k = 0; k < len; ++k)
+      for (int s = 0; s < S; ++s) {
+        const size_t si = i + s;
+        P.elist.push_back(si < j ? (int)order[sub[si].start + k] : -1);
+      }
+    for (size_t si = i; si < j; ++si) {
+      sub_wg[si] = w;
+      sub_slot[si] = (int64_t)(si - i);
+    }
+    pos += len * S;
+    i = j;
+  }
+  const int64_t n_wg = (int64_t)P.wg_off.size(), n_pos = pos;
+  P.cmask.assign(n_pos, 0ull);
+  P.cflag.assign(n_wg * S, 0);
+  // 6. events per node
+  std::vector<uint8_t> cnt(n_node, 0);
+  auto bump = [&](uint32_t g) {
+    if (cnt[g] < 255) ++cnt[g];
+  };
+  for (size_t i = 0; i < sub.size(); ++i) {
+    const int64_t len = sub[i].len;
+    for (int64_t k = 0; k < len; ++k) {
+      const uint32_t* me = &h[order[sub[i].start + k] * N3];
+      const int amax = (k == len - 1) ? N : N - 1;
+      for (int64_t t = 0; t < (int64_t)amax * N2; ++t) bump(me[t]);
+    }
+  }
+  // 7. face flags, column masks
+  auto bcol_of = [&](int b, int c) -> int {
+    if (b == 0) return c;
+    if (b == N - 1) return 3 * N - 4 + c;
+    if (c == 0) return N + 2 * (b - 1);
+    if (c == N - 1) return N + 2 * (b - 1) + 1;
+    return -1;
+  };
+  for (size_t i = 0; i < sub.size(); ++i) {
+    const int64_t len = sub[i].len;
+    const uint32_t* hd = &h[order[sub[i].start] * N3];
+    const uint32_t* tl = &h[order[sub[i].start + len - 1] * N3 + (int64_t)(N - 1) * N2];
+    uint8_t f = 0;
+    for (int j = 0; j < N2; ++j) {
+      if (cnt[hd[j]] > 1) f |= 1;
+      if (cnt[tl[j]] > 1) f |= 2;
+    }
+    P.cflag[sub_wg[i] * S + sub_slot[i]] = f;
+    for (int64_t k = 0; k < len; ++k) {
+      const int64_t p = P.wg_off[sub_wg[i]] + k * S + sub_slot[i];
+      const uint32_t* me = &h[order[sub[i].start + k] * N3];
+      unsigned long long mask = 0;
+      for (int b = 0; b < N; ++b)
+        for (int c = 0; c < N; ++c) {
+          const int bcol = bcol_of(b, c);
+          if (bcol < 0) continue;
+          for (int a = 0; a < N; ++a) {
+            if (a == N - 1 && k < len - 1) continue;
+            if (a == 0 && k == 0 && (f & 1)) continue;
+            if (a == N - 1 && k == len - 1 && (f & 2)) continue;
+            if (cnt[me[a * N2 + b * N + c]] > 1) {
+              mask |= 1ull << bcol;
+              break;
+            }
+          }
+        }
+      P.cmask[p] = mask;
+    }
+  }
+  // 8. replay the kernel's rule: plain stores must hit one-event nodes; the
+  //    slotted events of each seam node, in a fixed order (counting sort)
+  P.face_base = n_pos * N * NBC;
+  P.n_slot = P.face_base + n_wg * S * 2 * N2;
+  if (P.n_slot >= 0xFFFFFFFFll) return fail(SEM_E_INVALID, "hex plan: slot space exceeds 2^32");
+  std::vector<uint32_t> scount(n_node + 1, 0);
+  int64_t n_direct = 0;
+  auto for_events = [&](auto&& fn) -> int {
+    for (size_t i = 0; i < sub.size(); ++i) {
+      const int64_t len = sub[i].len, w = sub_wg[i], s = sub_slot[i];
+      const uint8_t f = P.cflag[w * S + s];
+      for (int64_t k = 0; k < len; ++k) {
+        const int64_t p = P.wg_off[w] + k * S + s;
+        const uint32_t* me = &h[order[sub[i].start + k] * N3];
+        const unsigned long long mask = P.cmask[p];
+        for (int b = 0; b < N; ++b)
+          for (int c = 0; c < N; ++c) {
+            const int bc = b * N + c, bcol = bcol_of(b, c);
+            const bool colslot = bcol >= 0 && ((mask >> bcol) & 1ull);
+            for (int a = 0; a < N; ++a) {
+              if (a == N - 1 && k < len - 1) continue;
+              const uint32_t g = me[a * N2 + bc];
+              int64_t sidx = -1;
+              if (a == 0 && k == 0 && (f & 1))
+                sidx = P.face_base + (w * S + s) * 2 * N2 + bc;
+              else if (a == N - 1 && k == len - 1 && (f & 2))
+                sidx = P.face_base + (w * S + s) * 2 * N2 + N2 + bc;
+              else if (colslot)
+                sidx = (p * N + a) * NBC + bcol;
+              if (int rc = fn(g, sidx)) return rc;
+            }
+          }
+      }
+    }
+    return SEM_OK;
+  };
+  int rc = for_events([&](uint32_t g, int64_t sidx) -> int {
+    if (sidx < 0) {
+      if (cnt[g] != 1)
+        return fail(SEM_E_NOTIMPL,
+                    "hex plan: a node inside an element column is shared (non-conforming mesh)");
+      ++n_direct;
+    } else {
+      ++scount[g];
+    }
+    return SEM_OK;
+  });
+  if (rc) return rc;
+  std::vector<uint32_t> start(n_node + 1, 0);
+  for (int64_t g = 0; g < n_node; ++g) start[g + 1] = start[g] + scount[g];
+  const uint32_t n_writes = start[n_node];
+  P.seam_idx.assign(n_writes, 0);
+  std::vector<uint32_t> fill(start.begin(), start.end() - 1);
+  for_events([&](uint32_t g, int64_t sidx) -> int {
+    if (sidx >= 0) P.seam_idx[fill[g]++] = (uint32_t)sidx;
+    return SEM_OK;
+  });
+  P.seam_ptr.push_back(0);
+  for (int64_t g = 0; g < n_node; ++g) {
+    if (scount[g]) {
+      P.seam_gid.push_back((uint32_t)g);
+      P.seam_ptr.push_back(start[g + 1]);
+    }
+    if (cnt[g] == 0) P.zero.push_back((uint32_t)g);
+  }
+  P.n_chains = n_chains;
+  P.n_sub = (int64_t)sub.size();
+  P.lc = lc;
+  P.n_direct = n_direct;
+  return SEM_OK;
+}
+
+// ---------------------------------------------------------------------------
+template <int N>
+int launch_hex_apply(sem_ctx* c, int mode, const double* u, double* y, hipStream_t st) {
+  HexState* H = c->hex;
+  const semh::HexLaunch L{H->d_wg_off, H->d_wg_len,  H->d_elist, H->d_cmask,
+                          H->d_cflag,  H->d_slot, H->face_base};
+  const dim3 g((unsigned)H->n_wg), b(semh::hex_threads(N));
+  if (mode == semh::HEX_SET)
+    hipLaunchKernelGGL((semh::k_hex_poisson<N, semh::HEX_SET>), g, b, 0, st, u, y, H->d_map,
+                       H->d_G, c->d_D, L);
+  else if (mode == semh::HEX_ACC)
+    hipLaunchKernelGGL((semh::k_hex_poisson<N, semh::HEX_ACC>), g, b, 0, st, u, y, H->d_map,
+                       H->d_G, c->d_D, L);
+  else
+    hipLaunchKernelGGL((semh::k_hex_poisson<N, semh::HEX_DIAG>), g, b, 0, st, u, y, H->d_map,
+                       H->d_G, c->d_D, L);
+  HIP_TRY(hipGetLastError());
+  if (H->n_seam) {
+    const dim3 gs(grid_for(H->n_seam, 256, 8192)), bs(256);
+    if (mode == semh::HEX_ACC)
+      hipLaunchKernelGGL(semh::k_hex_seam_sum<true>, gs, bs, 0, st, y, H->d_seam_gid,
+                         H->d_seam_ptr, H->d_seam_idx, H->n_seam, H->d_slot);
+    else
+      hipLaunchKernelGGL(semh::k_hex_seam_sum<false>, gs, bs, 0, st, y, H->d_seam_gid,
+                         H->d_seam_ptr, H->d_seam_idx, H->n_seam, H->d_slot);
+    HIP_TRY(hipGetLastError());
+  }
+  return SEM_OK;
+}
+
+template <int N>
+int launch_hex_geom(sem_ctx* c, const double* nodes, double* GP, double* xph, double* J,
+                    double* iJ, double* dJ, double* dJW, hipStream_t st) {
+  HexState* H = c->hex;
+  constexpr int S = semh::hex_slots(N);
+  const int64_t nb = std::min<int64_t>((c->n_elem + S - 1) / S, 16384);
+  hipLaunchKernelGGL(semh::k_hex_geom<N>, dim3((unsigned)nb), dim3(semh::hex_threads(N)), 0, st,
+                     nodes, c->n_node, H->d_map, c->n_elem, c->d_Vinv, c->d_D, c->d_w, GP, xph, J,
+                     iJ, dJ, dJW, c->d_bad);
+  HIP_TRY(hipGetLastError());
+  return SEM_OK;
+}
+
+#define HEX_DISPATCH(rc, n, FN, ...)            \
+  switch (n) {                                  \
+    case 2: rc = FN<2>(__VA_ARGS__); break;     \
+    case 3: rc = FN<3>(__VA_ARGS__); break;     \
+    case 4: rc = FN<4>(__VA_ARGS__); break;     \
+    case 5: rc = FN<5>(__VA_ARGS__); break;     \
+    case 6: rc = FN<6>(__VA_ARGS__); break;     \
+    case 7: rc = FN<7>(__VA_ARGS__); break;     \
+    case 8: rc = FN<8>(__VA_ARGS__); break;     \
+    case 9: rc = FN<9>(__VA_ARGS__); break;     \
+    case 10: rc = FN<10>(__VA_ARGS__); break;   \
+    case 11: rc = FN<11>(__VA_ARGS__); break;   \
+    case 12: rc = FN<12>(__VA_ARGS__); break;   \
+    default: rc = fail(SEM_E_NOTIMPL, "hexahedral order out of range"); break; \
+  }
+static_assert(semh::HEX_MAX_N == 12, "HEX_DISPATCH lists n = 2..12");
+
+int need_map(const sem_ctx* c) {
+  if (!c->have_basis) return fail(SEM_E_STATE, "sem_set_basis must precede this call");
+  if (!c->hex->d_map) return fail(SEM_E_STATE, "sem_set_map must precede this call");
+  return SEM_OK;
+}
+
+}  // namespace
+
+namespace semh {
+
+int ctx_init(sem_ctx* c) {
+  int rc = hex_check_order(c->n);
+  if (rc) return rc;
+  if (c->dpn != 1) return fail(SEM_E_NOTIMPL, "hexahedral operators: dofs_per_node == 1 only");
+  c->hex = new HexState();
+  c->hex->N = c->n;
+  c->hex->slots = hex_slots(c->n);
+  c->hex->threads = hex_threads(c->n);
+  c->hex->nbc = hex_nbc(c->n);
+  return SEM_OK;
+}
+
+void ctx_free(sem_ctx* c) {
+  if (!c->hex) return;
+  c->hex->free_plan();
+  (void)hipFree(c->hex->d_map);
+  (void)hipFree(c->hex->d_G);
+  delete c->hex;
+  c->hex = nullptr;
+}
+
+int set_map(sem_ctx* c, const uint32_t* d_e2n, hipStream_t st) {
+  HexState* H = c->hex;
+  const int N = c->n;
+  const int64_t N3 = (int64_t)N * N * N;
+  const size_t count = (size_t)c->n_elem * N3;
+  std::vector<uint32_t> h(count);
+  HIP_TRY(hipMemcpyAsync(h.data(), d_e2n, count * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (!c->n_cu) {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) ==
+            hipSuccess &&
+        ncu > 0)
+      c->n_cu = ncu;
+  }
+  const int64_t target = 8 * std::max(c->n_cu, 256);
+  HexPlanHost P;
+  int rc = hex_build_plan(h, c->n_elem, c->n_node, N, target, P);
+  if (rc) return rc;
+  c->epoch++;
+  c->map_epoch++;
+  H->free_plan();
+  (void)hipFree(H->d_map);
+  H->d_map = nullptr;
+  HIP_TRY(hipMalloc(&H->d_map, count * sizeof(uint32_t)));
+  HIP_TRY(hipMemcpy(H->d_map, h.data(), count * sizeof(uint32_t), hipMemcpyHostToDevice));
+  if ((rc = upload(&H->d_wg_off, P.wg_off)) || (rc = upload(&H->d_wg_len, P.wg_len)) ||
+      (rc = upload(&H->d_elist, P.elist)) || (rc = upload(&H->d_cmask, P.cmask)) ||
+      (rc = upload(&H->d_cflag, P.cflag)) || (rc = upload(&H->d_seam_gid, P.seam_gid)) ||
+      (rc = upload(&H->d_seam_ptr, P.seam_ptr)) || (rc = upload(&H->d_seam_idx, P.seam_idx)) ||
+      (rc = upload(&H->d_zero, P.zero)))
+    return rc;
+  H->n_wg = (int64_t)P.wg_off.size();
+  H->n_pos = (int64_t)P.elist.size();
+  H->face_base = P.face_base;
+  H->n_slot = P.n_slot;
+  H->n_seam = (int64_t)P.seam_gid.size();
+  H->n_seam_writes = (int64_t)P.seam_idx.size();
+  H->n_zero = (int64_t)P.zero.size();
+  H->n_chains = P.n_chains;
+  H->n_subchains = P.n_sub;
+  H->chain_len = P.lc;
+  H->n_direct = P.n_direct;
+  if (H->n_seam) HIP_TRY(hipMalloc(&H->d_slot, std::max<int64_t>(H->n_slot, 1) * sizeof(double)));
+  // geometry belonged to the previous map
+  (void)hipFree(H->d_G);
+  H->d_G = nullptr;
+  H->have_G = false;
+  c->d_e2n = d_e2n;
+  return SEM_OK;
+}
+
+static int ensure_G(sem_ctx* c) {
+  HexState* H = c->hex;
+  if (!H->d_G) {
+    const size_t bytes = (size_t)c->n_elem * 6 * c->n * c->n * c->n * sizeof(double);
+    HIP_TRY(hipMalloc(&H->d_G, bytes));
+  }
+  return SEM_OK;
+}
+
+int geom_from_nodes(sem_ctx* c, const double* d_nodes, int op_kind, int64_t* n_bad,
+                    hipStream_t st) {
+  if (op_kind != SEM_OP_POISSON)
+    return fail(SEM_E_NOTIMPL, "hexahedral operators: Poisson only");
+  int rc = need_map(c);
+  if (rc) return rc;
+  if ((rc = ensure_G(c))) return rc;
+  c->epoch++;
+  HIP_TRY(hipMemsetAsync(c->d_bad, 0, sizeof(unsigned long long), st));
+  HEX_DISPATCH(rc, c->n, launch_hex_geom, c, d_nodes, c->hex->d_G, nullptr, nullptr, nullptr,
+               nullptr, nullptr, st);
+  if (rc) return rc;
+  unsigned long long bad = 0;
+  HIP_TRY(hipMemcpyAsync(&bad, c->d_bad, sizeof(bad), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (n_bad) *n_bad = (int64_t)bad;
+  if (bad) {
+    c->hex->have_G = false;
+    return fail(SEM_E_DETJ, "detJ <= 0 at " + std::to_string(bad) + " quadrature nodes");
+  }
+  c->hex->have_G = true;
+  return SEM_OK;
+}
+
+int geom_fields(sem_ctx* c, const double* d_nodes, double* x_phys, double* J, double* invJ,
+                double* detJ, double* detJxW, hipStream_t st) {
+  int rc = need_map(c);
+  if (rc) return rc;
+  HIP_TRY(hipMemsetAsync(c->d_bad, 0, sizeof(unsigned long long), st));
+  HEX_DISPATCH(rc, c->n, launch_hex_geom, c, d_nodes, nullptr, x_phys, J, invJ, detJ, detJxW,
+               st);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(st));
+  return SEM_OK;
+}
+
+int set_geom(sem_ctx* c, const double* d_G, int op_kind, hipStream_t st) {
+  if (op_kind != SEM_OP_POISSON)
+    return fail(SEM_E_NOTIMPL, "hexahedral operators: Poisson only");
+  int rc = need_map(c);
+  if (rc) return rc;
+  if ((rc = ensure_G(c))) return rc;
+  c->epoch++;
+  const int64_t total = c->n_elem * 6 * c->n * c->n * c->n;
+  hipLaunchKernelGGL(k_hex_pack_geom, dim3(grid_for(total)), dim3(256), 0, st, d_G, c->n_elem,
+                     c->n, c->hex->d_G);
+  HIP_TRY(hipGetLastError());
+  c->hex->have_G = true;
+  return SEM_OK;
+}
+
+int apply(sem_ctx* c, int op_kind, const double* u, double* y, int flags, hipStream_t st) {
+  if (op_kind != SEM_OP_POISSON)
+    return fail(SEM_E_NOTIMPL, "hexahedral operators: Poisson only");
+  if (flags & ~(SEM_APPLY_ACCUMULATE | SEM_APPLY_SKIP_ZERO))
+    return fail(SEM_E_INVALID, "sem_apply flags not supported on hexahedra");
+  int rc = need_map(c);
+  if (rc) return rc;
+  HexState* H = c->hex;
+  if (!H->have_G) return fail(SEM_E_STATE, "geometry for this operator has not been computed");
+  const bool acc = flags & SEM_APPLY_ACCUMULATE;
+  if (!acc && !(flags & SEM_APPLY_SKIP_ZERO) && H->n_zero)
+    if ((rc = zero_shared(c, y, st))) return rc;
+  HEX_DISPATCH(rc, c->n, launch_hex_apply, c, acc ? HEX_ACC : HEX_SET, u, y, st);
+  return rc;
+}
+
+int diag(sem_ctx* c, int op_kind, double* d, hipStream_t st) {
+  if (op_kind != SEM_OP_POISSON) return fail(SEM_E_NOTIMPL, "sem_diag: Poisson only");
+  int rc = need_map(c);
+  if (rc) return rc;
+  if (!c->hex->have_G) return fail(SEM_E_STATE, "geometry/map not set");
+  if (c->hex->n_zero && (rc = zero_shared(c, d, st))) return rc;
+  HEX_DISPATCH(rc, c->n, launch_hex_apply, c, HEX_DIAG, nullptr, d, st);
+  return rc;
+}
+
+int zero_shared(sem_ctx* c, double* y, hipStream_t st) {
+  HexState* H = c->hex;
+  if (!H->d_map) return fail(SEM_E_STATE, "map must be set");
+  if (H->n_zero) {
+    hipLaunchKernelGGL(semh::k_hex_zero, dim3(grid_for(H->n_zero, 256, 4096)), dim3(256), 0, st, y,
+                       H->d_zero, H->n_zero);
+    HIP_TRY(hipGetLastError());
+  }
+  return SEM_OK;
+}
+
+int plan_info(const sem_ctx* c, int64_t* info, int n_info) {
+  const HexState* H = c->hex;
+  // [0] workgroups, [1] zero list, [2] atomic groups (0), [3] conforming (1),
+  // [4] element slots per workgroup, [5] chains (maximal), [6] sub-chain
+  // length cap, [7] launch positions, [8] sub-chains, [9] seam nodes,
+  // [10] slotted writes, [11] plain stores, [12] threads per workgroup,
+  // [13] ndim (3), [14] geometry ready
+  const int64_t v[] = {H->n_wg,        H->n_zero, 0,
+                       1,              H->slots,  H->n_chains,
+                       H->chain_len,   H->n_pos,  H->n_subchains,
+                       H->n_seam,      H->n_seam_writes, H->n_direct,
+                       H->threads,     3,         H->have_G ? 1 : 0};
+  const int nv = (int)(sizeof(v) / sizeof(v[0]));
+  for (int i = 0; i < n_info; ++i) info[i] = i < nv ? v[i] : 0;
+  return SEM_OK;
+}
+
+int zero_list(const sem_ctx* c, std::vector<uint32_t>* nodes, bool* only_unreferenced) {
+  const HexState* H = c->hex;
+  nodes->assign((size_t)H->n_zero, 0u);
+  *only_unreferenced = true;
+  if (H->n_zero)
+    HIP_TRY(hipMemcpy(nodes->data(), H->d_zero, H->n_zero * sizeof(uint32_t),
+                      hipMemcpyDeviceToHost));
+  return SEM_OK;
+}
+
+int assemble(sem_ctx* c, const double* vals, double* out, int accumulate, hipStream_t st) {
+  HexState* H = c->hex;
+  if (!H->d_map) return fail(SEM_E_STATE, "sem_set_map must precede sem_assemble");
+  if (!accumulate) HIP_TRY(hipMemsetAsync(out, 0, c->n_node * sizeof(double), st));
+  const int64_t total = c->n_elem * c->n * c->n * c->n;
+  hipLaunchKernelGGL(semh::k_hex_assemble, dim3(grid_for(total)), dim3(256), 0, st, H->d_map, vals,
+                     total, out);
+  HIP_TRY(hipGetLastError());
+  return SEM_OK;
+}
+
+}  // namespace semh

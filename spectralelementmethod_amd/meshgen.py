@@ -14,6 +14,19 @@ tests/test_discrete.py:19-33 (nodes via np.mgrid, x-major global ids):
 
 Both return ``nodes`` float64 [2, n_nodes] and ``e2n`` uint32 [E, n, n]
 (lexicographic (xi0, xi1), sem/discrete.py:1044).
+
+Hexahedra (``north_star``: "synthetic structured quad/hex meshes"):
+
+* ``structured_cube``: [-1,1]^3 with nex x ney x nez hexahedra of order p,
+  equispaced element nodes, optional warp x,y,z += a sin(pi x) sin(pi y)
+  sin(pi z);
+* ``extrude``: a quad mesh swept along z in nez uniform layers (the mesh of
+  the extrusion identity the hexahedral parity tests use).
+
+They return ``nodes`` float64 [3, n_nodes] and ``e2n`` uint32 [E, n, n, n]
+(lexicographic (xi0, xi1, xi2), xi2 fastest, as the reference's N-D
+``TensorProduct`` lays out an [n, n, n] coefficient block,
+sem/basis_functions.py:408-448, 626-650).
 """
 import numpy as np
 
@@ -46,6 +59,58 @@ def structured_square(nex, ney, p, warp=0.0, x0=-1.0, x1=1.0, y0=-1.0, y1=1.0):
         Y = Y + s
     nodes = np.stack([X.ravel(), Y.ravel()])
     return nodes, _element_map(nex, ney, p, Ny)
+
+
+def _element_map3(n_a, n_b, n_c, p, Nb, Nc):
+    """e2n[(ea*n_b + eb)*n_c + ec, i, j, k] = ((ea*p + i)*Nb + eb*p + j)*Nc + ec*p + k."""
+    n = p + 1
+    ea = np.arange(n_a, dtype=np.int64)[:, None, None, None, None, None]
+    eb = np.arange(n_b, dtype=np.int64)[None, :, None, None, None, None]
+    ec = np.arange(n_c, dtype=np.int64)[None, None, :, None, None, None]
+    i = np.arange(n, dtype=np.int64)[None, None, None, :, None, None]
+    j = np.arange(n, dtype=np.int64)[None, None, None, None, :, None]
+    k = np.arange(n, dtype=np.int64)[None, None, None, None, None, :]
+    ids = ((ea * p + i) * Nb + eb * p + j) * Nc + ec * p + k
+    return ids.reshape(n_a * n_b * n_c, n, n, n).astype(np.uint32)
+
+
+def structured_cube(nex, ney, nez, p, warp=0.0, lo=-1.0, hi=1.0):
+    """Structured hexahedral mesh of [lo, hi]^3.  Node (ix, iy, iz) -> id
+    (ix*Ny + iy)*Nz + iz; element (ex, ey, ez) -> id (ex*ney + ey)*nez + ez;
+    local node (a, b, c) of element (ex, ey, ez) is node
+    (ex*p + a, ey*p + b, ez*p + c)."""
+    Nx, Ny, Nz = nex * p + 1, ney * p + 1, nez * p + 1
+    if Nx * Ny * Nz >= 2 ** 32:
+        raise ValueError("mesh too large for a uint32 element map")
+    X, Y, Z = np.meshgrid(np.linspace(lo, hi, Nx), np.linspace(lo, hi, Ny),
+                          np.linspace(lo, hi, Nz), indexing="ij")
+    if warp:
+        s = warp * np.sin(np.pi * X) * np.sin(np.pi * Y) * np.sin(np.pi * Z)
+        X = X + s
+        Y = Y + 0.5 * s
+        Z = Z - s
+    nodes = np.stack([X.ravel(), Y.ravel(), Z.ravel()])
+    return nodes, _element_map3(nex, ney, nez, p, Ny, Nz)
+
+
+def extrude(nodes2, e2n2, nez, p, z0=0.0, z1=1.0):
+    """Sweep a quad mesh (nodes2 [2, N2], e2n2 [E2, n, n]) along z in nez
+    uniform layers of order-p elements over [z0, z1].  Node (i2, kz) -> id
+    i2*Nz + kz (Nz = nez*p + 1); element (e2, ez) -> id e2*nez + ez, local
+    node (a, b, c) = (2-D local node (a, b), layer node ez*p + c)."""
+    nodes2 = np.asarray(nodes2, dtype=np.float64)
+    e2n2 = np.asarray(e2n2).astype(np.int64)
+    E2, n = e2n2.shape[0], e2n2.shape[1]
+    Nz = nez * p + 1
+    z = np.linspace(z0, z1, Nz)
+    N2 = nodes2.shape[1]
+    nodes = np.stack([np.repeat(nodes2[0], Nz), np.repeat(nodes2[1], Nz), np.tile(z, N2)])
+    ez = np.arange(nez, dtype=np.int64)[None, :, None, None, None]
+    c = np.arange(n, dtype=np.int64)[None, None, None, None, :]
+    ids = e2n2[:, None, :, :, None] * Nz + ez * p + c
+    if N2 * Nz >= 2 ** 32:
+        raise ValueError("mesh too large for a uint32 element map")
+    return nodes, ids.reshape(E2 * nez, n, n, n).astype(np.uint32)
 
 
 def structured_strip(nex, ney, p, ex0, ex1, warp=0.0):

@@ -57,13 +57,15 @@ def _device_index(device):
     return device.index if device.index is not None else torch.cuda.current_device()
 
 
-def _basis_arrays(p, basis):
+def _basis_arrays(p, basis, ndim=2):
     if basis is None:
         b1 = LagrangeGaussLobatto(p)
-        basis = TensorProductQS(b1, b1)
-    D = np.ascontiguousarray(basis.get_D1_matrices()[0], dtype=np.float64)
-    D1 = basis.get_D1_matrices()[1]
-    if not np.array_equal(D, D1):
+        basis = TensorProductQS(*([b1] * ndim))
+    mats = basis.get_D1_matrices()
+    if len(mats) != ndim:
+        raise ValueError("basis spans %d dimensions, the mesh %d" % (len(mats), ndim))
+    D = np.ascontiguousarray(mats[0], dtype=np.float64)
+    if not all(np.array_equal(D, Dk) for Dk in mats[1:]):
         raise NotImplementedError("anisotropic tensor bases are not supported by the kernels")
     w = np.ascontiguousarray(basis.quad_rule.weights[0], dtype=np.float64)
     sub = basis._subbases[0]
@@ -77,10 +79,12 @@ class SEMOperator(object):
     Parameters
     ----------
     p : int
-        Polynomial order (1..16).
-    e2n : array-like uint32 [n_elem, p+1, p+1]
-        Element -> global node map (lexicographic, sem/discrete.py:1044).
-    nodes : array-like float64 [2, n_node]
+        Polynomial order (1..16 on quadrilaterals, 1..11 on hexahedra).
+    e2n : array-like uint32 [n_elem, p+1, p+1] or [n_elem, p+1, p+1, p+1]
+        Element -> global node map (lexicographic, sem/discrete.py:1044); a
+        4-D map makes a hexahedral operator (include/sem_hip.h
+        sem_ctx_create_nd: Poisson, stored geometry).
+    nodes : array-like float64 [ndim, n_node]
         Mesh node coordinates (equispaced within each element).
     dofs_per_node : int
         1 for the Poisson operator, 2 (interleaved psi, omega) for the
@@ -125,13 +129,19 @@ class SEMOperator(object):
         self.dpn = int(dofs_per_node)
         dev = _device_index(device)
         self.device = torch.device("cuda", dev)
-        self.basis, self.D, self.w, self.Vinv = _basis_arrays(self.p, basis)
         e2n_t = self._to_map(e2n)
-        if e2n_t.dim() != 3 or tuple(e2n_t.shape[1:]) != (self.n, self.n):
-            raise ValueError("e2n must have shape [E, %d, %d]" % (self.n, self.n))
+        self.ndim = e2n_t.dim() - 1
+        if self.ndim not in (2, 3) or tuple(e2n_t.shape[1:]) != (self.n,) * self.ndim:
+            raise ValueError("e2n must have shape [E, %d, %d] or [E, %d, %d, %d]"
+                             % ((self.n,) * 5))
+        if self.ndim == 3 and (self.dpn != 1 or node_state is not None or
+                               geometry == "nodal" or kernel == "mfma"):
+            raise NotImplementedError("hexahedral operators: Poisson (dofs_per_node = 1), "
+                                      "stored geometry, column kernel, no node states")
+        self.basis, self.D, self.w, self.Vinv = _basis_arrays(self.p, basis, self.ndim)
         nodes_t = torch.as_tensor(nodes, dtype=torch.float64)
-        if nodes_t.dim() != 2 or nodes_t.shape[0] != 2:
-            raise ValueError("nodes must have shape [2, n_node]")
+        if nodes_t.dim() != 2 or nodes_t.shape[0] != self.ndim:
+            raise ValueError("nodes must have shape [%d, n_node]" % self.ndim)
         self.n_elem = int(e2n_t.shape[0])
         self.n_node = int(nodes_t.shape[1])
         self.ndof = self.dpn * self.n_node
@@ -139,8 +149,8 @@ class SEMOperator(object):
             self.e2n = e2n_t.to(self.device).contiguous()
             self.nodes = nodes_t.to(self.device).contiguous()
             ctx = C.c_void_p()
-            _lib.check(self._lib.sem_ctx_create(C.byref(ctx), self.p, self.n_elem, self.n_node,
-                                                self.dpn, dev))
+            _lib.check(self._lib.sem_ctx_create_nd(C.byref(ctx), self.ndim, self.p, self.n_elem,
+                                                   self.n_node, self.dpn, dev))
             self._ctx = ctx
             _lib.check(self._lib.sem_set_geom_mode(ctx, self.GEOMETRY_MODES[geometry]))
             if kernel != "auto":
@@ -192,6 +202,12 @@ class SEMOperator(object):
         info = (C.c_int64 * 26)()
         _lib.check(self._lib.sem_plan_info(self._ctx, info, 26))
         v = list(info)
+        if self.ndim == 3:
+            return dict(ndim=3, workgroups=v[0], zero_list=v[1], conforming=bool(v[3]),
+                        slots_per_workgroup=v[4], chains=v[5], chain_length_cap=v[6],
+                        positions=v[7], subchains=v[8], seam_nodes=v[9], slotted_writes=v[10],
+                        plain_stores=v[11], threads=v[12], geometry="stored",
+                        kernel="column", plan="chains-seams")
         counts = [x for x in v[8:8 + v[5]]]
         while counts and counts[-1] == 0:
             counts.pop()
@@ -223,13 +239,14 @@ class SEMOperator(object):
         return self
 
     def set_geometry(self, G, kind=POISSON, stream=None):
-        """Install user factors [E, ncomp, n, n] (device or host)."""
+        """Install user factors [E, ncomp, n, n] (hexahedra: [E, 6, n, n, n],
+        components 00, 01, 02, 11, 12, 22) (device or host)."""
         kind = op_kind(kind)
-        ncomp = self._lib.sem_op_ncomp(kind)
+        ncomp = self._lib.sem_op_ncomp(kind) if self.ndim == 2 else 6
         G = torch.as_tensor(G, dtype=torch.float64).to(self.device).contiguous()
-        if tuple(G.shape) != (self.n_elem, ncomp, self.n, self.n):
-            raise ValueError("G must have shape [%d, %d, %d, %d]" % (self.n_elem, ncomp, self.n,
-                                                                     self.n))
+        shape = (self.n_elem, ncomp) + (self.n,) * self.ndim
+        if tuple(G.shape) != shape:
+            raise ValueError("G must have shape %s" % (list(shape),))
         with torch.cuda.device(self.device):
             _lib.check(self._lib.sem_set_geom(self._ctx, _lib.tptr(G), kind, self._stream(stream)))
             torch.cuda.current_stream().synchronize()
@@ -240,11 +257,12 @@ class SEMOperator(object):
         """Reference-layout x_phys [E,2,n,n], J/invJ [E,2,2,n,n],
         detJ/detJxW [E,n,n] as device tensors (FiniteElement properties,
         sem/discrete.py:582-597)."""
-        E, n = self.n_elem, self.n
+        E, d = self.n_elem, self.ndim
+        loc = (self.n,) * d
         kw = dict(dtype=torch.float64, device=self.device)
-        out = dict(x_phys=torch.empty(E, 2, n, n, **kw), J=torch.empty(E, 2, 2, n, n, **kw),
-                   invJ=torch.empty(E, 2, 2, n, n, **kw), detJ=torch.empty(E, n, n, **kw),
-                   detJxW=torch.empty(E, n, n, **kw))
+        out = dict(x_phys=torch.empty(E, d, *loc, **kw), J=torch.empty(E, d, d, *loc, **kw),
+                   invJ=torch.empty(E, d, d, *loc, **kw), detJ=torch.empty(E, *loc, **kw),
+                   detJxW=torch.empty(E, *loc, **kw))
         with torch.cuda.device(self.device):
             _lib.check(self._lib.sem_geom_fields(
                 self._ctx, _lib.tptr(self.nodes), _lib.dptr(self.Vinv), _lib.tptr(out["x_phys"]),
@@ -323,9 +341,9 @@ class SEMOperator(object):
         if self.dpn != 1:
             raise NotImplementedError("assemble: dofs_per_node == 1")
         v = torch.as_tensor(elem_vals, dtype=torch.float64).to(self.device).contiguous()
-        if tuple(v.shape) != (self.n_elem, self.n, self.n):
-            raise ValueError("element values must have shape [%d, %d, %d]" % (self.n_elem, self.n,
-                                                                               self.n))
+        shape = (self.n_elem,) + (self.n,) * self.ndim
+        if tuple(v.shape) != shape:
+            raise ValueError("element values must have shape %s" % (list(shape),))
         if out is None:
             out = torch.empty(self.ndof, dtype=torch.float64, device=self.device)
             accumulate = False

@@ -55,3 +55,8 @@ def rel_l2(a, b):
 @pytest.fixture(scope="session")
 def axisym_ns():
     return load_golden("axisym_ns.npz")
+
+
+@pytest.fixture(scope="session")
+def hex_golden():
+    return load_golden("hex.npz")

@@ -555,9 +555,89 @@ def gen_msh():
     print("msh_reference.npz")
 
 
+def ref_basis3(p):
+    import sem.basis_functions as bf
+    b1 = bf.LagrangeGaussLobatto(p)
+    return b1, bf.TensorProductQS(b1, b1, b1)
+
+
+def hex_Lse(invJ, JxW, D):
+    """3-D element Laplacian [n^3, n^3] (RESTATED: examples/poisson.py:166-193
+    with gradh = invJ . D per direction, written with Kronecker factors; the
+    reference has no 3-D example)."""
+    n = D.shape[0]
+    I = np.eye(n)
+    dphi = [np.kron(np.kron(D, I), I), np.kron(np.kron(I, D), I), np.kron(np.kron(I, I), D)]
+    W = JxW.ravel()
+    L = np.zeros((n ** 3, n ** 3))
+    for x in range(3):
+        g = sum(invJ[d, x].ravel()[:, None] * dphi[d] for d in range(3))
+        L += g.T @ (W[:, None] * g)
+    return L
+
+
+def gen_hex():
+    """Hexahedral goldens from the reference's N-dimensional basis layer:
+    TensorProductQS(b, b, b).gradient / compute_coeffs_grid_eq
+    (sem/basis_functions.py:599-650) and quad_rule.xweight
+    (sem/quadratures.py:268-275) on random data, and Poisson actions on small
+    warped hexahedral meshes whose per-element ingredients come from the same
+    reference calls: x_phys = compute_coeffs_grid_eq(element nodes)
+    (Mapping._compute_x_phys, sem/mapping.py:98-103), J = gradient(x_phys)
+    .swapaxes(0, 1) (sem/mapping.py:113-114), detJxW = xweight(detJ)
+    (sem/discrete.py:594-597).  The 3x3 det / inverse (numpy.linalg) and the
+    element Laplacian (hex_Lse) are restatements: the reference stops at 2-D
+    there (sem/mapping.py:110-111)."""
+    sys.path.insert(1, os.path.dirname(os.path.dirname(OUT)))
+    from spectralelementmethod_amd import meshgen
+    rng = np.random.default_rng(11)
+    out = {}
+    for p in (2, 4, 8):
+        _, tb = ref_basis3(p)
+        c = rng.standard_normal((3, p + 1, p + 1, p + 1))
+        out["c_%d" % p] = c
+        out["grad_%d" % p] = tb.gradient(c)
+        out["coeffs_eq_%d" % p] = tb.compute_coeffs_grid_eq(c)
+        out["xweight_%d" % p] = tb.quad_rule.xweight(c)
+    cases = [("p2_3x2x2w", 2, (3, 2, 2)), ("p3_2x2x2w", 3, (2, 2, 2)),
+             ("p4_2x2x1w", 4, (2, 2, 1)), ("p5_1x2x1w", 5, (1, 2, 1))]
+    for name, p, (nx, ny, nz) in cases:
+        nodes, e2n = meshgen.structured_cube(nx, ny, nz, p, warp=0.05)
+        _, tb = ref_basis3(p)
+        D = tb.get_D1_matrices()[0]
+        ndof = nodes.shape[1]
+        u = rng.standard_normal(ndof)
+        y = np.zeros(ndof)
+        fields = {k: [] for k in ("x_phys", "J", "invJ", "detJ", "detJxW")}
+        for e in range(e2n.shape[0]):
+            X = nodes[:, e2n[e]]
+            xp = tb.compute_coeffs_grid_eq(X)
+            J = tb.gradient(xp).swapaxes(0, 1)
+            Jm = np.moveaxis(J, (0, 1), (-2, -1))
+            detJ = np.linalg.det(Jm)
+            invJ = np.moveaxis(np.linalg.inv(Jm), (-2, -1), (0, 1))
+            JxW = tb.quad_rule.xweight(detJ)
+            L = hex_Lse(invJ, JxW, D)
+            np.add.at(y, e2n[e].ravel(), L @ u[e2n[e]].ravel())
+            for k, v in (("x_phys", xp), ("J", J), ("invJ", invJ), ("detJ", detJ),
+                         ("detJxW", JxW)):
+                fields[k].append(v)
+        out[name + "_nodes"] = nodes
+        out[name + "_e2n"] = e2n
+        out[name + "_u"] = u
+        out[name + "_y"] = y
+        out[name + "_p"] = np.array(p)
+        for k, v in fields.items():
+            out[name + "_geom_" + k] = np.stack(v)
+        print("  hex action %s ndof=%d |y|=%.6e" % (name, ndof, np.linalg.norm(y)))
+    np.savez_compressed(os.path.join(OUT, "hex.npz"), **out)
+    print("hex.npz")
+
+
 GENERATORS = {"gll": gen_gll, "tensor_ops": gen_tensor_ops, "poisson_action": gen_poisson_action,
               "poisson_solution": gen_poisson_solution, "axisym": gen_axisym,
-              "geometry": gen_geometry, "msh": gen_msh, "axisym_ns": gen_axisym_ns}
+              "geometry": gen_geometry, "msh": gen_msh, "axisym_ns": gen_axisym_ns,
+              "hex": gen_hex}
 
 
 def main(names=None):

@@ -1,0 +1,231 @@
+"""GPU parity of the hexahedral (3-D) Poisson path: libsem_hip.so through the
+C ABI (sem_ctx_create_nd, ndim = 3) against
+
+* the goldens built from the reference's own N-D basis calls
+  (tests/golden/hex.npz: TensorProductQS(b, b, b).compute_coeffs_grid_eq /
+  gradient / quad_rule.xweight, sem/basis_functions.py:599-650,
+  sem/quadratures.py:268-275), p = 2..5, warped hexahedra;
+* the extrusion identity K3 (u (x) 1) = (K2 u) (x) (M_z 1) on the reference's
+  2-D golden meshes swept along z: the 3-D action pinned to the reference's
+  own 2-D action output;
+* the NumPy oracle (oracle/sem_oracle.py, HexPoissonProblem, itself pinned to
+  the two above) at every built order p = 1..11, on broken-chain numberings
+  and at ~1e7 DOF (p = 8, 27^3 hexahedra) at the north-star 1e-10.
+
+The 3x3 determinant / inverse and the 3-D element operator have no reference
+counterpart (sem/mapping.py:110-111 stops at 2-D): beyond the extrusion
+identity they are "parity unpinned" restatements."""
+import numpy as np
+import pytest
+
+from conftest import rel_l2
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-12        # small meshes, vs reference goldens / oracle
+TOL_FULL = 1e-10   # BASELINE.json north_star at ~1e7 DOF
+HEX_CASES = ["p2_3x2x2w", "p3_2x2x2w", "p4_2x2x1w", "p5_1x2x1w"]
+
+
+@pytest.fixture(scope="module")
+def sem():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from spectralelementmethod_amd import operators
+    return operators
+
+
+def _oracle(gll, nodes, e2n, p):
+    import sem_oracle
+    return sem_oracle.HexPoissonProblem(nodes, e2n, gll["half_%d" % p])
+
+
+@pytest.mark.parametrize("name", HEX_CASES)
+def test_hex_action_golden(sem, hex_golden, name):
+    p = int(hex_golden[name + "_p"])
+    op = sem.SEMOperator(p, hex_golden[name + "_e2n"], hex_golden[name + "_nodes"])
+    assert op.ndim == 3
+    y = op.apply(torch.from_numpy(hex_golden[name + "_u"]).cuda()).cpu().numpy()
+    assert rel_l2(y, hex_golden[name + "_y"]) < TOL
+
+
+@pytest.mark.parametrize("name", HEX_CASES)
+def test_hex_geometry_fields_golden(sem, hex_golden, name):
+    p = int(hex_golden[name + "_p"])
+    op = sem.SEMOperator(p, hex_golden[name + "_e2n"], hex_golden[name + "_nodes"])
+    f = op.geometry_fields()
+    for k in ("x_phys", "J", "invJ", "detJ", "detJxW"):
+        assert rel_l2(f[k].cpu().numpy(), hex_golden[name + "_geom_" + k]) < TOL, k
+
+
+@pytest.mark.parametrize("name,nez", [("p8_8x8w", 3), ("p4_4x4", 5), ("p6_3x4w", 2),
+                                      ("p2_6x5", 4)])
+def test_hex_extrusion_identity(sem, gll, poisson_action, name, nez):
+    """3-D action of u2 (x) 1 on the extruded reference mesh = the
+    reference's 2-D golden action times the assembled z mass."""
+    import sem_oracle
+    from spectralelementmethod_amd import meshgen
+    p = int(poisson_action[name + "_p"])
+    z0, z1 = -0.5, 0.25
+    nodes3, e2n3 = meshgen.extrude(poisson_action[name + "_nodes"], poisson_action[name + "_e2n"],
+                                   nez, p, z0, z1)
+    op = sem.SEMOperator(p, e2n3, nodes3)
+    Nz = nez * p + 1
+    u = torch.from_numpy(np.repeat(poisson_action[name + "_u"], Nz)).cuda()
+    y = op.apply(u).cpu().numpy()
+    _, _, quad = sem_oracle.gll_unfold(gll["half_%d" % p])
+    mz = np.zeros(Nz)
+    for ez in range(nez):
+        mz[ez * p:ez * p + p + 1] += 0.5 * (z1 - z0) / nez * quad
+    assert rel_l2(y, np.outer(poisson_action[name + "_y"], mz).ravel()) < TOL
+
+
+@pytest.mark.parametrize("p", range(1, 12))
+def test_hex_orders_vs_oracle(sem, gll, p):
+    from spectralelementmethod_amd import meshgen
+    ne = {1: 6, 2: 5, 3: 4, 4: 3, 5: 3}.get(p, 2)
+    nodes, e2n = meshgen.structured_cube(ne + 1, ne, ne - 1 if ne > 2 else 2, p, warp=0.05)
+    P = _oracle(gll, nodes, e2n, p)
+    op = sem.SEMOperator(p, e2n, nodes)
+    u = np.random.default_rng(p).standard_normal(P.ndof)
+    y = op.apply(torch.from_numpy(u).cuda()).cpu().numpy()
+    assert rel_l2(y, P.apply(u)) < TOL
+    info = op.plan_info()
+    assert info["ndim"] == 3 and info["chains"] == ne * (ne - 1 if ne > 2 else 2)
+
+
+def _permute_local(e2n, rng, frac=0.5):
+    """Re-orient a fraction of the elements (swap / reverse local axes): the
+    mesh is the same, the xi0 chains break wherever orientations differ."""
+    e2n = e2n.copy()
+    for e in np.flatnonzero(rng.random(e2n.shape[0]) < frac):
+        perm = rng.permutation(3)
+        flips = rng.random(3) < 0.5
+        # orientation-preserving only (a reflection would make detJ < 0)
+        sign = np.linalg.det(np.eye(3)[perm]) * (-1) ** int(flips.sum())
+        if sign < 0:
+            flips[0] = not flips[0]
+        t = np.transpose(e2n[e], perm)
+        for ax in range(3):
+            if flips[ax]:
+                t = np.flip(t, axis=ax)
+        e2n[e] = t
+    return e2n
+
+
+@pytest.mark.parametrize("case", ["shuffle_elements", "shuffle_nodes", "reoriented",
+                                  "reoriented_shuffled"])
+def test_hex_broken_chains_vs_oracle(sem, gll, case):
+    """The planner on numberings that defeat the chains: still exact."""
+    from spectralelementmethod_amd import meshgen
+    p = 4
+    nodes, e2n = meshgen.structured_cube(4, 3, 3, p, warp=0.05)
+    rng = np.random.default_rng(5)
+    if case in ("shuffle_elements", "reoriented_shuffled"):
+        e2n = meshgen.shuffle_elements(e2n, seed=3)
+    if case == "shuffle_nodes":
+        nodes, e2n = meshgen.shuffle_nodes(nodes, e2n, seed=4)
+    if case.startswith("reoriented"):
+        e2n = _permute_local(e2n, rng)
+    P = _oracle(gll, nodes, e2n, p)
+    op = sem.SEMOperator(p, e2n, nodes)
+    u = rng.standard_normal(P.ndof)
+    y = op.apply(torch.from_numpy(u).cuda()).cpu().numpy()
+    assert rel_l2(y, P.apply(u)) < TOL
+
+
+def test_hex_accumulate_diag_assemble_and_set_geometry(sem, gll):
+    from spectralelementmethod_amd import meshgen
+    p = 5
+    nodes, e2n = meshgen.structured_cube(3, 2, 2, p, warp=0.05)
+    P = _oracle(gll, nodes, e2n, p)
+    op = sem.SEMOperator(p, e2n, nodes)
+    rng = np.random.default_rng(9)
+    u = torch.from_numpy(rng.standard_normal(P.ndof)).cuda()
+    y0 = torch.from_numpy(rng.standard_normal(P.ndof)).cuda()
+    y = y0.clone()
+    op.apply(u, out=y, accumulate=True)
+    ref = y0.cpu().numpy() + P.apply(u.cpu().numpy())
+    assert rel_l2(y.cpu().numpy(), ref) < TOL
+    # diagonal of the assembled operator
+    L = P.element_matrices()
+    dref = np.bincount(P.e2n.reshape(P.e2n.shape[0], -1).ravel(),
+                       weights=np.einsum("eii->ei", L).ravel(), minlength=P.ndof)
+    assert rel_l2(op.diag().cpu().numpy(), dref) < TOL
+    # load vector of f = 1 (sem_assemble of detJxW)
+    f = op.geometry_fields()["detJxW"]
+    F = op.assemble(f).cpu().numpy()
+    Fref = np.bincount(P.e2n.ravel(), weights=P.detJxW.ravel(), minlength=P.ndof)
+    assert rel_l2(F, Fref) < TOL
+    # caller-installed factors give the same action
+    op2 = sem.SEMOperator(p, e2n, nodes)
+    op2.set_geometry(P.G)
+    assert rel_l2(op2.apply(u).cpu().numpy(), ref - y0.cpu().numpy()) < TOL
+
+
+def test_hex_apply_is_deterministic(sem):
+    from spectralelementmethod_amd import meshgen
+    p = 6
+    nodes, e2n = meshgen.structured_cube(5, 4, 3, p, warp=0.05)
+    op = sem.SEMOperator(p, e2n, nodes)
+    u = torch.from_numpy(np.random.default_rng(1).standard_normal(nodes.shape[1])).cuda()
+    y1 = op.apply(u).clone()
+    for _ in range(3):
+        assert torch.equal(op.apply(u), y1)
+
+
+def test_hex_detj_nonpositive_raises(sem):
+    from spectralelementmethod_amd import meshgen
+    p = 3
+    nodes, e2n = meshgen.structured_cube(2, 2, 2, p)
+    e2n = e2n.copy()
+    e2n[1] = e2n[1][::-1]  # mirrored element: detJ < 0
+    op = sem.SEMOperator(p, e2n, nodes)
+    with pytest.raises(AssertionError):
+        op.compute_geometry()
+
+
+def test_hex_pcg_vs_direct_solve(sem, gll):
+    """Assembled 3-D Poisson solve on the device (Jacobi-PCG, sem_pcg_solve)
+    against a direct sparse solve of the oracle's assembled K (u = 0.2 (x +
+    y + z + 3) on the x = -1 and y = -1 faces, f = 1)."""
+    import scipy.sparse as sps
+    import scipy.sparse.linalg as spsl
+    from spectralelementmethod_amd import meshgen
+    p = 4
+    nodes, e2n = meshgen.structured_cube(3, 3, 2, p, warp=0.05)
+    P = _oracle(gll, nodes, e2n, p)
+    L = P.element_matrices()
+    E, nl = L.shape[0], L.shape[1]
+    loc = P.e2n.reshape(E, nl)
+    K = sps.coo_matrix((L.ravel(), (np.repeat(loc, nl, axis=1).ravel(),
+                                    np.tile(loc, (1, nl)).ravel())),
+                       shape=(P.ndof, P.ndof)).tocsr()
+    F = np.bincount(P.e2n.ravel(), weights=P.detJxW.ravel(), minlength=P.ndof)
+    x, yv, zv = nodes
+    ebc = (np.abs(x + 1) < 1e-12) | (np.abs(yv + 1) < 1e-12)
+    g = np.where(ebc, 0.2 * (x + yv + zv + 3), 0.0)
+    free = ~ebc
+    ref = g.copy()
+    ref[free] = spsl.spsolve(K[free][:, free].tocsc(), F[free] - K[free][:, ebc] @ g[ebc])
+    op = sem.SEMOperator(p, e2n, nodes)
+    xd = torch.from_numpy(g.copy()).cuda()
+    xd, its, rel = op.pcg_solve(torch.from_numpy(F).cuda(), xd, ebc, rtol=1e-14,
+                                max_iter=5000)
+    assert rel_l2(xd.cpu().numpy(), ref) < 1e-10, (its, rel)
+
+
+def test_hex_full_size_p8(sem, gll):
+    """~1e7 DOF: p = 8, 27^3 warped hexahedra (10,218,313 DOF) vs the oracle
+    at the north-star 1e-10; the plan forms chains along xi0."""
+    from spectralelementmethod_amd import meshgen
+    p, ne = 8, 27
+    nodes, e2n = meshgen.structured_cube(ne, ne, ne, p, warp=0.05)
+    P = _oracle(gll, nodes, e2n, p)
+    op = sem.SEMOperator(p, e2n, nodes)
+    u = np.random.default_rng(27).standard_normal(P.ndof)
+    y = op.apply(torch.from_numpy(u).cuda()).cpu().numpy()
+    assert rel_l2(y, P.apply(u)) < TOL_FULL
+    info = op.plan_info()
+    assert info["chains"] == ne * ne and info["plain_stores"] > 0
