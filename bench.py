@@ -11,6 +11,7 @@ region.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--p 8] [--nex 1024] [--ney 1024]
                   [--scaling strong|weak] [--op poisson|axisym_stokes|axisym_ns|pcg]
+  python bench.py --dim 3 [--p 8] [--hex-ne 27]     (hexahedra, one GPU; bench_hex)
 
 --gpus N without a launcher: this process starts N rank processes (before
 touching the GPU) and waits for them; under torchrun (WORLD_SIZE set) each
@@ -193,6 +194,213 @@ def cpu_baseline(p, warp, budget_s=20.0, workers=16):
     out["faithful_mp"] = dict(ndof=ndof_mp, n_elem=nex_mp * nex_mp, workers=nw,
                               sec_per_action=t_mp, dof_per_s=ndof_mp / t_mp, reps=reps)
     return out
+
+
+def alg_bytes_hex(n_nodes, n_elem, p):
+    """The 3-D form of SURVEY.md §8(d): u read once and y written once (16
+    per DOF), 6 fp64 geometric factors + one uint32 map entry per element
+    node (52 B): B = 16*ndof + 52*E*(p+1)^3."""
+    return 16 * n_nodes + 52 * n_elem * (p + 1) ** 3
+
+
+def alg_flops_hex(n_elem, p):
+    """fp64 FLOP per hexahedral action: six sum-factorised contractions
+    (2 n^4 each) + 15 per node for the 3x3 factor product."""
+    n = p + 1
+    return n_elem * (12 * n ** 4 + 15 * n ** 3)
+
+
+def _faithful_hex_worker(args):
+    """One worker of the multi-process reference-faithful hexahedral action:
+    dense element Laplacians (the 3-D form of examples/poisson.py:168-193) of
+    its element slice, applied per element + np.add.at, timed after a barrier."""
+    p, ne, warp, w, nw, reps, barrier = args
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import sem_oracle
+    from spectralelementmethod_amd import meshgen
+    gll = np.load(os.path.join(ROOT, "tests", "golden", "gll.npz"))
+    nodes, e2n = meshgen.structured_cube(ne, ne, ne, p, warp=warp)
+    prob = sem_oracle.HexPoissonProblem(nodes, e2n, gll["half_%d" % p])
+    E = e2n.shape[0]
+    sl = np.arange(w * E // nw, (w + 1) * E // nw)
+    L = prob.element_matrices(sl)
+    loc = prob.e2n[sl].reshape(len(sl), -1)
+    u = np.random.default_rng(0).standard_normal(prob.ndof)
+
+    def run():
+        y = np.zeros(prob.ndof)
+        for k in range(len(sl)):
+            np.add.at(y, loc[k], L[k] @ u[loc[k]])
+        return y
+    run()
+    ts = []
+    for _ in range(reps):
+        barrier.wait()
+        t0 = time.perf_counter()
+        run()
+        ts.append(time.perf_counter() - t0)
+    return ts
+
+
+def cpu_baseline_hex(p, warp, budget_s=20.0, workers=16):
+    """The reference path on hexahedra on this host (oracle restatement,
+    OMP_NUM_THREADS = 1 per process): (1) per-element dense Laplacian applied
+    element by element + np.add.at, `workers` processes over an 8^3 mesh;
+    (2) batched sum-factorised NumPy on 12^3 (one process)."""
+    import multiprocessing as mp
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import sem_oracle
+    from spectralelementmethod_amd import meshgen
+    gll = np.load(os.path.join(ROOT, "tests", "golden", "gll.npz"))
+    out = {}
+    nodes, e2n = meshgen.structured_cube(12, 12, 12, p, warp=warp)
+    prob = sem_oracle.HexPoissonProblem(nodes, e2n, gll["half_%d" % p])
+    u = np.random.default_rng(0).standard_normal(prob.ndof)
+    prob.apply(u)
+    ts, t_start = [], time.perf_counter()
+    while len(ts) < 3 or (time.perf_counter() - t_start < budget_s / 2 and len(ts) < 10):
+        t0 = time.perf_counter()
+        prob.apply(u)
+        ts.append(time.perf_counter() - t0)
+    t3 = float(np.median(ts))
+    out["batched_sumfact"] = dict(ndof=prob.ndof, sec_per_action=t3, dof_per_s=prob.ndof / t3,
+                                  reps=len(ts))
+    del prob
+    nw = max(1, min(workers, os.cpu_count() or 1))
+    ne, reps = 8, 5
+    ctx = mp.get_context("fork")
+    barrier = ctx.Manager().Barrier(nw)
+    with ctx.Pool(nw) as pool:
+        res = pool.map(_faithful_hex_worker, [(p, ne, warp, w, nw, reps, barrier)
+                                              for w in range(nw)])
+    t_max = [max(r[k] for r in res) for k in range(reps)]
+    ndof = (ne * p + 1) ** 3
+    parts = [np.random.default_rng(w).standard_normal(ndof) for w in range(nw)]
+    t0 = time.perf_counter()
+    np.add.reduce(parts)
+    t_mp = float(np.median(t_max)) + time.perf_counter() - t0
+    out["faithful_mp"] = dict(ndof=ndof, n_elem=ne ** 3, workers=nw, sec_per_action=t_mp,
+                              dof_per_s=ndof / t_mp, reps=reps)
+    return out
+
+
+def bench_hex(args):
+    """Hexahedral Poisson action on one GPU (row N2: north_star's "structured
+    quad/hex meshes"): --hex-ne^3 warped hexahedra of order p (default p = 8,
+    27^3 = 19,683 elements, 10,218,313 DOF, ~1e7 DOF like config 4).  A step
+    = one sem_apply (element kernel + seam sum).  --gpus N > 1 runs N
+    independent replicas (the hex path has no multi-GPU decomposition yet)."""
+    import torch
+    from spectralelementmethod_amd import operators, meshgen
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    p, ne = args.p, args.hex_ne
+    t0 = time.time()
+    nodes, e2n = meshgen.structured_cube(ne, ne, ne, p, warp=args.warp)
+    log("hex mesh %d^3 p=%d: %d elements, %d nodes (%.1fs)" % (ne, p, e2n.shape[0],
+                                                               nodes.shape[1], time.time() - t0))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    op = operators.SEMOperator(p, e2n, nodes, device=dev)
+    op.compute_geometry()
+    torch.cuda.synchronize()
+    t_setup = time.perf_counter() - t0
+    plan = op.plan_info()
+    log("hex plan %s; setup %.2fs" % (plan, t_setup))
+    g = torch.Generator(device=dev).manual_seed(1234)
+    u = torch.randn(op.ndof, dtype=torch.float64, device=dev, generator=g)
+    y = torch.empty_like(u)
+    for _ in range(args.warmup):
+        op.apply(u, out=y)
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    events = [(ev(), ev()) for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        events[k][0].record()
+        op.apply(u, out=y)
+        events[k][1].record()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    kern_ms = [a.elapsed_time(b) for a, b in events]
+    kern_avg_s = float(np.mean(kern_ms)) / 1e3
+    parity = None
+    if not args.no_check:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import sem_oracle
+        gll = np.load(os.path.join(ROOT, "tests", "golden", "gll.npz"))
+        t0 = time.perf_counter()
+        P = sem_oracle.HexPoissonProblem(nodes, e2n, gll["half_%d" % p])
+        ref = P.apply(u.cpu().numpy())
+        got = y.cpu().numpy()
+        parity = {"rel_l2": float(np.linalg.norm(got - ref) / np.linalg.norm(ref)),
+                  "vs": "oracle/sem_oracle.py HexPoissonProblem (whole mesh)",
+                  "tolerance": 1e-10, "oracle_sec": time.perf_counter() - t0}
+        log("hex parity %s" % parity)
+        assert parity["rel_l2"] < parity["tolerance"], parity
+    n_nodes, E = op.ndof, op.n_elem
+    B = alg_bytes_hex(n_nodes, E, p)
+    F = alg_flops_hex(E, p)
+    achieved = B / kern_avg_s / 1e9
+    traffic = None
+    if args.traffic_json and os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+    result = {
+        "metric": METRIC.replace("Poisson p=8", "Poisson p=%d on hexahedra" % p),
+        "value": n_nodes * world * args.steps / elapsed, "unit": "DOF/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (structured warped hexahedral mesh, u ~ N(0,1))",
+        "config": {
+            "workload": "poisson hex p=%d, %d^3 hexahedra (row N2, north_star 'quad/hex')"
+                        % (p, ne),
+            "p": p, "ndim": 3, "geometry": "stored", "n_elem": E, "ndof": n_nodes,
+            "parallelism": "single GPU" if world == 1 else "%d independent replicas" % world,
+            "kernel_ms_avg": kern_avg_s * 1e3, "kernel_ms_min": float(np.min(kern_ms)),
+            "kernel_ms_quartiles": [float(q) for q in np.percentile(kern_ms, [25, 50, 75])],
+            "kernel_ms_note": "HIP events around each sem_apply on the launch stream: the "
+                              "element kernel + the seam-sum kernel",
+            "gflops_kernel": F / kern_avg_s / 1e9, "gpu_setup_sec": t_setup,
+            "plan": plan,
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "bytes_model": "16*ndof + 52*E*(p+1)^3 (u, y, 6 factors + uint32 map per element node)",
+            "alg_bytes_per_launch": B, "kernel": "k_hex_poisson<%d,0> + k_hex_seam_sum" % (p + 1),
+            "fp64_tflops": F / kern_avg_s / 1e12, "fp64_peak_tflops": FP64_PEAK_TFLOPS,
+        },
+    }
+    if parity is not None:
+        result["parity"] = parity
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("timing CPU baseline (hexahedral NumPy oracle, child process)...")
+        env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1",
+                   MKL_NUM_THREADS="1")
+        out = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-baseline-only",
+                              "--dim", "3", "--p", str(p), "--warp", str(args.warp),
+                              "--cpu-budget", str(args.cpu_budget), "--cpu-workers",
+                              str(args.cpu_workers)],
+                             env=env, capture_output=True, text=True, check=True)
+        cb = json.loads(out.stdout.strip().splitlines()[-1])
+        fm = cb["faithful_mp"]
+        result["cpu_baseline"] = {
+            "value": fm["dof_per_s"], "unit": "DOF/s", "cores": fm["workers"], "kind": "port",
+            "sample": "per-element dense 3-D Laplacian applied element by element + np.add.at "
+                      "(the hexahedral form of examples/poisson.py:168-193 / squirmer:286), %d "
+                      "processes x OMP_NUM_THREADS=1 over an 8^3 p=%d warped mesh (%d DOF); "
+                      "host os.cpu_count()=%d" % (fm["workers"], p, fm["ndof"], os.cpu_count()),
+            "batched_sumfact_1thread_dof_per_s": cb["batched_sumfact"]["dof_per_s"],
+            "batched_sumfact_sample": "12^3 p=%d (%d DOF)" % (p, cb["batched_sumfact"]["ndof"]),
+        }
+    if rank == 0:
+        print(json.dumps(result), file=JSON_OUT, flush=True)
+    op.close()
+    return 0
 
 
 # ---------------------------------------------------------------- launcher
@@ -408,11 +616,17 @@ def main():
                          "ids, values) to DIR/iface_rank<r>.npz after the timed steps")
     ap.add_argument("--traffic-json", default=None,
                     help="JSON with PMC-measured HBM bytes per launch (profiles/)")
+    ap.add_argument("--dim", type=int, choices=[2, 3], default=2,
+                    help="3: the hexahedral Poisson action (bench_hex)")
+    ap.add_argument("--hex-ne", type=int, default=27, help="--dim 3: hexahedra per side")
     args = ap.parse_args()
 
     if args.cpu_baseline_only:  # child process: no GPU
-        print(json.dumps(cpu_baseline(args.p, args.warp, args.cpu_budget, args.cpu_workers)))
+        fn = cpu_baseline_hex if args.dim == 3 else cpu_baseline
+        print(json.dumps(fn(args.p, args.warp, args.cpu_budget, args.cpu_workers)))
         return 0
+    if args.dim == 3:
+        return bench_hex(args)
     if args.time_rank is not None:
         return time_rank(args)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
