@@ -586,17 +586,15 @@ int build_finish(sem_dd* d) {
         }
     }
   }
-  (void)hipFree(d->d_sidx);
-  (void)hipFree(d->d_seam_cj);
-  (void)hipFree(d->d_rest);
-  (void)hipFree(d->d_fidx);
-  (void)hipFree(d->d_rp);
-  (void)hipFree(d->d_rpos);
-  (void)hipFree(d->d_fzero);
-  d->d_fidx = nullptr;
-  d->d_rp = nullptr;
-  d->d_rpos = nullptr;
-  d->d_fzero = nullptr;
+  // every finish table is freed (and nulled) exactly once, before any new
+  // allocation: a rebuild after a map change may be handed the same addresses
+  for (void** pp : {(void**)&d->d_sidx, (void**)&d->d_seam_cj, (void**)&d->d_rest,
+                    (void**)&d->d_fidx, (void**)&d->d_rp, (void**)&d->d_rpos,
+                    (void**)&d->d_fzero}) {
+    (void)hipFree(*pp);
+    *pp = nullptr;
+  }
+  d->n_rest = 0;
   HIP_TRY(hipMalloc(&d->d_fidx, std::max<int64_t>(nc, 1) * sizeof(uint32_t)));
   HIP_TRY(hipMalloc(&d->d_rp, rp.size() * sizeof(int32_t)));
   HIP_TRY(hipMalloc(&d->d_rpos, rpos.size() * sizeof(uint32_t)));
@@ -611,10 +609,6 @@ int build_finish(sem_dd* d) {
   d->defer_zero = defer;
   // the interior's seam nodes (one DOF per node: DOF = node id) and the
   // interface DOFs the fused finish handles outside them
-  (void)hipFree(d->d_seam_cj);
-  (void)hipFree(d->d_rest);
-  d->d_seam_cj = nullptr;
-  d->d_rest = nullptr;
   // SEM_DD_FUSE_SEAM=0: the interior's own seam-sum launch, then k_dd_finish
   // (A/B and the bitwise test of the fused form)
   const char* fe = std::getenv("SEM_DD_FUSE_SEAM");
@@ -648,8 +642,6 @@ int build_finish(sem_dd* d) {
     // touches) is never needed unless it holds atomic first writers
     std::vector<uint32_t> sidx((size_t)std::max<int64_t>(ne, 1), 0u);
     for (int64_t t = 0; t < ne; ++t) sidx[t] = cidx[pidx[t]];
-    (void)hipFree(d->d_sidx);
-    d->d_sidx = nullptr;
     HIP_TRY(hipMalloc(&d->d_sidx, sidx.size() * sizeof(uint32_t)));
     HIP_TRY(hipMemcpy(d->d_sidx, sidx.data(), sidx.size() * sizeof(uint32_t),
                       hipMemcpyHostToDevice));
@@ -1205,6 +1197,9 @@ void sem_dd_destroy(sem_dd* d) {
   (void)hipFree(d->d_rp);
   (void)hipFree(d->d_rpos);
   (void)hipFree(d->d_fzero);
+  (void)hipFree(d->d_sidx);
+  (void)hipFree(d->d_seam_cj);
+  (void)hipFree(d->d_rest);
   if (d->ev0) (void)hipEventDestroy(d->ev0);
   if (d->ev1) (void)hipEventDestroy(d->ev1);
   if (d->side) (void)hipStreamDestroy(d->side);

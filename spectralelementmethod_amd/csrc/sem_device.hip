@@ -168,7 +168,10 @@ uint64_t ctx_epoch(const sem_ctx* c) { return c->epoch; }
 int ctx_dpn(const sem_ctx* c) { return c->dpn; }
 uint64_t ctx_map_epoch(const sem_ctx* c) { return c->map_epoch; }
 bool ctx_seam_fusable(const sem_ctx* c) {
-  return c->seam && c->n_seam > 0 && c->dpn == 1 && c->seam_ns >= 1 && c->seam_ns <= 8;
+  // the n = 17 MFMA seam form sums its own seams (launch_apply_n ignores
+  // defer_seam_sum there), so it is never fused with the finish
+  return c->seam && !c->mfma && c->n_seam > 0 && c->dpn == 1 && c->seam_ns >= 1 &&
+         c->seam_ns <= 8;
 }
 int ctx_seam_gids(const sem_ctx* c, std::vector<uint32_t>* gids) {
   gids->assign((size_t)c->n_seam, 0u);

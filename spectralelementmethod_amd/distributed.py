@@ -511,6 +511,18 @@ class OverlappedOperator(object):
             # rank-sized y_c (sem_dd_create's local mode)
             self.iface = SEMOperator(p, e2n[pl.iface_elems], nodes, **kw) \
                 if pl.iface_elems.size else None
+            # a local-mode interface plan with atomic first
+            # writers zeroes its whole zero list (nearly every node of the
+            # rank) on every step; such plans (generic / unstructured
+            # partitions) take the compact numbering of the interface DOFs
+            # instead (sem_dd_create's compact mode)
+            self.iface_compact = False
+            if (self.iface is not None and dofs_per_node == 1 and
+                    self.iface.plan_info().get("atomic_groups", 0) > 0):
+                self.iface.close()
+                self.iface = SEMOperator(p, pl.e2n_iface, np.asarray(nodes)[:, pl.iface_nodes],
+                                         **kw)
+                self.iface_compact = True
             self.interior = SEMOperator(p, e2n[pl.interior_elems], nodes, **kw) \
                 if pl.interior_elems.size else None
             self.ops = [o for o in (self.iface, self.interior) if o is not None]

@@ -449,3 +449,72 @@ def test_captured_step_equals_eager(gpu):
         assert dx < 1e-12 and abs(its0 - its1) <= 16, (rank, dx, its0, its1)
         print("rank %d host enqueue per step (transport call excluded): eager %.1f us, "
               "graphs %.1f us" % (rank, us_eager, us_graph))
+
+
+def _remap_worker(rank, world, port, q):
+    """sem_set_map on both contexts of a live decomposition
+    rebuilds its finish tables (freed once, reallocated); the next step must
+    equal a freshly built decomposition bit for bit, eager and captured."""
+    import sys
+    for pth in (ROOT, os.path.join(ROOT, "oracle")):
+        if pth not in sys.path:
+            sys.path.insert(0, pth)
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from spectralelementmethod_amd import _lib
+        from spectralelementmethod_amd.distributed import OverlappedOperator, StripPartition
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        p = 8
+        part = StripPartition(24, 16, p, world, rank)
+        nodes, e2n = part.local_mesh(0.05)
+        kw = dict(owned=part.owned, transport="torch", world=world, rank=rank)
+        op = OverlappedOperator(p, nodes, e2n, part.neighbors, 1, dev, **kw)
+        g = torch.Generator(device=dev).manual_seed(11 + rank)
+        u = torch.randn(op.ndof, dtype=torch.float64, device=dev, generator=g)
+        y = torch.zeros_like(u)
+        op.step(u, y)
+        for o in op.ops:  # the same map again: a new plan, new finish tables
+            _lib.check(o._lib.sem_set_map(o._ctx, _lib.tptr(o.e2n), _lib.stream_ptr()))
+            o.compute_geometry()
+        ys = {}
+        for mode in (False, True):
+            op.set_graphs(mode)
+            yy = torch.full_like(u, 5.0)
+            for _ in range(3):
+                op.step(u, yy)
+            torch.cuda.synchronize()
+            ys[mode] = yy.clone()
+        op.set_graphs(False)
+        fresh = OverlappedOperator(p, nodes, e2n, part.neighbors, 1, dev, **kw)
+        y_ref = torch.zeros_like(u)
+        fresh.step(u, y_ref)
+        torch.cuda.synchronize()
+        q.put((rank, torch.equal(ys[False], y_ref), torch.equal(ys[True], y_ref)))
+        fresh.close()
+        op.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_remap_rebuilds_finish_bitwise(gpu):
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_remap_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    try:
+        res = [q.get(timeout=150) for _ in range(world)]
+    finally:
+        for pr in procs:
+            pr.join(timeout=60)
+    for pr in procs:
+        assert pr.exitcode == 0
+    for rank, eager_ok, graph_ok in res:
+        assert eager_ok and graph_ok, (rank, eager_ok, graph_ok)
