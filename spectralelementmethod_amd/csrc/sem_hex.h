@@ -53,12 +53,30 @@ struct HexLaunch {
   const int* wg_len;                // [n_wg] chain length of workgroup w
   const int* elist;                 // [pos] element at position wg_off + k*S + s, -1 = empty slot
   const unsigned long long* cmask;  // [pos] boundary columns written into slots
-  const uint8_t* cflag;             // [n_wg*S] bit 0: chain head face slotted, bit 1: tail face
+  const uint8_t* cflag;             // [n_wg*S] bit 0: chain head face slotted, bit 1: tail face,
+                                    // bit 2: the sub-chain's xi2 = 0 face is the xi2 = n-1
+                                    // face of slot s-1's (z-merge: summed in LDS)
   double* slot;                     // column slots [pos][n][NBC], then face slots [n_wg*S][2][n^2]
   int64_t face_base;
 };
 
 enum { HEX_SET = 0, HEX_ACC = 1, HEX_DIAG = 2 };
+
+// z-merge (xi2 faces between the slots of a workgroup summed in LDS): off by
+// default -- its exchange buffer pushes n = 9 past three workgroups per CU
+#ifndef SEM_HEX_ZMERGE
+#define SEM_HEX_ZMERGE 0
+#endif
+constexpr bool HEX_ZMERGE = SEM_HEX_ZMERGE != 0;
+
+// D and D^T as a kernel argument: the wave-uniform coefficients of the
+// register-direction contractions are read with scalar loads (SGPR operands)
+// instead of LDS broadcasts, which cost the LDS pipe as much as data reads.
+template <int N>
+struct HexD {
+  double dt[N * N];  // dt[r*N + a] = D[a][r]: column r of D, contiguous
+  double d[N * N];   // d[q*N + a] = D[q][a]: row q of D
+};
 
 // boundary-column index of (b, c) in [0, 4(n-1)), -1 for an interior column
 template <int N>
@@ -72,7 +90,8 @@ __device__ __forceinline__ int hex_bcol(int b, int c) {
 
 // Poisson stiffness action on hexahedra (MODE HEX_SET / HEX_ACC), or the
 // diagonal of the assembled operator (HEX_DIAG; u unused).  G: stored factors
-// [E][a][6][b*n + c], components (00, 01, 02, 11, 12, 22).
+// [E][a][b*n + c][6], components (00, 01, 02, 11, 12, 22): a thread reads its
+// node's six as three 16-byte loads.
 #ifndef SEM_HEX_MIN_WAVES
 #define SEM_HEX_MIN_WAVES 4
 #endif
@@ -80,12 +99,15 @@ template <int N, int MODE>
 __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
     k_hex_poisson(const double* __restrict__ u, double* __restrict__ y,
                   const uint32_t* __restrict__ map, const double* __restrict__ G,
-                  const double* __restrict__ gD, HexLaunch P) {
+                  const double* __restrict__ gD, HexLaunch P, const HexD<N> Dk) {
   constexpr int N2 = N * N, N3 = N2 * N, S = hex_slots(N), T = hex_threads(N), NBC = hex_nbc(N);
   __shared__ double sD[N2];
   __shared__ double sU[S * N3];
   __shared__ double sA[S * N3];
   __shared__ double sB[S * N3];
+#if SEM_HEX_ZMERGE
+  __shared__ double sX[S * N2];  // z-merge: xi2 = 0 face columns handed to slot s-1
+#endif
   const int tid = threadIdx.x;
   for (int i = tid; i < N2; i += T) sD[i] = gD[i];
   const int w = blockIdx.x;
@@ -101,36 +123,63 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
   double* const sb = sB + sl * N3;
   const int bcol = hex_bcol<N>(b, c);
   const uint8_t cf = active ? P.cflag[w * S + s] : 0;
+  // z-merge: slot s hands its xi2 = 0 face to slot s-1, whose xi2 = n-1 face
+  // holds the same nodes in the same (a, b) order (the planner checked every
+  // chain step); the merged node then has one writer fewer
+  const bool give = (cf & 4) && c == 0;
+  const bool take = active && c == N - 1 && s + 1 < S && (P.cflag[w * S + s + 1] & 4);
+  bool wg_merge = false;
+#if SEM_HEX_ZMERGE
+#pragma unroll
+  for (int t = 1; t < S; ++t) wg_merge |= (P.cflag[w * S + t] & 4) != 0;
+#endif
   double* const face = P.slot + P.face_base + (int64_t)(w * S + sl) * 2 * N2 + bc;
   __syncthreads();  // sD
   double carry = 0.0;
+  // the element map of the next chain step is loaded one step ahead
+  uint32_t mn[N];
+  int en = active ? P.elist[base + s] : 0;
+  if (active) {
+#pragma unroll
+    for (int a = 0; a < N; ++a) mn[a] = map[(int64_t)en * N3 + a * N2 + bc];
+  }
 #pragma unroll 1
   for (int k = 0; k < L; ++k) {
     const int pos = base + k * S + s;
-    const int e = active ? P.elist[pos] : 0;
+    const int e = en;
     uint32_t m[N];
-    const double* g = G + (int64_t)e * 6 * N3 + bc;
-    if (active) {
-      const uint32_t* me = map + (int64_t)e * N3 + bc;
 #pragma unroll
-      for (int a = 0; a < N; ++a) m[a] = me[a * N2];
+    for (int a = 0; a < N; ++a) m[a] = mn[a];
+    const double* g = G + ((int64_t)e * N3 + bc) * 6;
+    if (active) {
       if constexpr (MODE != HEX_DIAG) {
         double uc[N];
 #pragma unroll
-        for (int a = 0; a < N; ++a) uc[a] = u[m[a]];
+        for (int a = 0; a < N; ++a) {
+#ifdef SEM_HEX_DIAG_NOGATHER  // diagnostic builds only: no u gather
+          uc[a] = (double)m[a];
+#else
+          uc[a] = u[m[a]];
+#endif
+        }
 #pragma unroll
         for (int a = 0; a < N; ++a) su[a * N2 + bc] = uc[a];
       } else {
         // diagonal: G00 of this column, G11 / G22 of the other threads' nodes
 #pragma unroll
         for (int a = 0; a < N; ++a) {
-          su[a * N2 + bc] = g[(a * 6 + 0) * N2];
-          sa[a * N2 + bc] = g[(a * 6 + 3) * N2];
-          sb[a * N2 + bc] = g[(a * 6 + 5) * N2];
+          su[a * N2 + bc] = g[a * N2 * 6 + 0];
+          sa[a * N2 + bc] = g[a * N2 * 6 + 3];
+          sb[a * N2 + bc] = g[a * N2 * 6 + 5];
         }
       }
     }
     __syncthreads();
+    if (active && k + 1 < L) {
+      en = P.elist[pos + S];
+#pragma unroll
+      for (int a = 0; a < N; ++a) mn[a] = map[(int64_t)en * N3 + a * N2 + bc];
+    }
     // The contractions run with the summation index outermost and NOT
     // unrolled, the node row a unrolled inside: every register array is
     // indexed by a compile-time a, and a step holds only its own operands
@@ -151,16 +200,22 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
           const double dbr = sD[b * N + r], dcr = sD[c * N + r];
 #pragma unroll
           for (int a = 0; a < N; ++a) {
-            d0[a] = fma(sD[a * N + r], ur, d0[a]);
+            d0[a] = fma(Dk.dt[r * N + a], ur, d0[a]);
             d1[a] = fma(dbr, su[a * N2 + r * N + c], d1[a]);
             d2[a] = fma(dcr, su[a * N2 + b * N + r], d2[a]);
           }
         }
 #pragma unroll
         for (int a = 0; a < N; ++a) {
-          const double* ga = g + a * 6 * N2;
-          const double g00 = ga[0], g01 = ga[N2], g02 = ga[2 * N2], g11 = ga[3 * N2],
-                       g12 = ga[4 * N2], g22 = ga[5 * N2];
+          const double2* ga = reinterpret_cast<const double2*>(g + a * N2 * 6);
+#ifdef SEM_HEX_DIAG_NOG  // diagnostic builds only: no factor stream
+          const double2 q0 = make_double2(1.0, 0.1 * a), q1 = make_double2(0.2, 1.0),
+                        q2 = make_double2(0.3 * c, 1.0);
+          (void)ga;
+#else
+          const double2 q0 = ga[0], q1 = ga[1], q2 = ga[2];
+#endif
+          const double g00 = q0.x, g01 = q0.y, g02 = q1.x, g11 = q1.y, g12 = q2.x, g22 = q2.y;
           w0[a] = g00 * d0[a] + g01 * d1[a] + g02 * d2[a];
           sa[a * N2 + bc] = g01 * d0[a] + g11 * d1[a] + g12 * d2[a];
           sb[a * N2 + bc] = g02 * d0[a] + g12 * d1[a] + g22 * d2[a];
@@ -178,7 +233,7 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
           const double dqb = sD[q * N + b], dqc = sD[q * N + c];
 #pragma unroll
           for (int a = 0; a < N; ++a) {
-            yv[a] = fma(sD[q * N + a], wq, yv[a]);
+            yv[a] = fma(Dk.d[q * N + a], wq, yv[a]);
             yv[a] = fma(dqb, sa[a * N2 + q * N + c], yv[a]);
             yv[a] = fma(dqc, sb[a * N2 + b * N + q], yv[a]);
           }
@@ -203,14 +258,25 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
         }
 #pragma unroll
         for (int a = 0; a < N; ++a) {
-          const double* ga = g + a * 6 * N2;
+          const double* ga = g + a * N2 * 6;
           const double daa = sD[a * N + a];
-          yv[a] += 2.0 * (daa * dbb * ga[N2] + daa * dcc * ga[2 * N2] + dbb * dcc * ga[4 * N2]);
+          yv[a] += 2.0 * (daa * dbb * ga[1] + daa * dcc * ga[2] + dbb * dcc * ga[4]);
         }
       }
       __syncthreads();  // su / sa / sb are rewritten by the next element
     }
-    if (active) {
+#if SEM_HEX_ZMERGE
+    if (wg_merge) {  // workgroup-uniform
+      if (give)
+#pragma unroll
+        for (int a = 0; a < N; ++a) sX[sl * N2 + a * N + b] = yv[a];
+      __syncthreads();
+      if (take)
+#pragma unroll
+        for (int a = 0; a < N; ++a) yv[a] += sX[(sl + 1) * N2 + a * N + b];
+    }
+#endif
+    if (active && !give) {
       if (k > 0) yv[0] += carry;
       const bool last = k == L - 1;
       if (!last) carry = yv[N - 1];
@@ -220,6 +286,9 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
       for (int a = 0; a < N; ++a) {
         if (a == N - 1 && !last) continue;  // carried into the next element's row 0
         const double v = yv[a];
+#ifdef SEM_HEX_DIAG_NOSTORE  // diagnostic builds only: no stores
+        if (!(v != v)) continue;
+#endif
         if (a == 0 && k == 0 && (cf & 1)) {
           face[0] = v;
         } else if (a == N - 1 && last && (cf & 2)) {
@@ -265,7 +334,7 @@ __global__ void k_hex_seam_sum(double* __restrict__ y, const uint32_t* __restric
 // The transforms act on coordinates relative to the element's node (0,0,0)
 // (the constant is added back to x_phys) to keep the rounding of V^-1's
 // large alternating entries off the absolute position.  Outputs may be null:
-// GP [E][a][6][n^2] (the action's layout), x_phys [E][3][n^3], J / invJ
+// GP [E][n^3][6] (the action's layout), x_phys [E][3][n^3], J / invJ
 // [E][3][3][n^3], detJ / detJxW [E][n^3].  bad counts nodes with detJ <= 0.
 template <int N>
 __global__ void __launch_bounds__(hex_threads(N))
@@ -395,13 +464,16 @@ __global__ void __launch_bounds__(hex_threads(N))
         const double W = ((det * sw[a]) * sw[b]) * sw[c];
         const int64_t node = e * N3 + a * N2 + bc;
         if (GP) {
-          double* gp = GP + (e * N + a) * 6 * N2 + bc;
-          gp[0] = W * (iJ[0][0] * iJ[0][0] + iJ[0][1] * iJ[0][1] + iJ[0][2] * iJ[0][2]);
-          gp[N2] = W * (iJ[0][0] * iJ[1][0] + iJ[0][1] * iJ[1][1] + iJ[0][2] * iJ[1][2]);
-          gp[2 * N2] = W * (iJ[0][0] * iJ[2][0] + iJ[0][1] * iJ[2][1] + iJ[0][2] * iJ[2][2]);
-          gp[3 * N2] = W * (iJ[1][0] * iJ[1][0] + iJ[1][1] * iJ[1][1] + iJ[1][2] * iJ[1][2]);
-          gp[4 * N2] = W * (iJ[1][0] * iJ[2][0] + iJ[1][1] * iJ[2][1] + iJ[1][2] * iJ[2][2]);
-          gp[5 * N2] = W * (iJ[2][0] * iJ[2][0] + iJ[2][1] * iJ[2][1] + iJ[2][2] * iJ[2][2]);
+          double2* gp = reinterpret_cast<double2*>(GP + node * 6);
+          gp[0] = make_double2(
+              W * (iJ[0][0] * iJ[0][0] + iJ[0][1] * iJ[0][1] + iJ[0][2] * iJ[0][2]),
+              W * (iJ[0][0] * iJ[1][0] + iJ[0][1] * iJ[1][1] + iJ[0][2] * iJ[1][2]));
+          gp[1] = make_double2(
+              W * (iJ[0][0] * iJ[2][0] + iJ[0][1] * iJ[2][1] + iJ[0][2] * iJ[2][2]),
+              W * (iJ[1][0] * iJ[1][0] + iJ[1][1] * iJ[1][1] + iJ[1][2] * iJ[1][2]));
+          gp[2] = make_double2(
+              W * (iJ[1][0] * iJ[2][0] + iJ[1][1] * iJ[2][1] + iJ[1][2] * iJ[2][2]),
+              W * (iJ[2][0] * iJ[2][0] + iJ[2][1] * iJ[2][1] + iJ[2][2] * iJ[2][2]));
         }
         if (xph)
 #pragma unroll
@@ -439,7 +511,7 @@ __global__ void k_hex_assemble(const uint32_t* __restrict__ e2n, const double* _
     unsafeAtomicAdd(out + e2n[t], vals[t]);
 }
 
-// user factors [E][6][n^3] -> the action's layout [E][a][6][n^2]
+// user factors [E][6][n^3] -> the action's layout [E][n^3][6]
 __global__ void k_hex_pack_geom(const double* __restrict__ G, int64_t n_elem, int n,
                                 double* __restrict__ GP) {
   const int64_t n2 = (int64_t)n * n, n3 = n2 * n;
@@ -450,8 +522,7 @@ __global__ void k_hex_pack_geom(const double* __restrict__ G, int64_t n_elem, in
     const int64_t rem = t - e * 6 * n3;
     const int comp = (int)(rem / n3);
     const int64_t node = rem - comp * n3;
-    const int64_t a = node / n2, bc = node - a * n2;
-    GP[((e * n + a) * 6 + comp) * n2 + bc] = G[t];
+    GP[(e * n3 + node) * 6 + comp] = G[t];
   }
 }
 

@@ -34,7 +34,7 @@ struct HexState {
   uint32_t* d_zero = nullptr;  // unreferenced nodes (overwrite mode zeroes them)
   int64_t n_zero = 0;
   uint32_t* d_map = nullptr;   // the library's copy of the caller's map [E][n][n][n]
-  double* d_G = nullptr;       // stored factors [E][a][6][n^2]
+  double* d_G = nullptr;       // stored factors [E][n^3][6]
   bool have_G = false;
   // diagnostics (sem_plan_info)
   int64_t n_chains = 0, n_subchains = 0, chain_len = 0, n_direct = 0;
@@ -173,12 +173,26 @@ int hex_build_plan(const std::vector<uint32_t>& h, int64_t E, int64_t n_node, in
       off += len;
     }
   }
-  // 4. longest first, then by head element (neighbouring sub-chains share
-  //    faces: they run in the same or adjacent workgroups)
-  std::stable_sort(sub.begin(), sub.end(), [&](const Sub& x, const Sub& y) {
-    if (x.len != y.len) return x.len > y.len;
-    return order[x.start] < order[y.start];
-  });
+  // 4. longest first, then by the smallest node id of the head element
+  //    (neighbouring sub-chains share faces: on a locality-ordered node
+  //    numbering they run in the same or adjacent workgroups, whatever the
+  //    element order)
+  std::vector<uint32_t> key(sub.size());
+  for (size_t i = 0; i < sub.size(); ++i) {
+    const uint32_t* me = &h[order[sub[i].start] * N3];
+    key[i] = *std::min_element(me, me + N3);
+  }
+  {
+    std::vector<size_t> idx(sub.size());
+    std::iota(idx.begin(), idx.end(), 0);
+    std::stable_sort(idx.begin(), idx.end(), [&](size_t x, size_t y) {
+      if (sub[x].len != sub[y].len) return sub[x].len > sub[y].len;
+      return key[x] < key[y];
+    });
+    std::vector<Sub> sorted(sub.size());
+    for (size_t i = 0; i < idx.size(); ++i) sorted[i] = sub[idx[i]];
+    sub.swap(sorted);
+  }
   // 5. workgroups of S equal-length sub-chains
   std::vector<int64_t> sub_wg(sub.size()), sub_slot(sub.size());
   int64_t pos = 0;
@@ -205,6 +219,29 @@ int hex_build_plan(const std::vector<uint32_t>& h, int64_t E, int64_t n_node, in
   const int64_t n_wg = (int64_t)P.wg_off.size(), n_pos = pos;
   P.cmask.assign(n_pos, 0ull);
   P.cflag.assign(n_wg * S, 0);
+  // 5b. z-merge: slot s of a workgroup hands its xi2 = 0 face to slot s-1
+  //     when, at every chain step, that face IS slot s-1's xi2 = n-1 face
+  //     node for node (same (a, b)); the kernel sums it in LDS
+  std::vector<uint8_t> zm(n_wg * S, 0);
+  const char* zenv = std::getenv("SEM_HEX_ZMERGE");
+  if (semh::HEX_ZMERGE && !(zenv && std::atoi(zenv) == 0))
+    for (int64_t w = 0; w < n_wg; ++w)
+      for (int s = 1; s < S; ++s) {
+        bool ok = true;
+        for (int64_t k = 0; k < P.wg_len[w] && ok; ++k) {
+          const int e1 = P.elist[P.wg_off[w] + k * S + s - 1], e2 = P.elist[P.wg_off[w] + k * S + s];
+          if (e1 < 0 || e2 < 0) {
+            ok = false;
+            break;
+          }
+          const uint32_t* m1 = &h[(int64_t)e1 * N3];
+          const uint32_t* m2 = &h[(int64_t)e2 * N3];
+          for (int ab = 0; ab < N2 && ok; ++ab) ok = m1[ab * N + N - 1] == m2[ab * N];
+        }
+        zm[w * S + s] = ok ? 1 : 0;
+      }
+  // a thread whose face is merged emits no write of its own
+  auto merged = [&](int64_t w, int64_t s, int c) { return c == 0 && zm[w * S + s]; };
   // 6. events per node
   std::vector<uint8_t> cnt(n_node, 0);
   auto bump = [&](uint32_t g) {
@@ -215,7 +252,8 @@ int hex_build_plan(const std::vector<uint32_t>& h, int64_t E, int64_t n_node, in
     for (int64_t k = 0; k < len; ++k) {
       const uint32_t* me = &h[order[sub[i].start + k] * N3];
       const int amax = (k == len - 1) ? N : N - 1;
-      for (int64_t t = 0; t < (int64_t)amax * N2; ++t) bump(me[t]);
+      for (int64_t t = 0; t < (int64_t)amax * N2; ++t)
+        if (!merged(sub_wg[i], sub_slot[i], (int)(t % N))) bump(me[t]);
     }
   }
   // 7. face flags, column masks
@@ -235,6 +273,7 @@ int hex_build_plan(const std::vector<uint32_t>& h, int64_t E, int64_t n_node, in
       if (cnt[hd[j]] > 1) f |= 1;
       if (cnt[tl[j]] > 1) f |= 2;
     }
+    if (zm[sub_wg[i] * S + sub_slot[i]]) f |= 4;
     P.cflag[sub_wg[i] * S + sub_slot[i]] = f;
     for (int64_t k = 0; k < len; ++k) {
       const int64_t p = P.wg_off[sub_wg[i]] + k * S + sub_slot[i];
@@ -243,7 +282,7 @@ int hex_build_plan(const std::vector<uint32_t>& h, int64_t E, int64_t n_node, in
       for (int b = 0; b < N; ++b)
         for (int c = 0; c < N; ++c) {
           const int bcol = bcol_of(b, c);
-          if (bcol < 0) continue;
+          if (bcol < 0 || merged(sub_wg[i], sub_slot[i], c)) continue;
           for (int a = 0; a < N; ++a) {
             if (a == N - 1 && k < len - 1) continue;
             if (a == 0 && k == 0 && (f & 1)) continue;
@@ -275,6 +314,7 @@ int hex_build_plan(const std::vector<uint32_t>& h, int64_t E, int64_t n_node, in
         for (int b = 0; b < N; ++b)
           for (int c = 0; c < N; ++c) {
             const int bc = b * N + c, bcol = bcol_of(b, c);
+            if (merged(w, s, c)) continue;
             const bool colslot = bcol >= 0 && ((mask >> bcol) & 1ull);
             for (int a = 0; a < N; ++a) {
               if (a == N - 1 && k < len - 1) continue;
@@ -286,14 +326,14 @@ int hex_build_plan(const std::vector<uint32_t>& h, int64_t E, int64_t n_node, in
                 sidx = P.face_base + (w * S + s) * 2 * N2 + N2 + bc;
               else if (colslot)
                 sidx = (p * N + a) * NBC + bcol;
-              if (int rc = fn(g, sidx)) return rc;
+              if (int rc = fn(g, sidx, (int64_t)i)) return rc;
             }
           }
       }
     }
     return SEM_OK;
   };
-  int rc = for_events([&](uint32_t g, int64_t sidx) -> int {
+  int rc = for_events([&](uint32_t g, int64_t sidx, int64_t) -> int {
     if (sidx < 0) {
       if (cnt[g] != 1)
         return fail(SEM_E_NOTIMPL,
@@ -310,7 +350,7 @@ int hex_build_plan(const std::vector<uint32_t>& h, int64_t E, int64_t n_node, in
   const uint32_t n_writes = start[n_node];
   P.seam_idx.assign(n_writes, 0);
   std::vector<uint32_t> fill(start.begin(), start.end() - 1);
-  for_events([&](uint32_t g, int64_t sidx) -> int {
+  for_events([&](uint32_t g, int64_t sidx, int64_t) -> int {
     if (sidx >= 0) P.seam_idx[fill[g]++] = (uint32_t)sidx;
     return SEM_OK;
   });
@@ -333,18 +373,24 @@ int hex_build_plan(const std::vector<uint32_t>& h, int64_t E, int64_t n_node, in
 template <int N>
 int launch_hex_apply(sem_ctx* c, int mode, const double* u, double* y, hipStream_t st) {
   HexState* H = c->hex;
-  const semh::HexLaunch L{H->d_wg_off, H->d_wg_len,  H->d_elist, H->d_cmask,
-                          H->d_cflag,  H->d_slot, H->face_base};
+  const semh::HexLaunch L{H->d_wg_off, H->d_wg_len, H->d_elist,   H->d_cmask,
+                          H->d_cflag,  H->d_slot,   H->face_base};
   const dim3 g((unsigned)H->n_wg), b(semh::hex_threads(N));
+  semh::HexD<N> Dk;
+  for (int i = 0; i < N; ++i)
+    for (int j = 0; j < N; ++j) {
+      Dk.dt[j * N + i] = c->hD[i * N + j];
+      Dk.d[i * N + j] = c->hD[i * N + j];
+    }
   if (mode == semh::HEX_SET)
     hipLaunchKernelGGL((semh::k_hex_poisson<N, semh::HEX_SET>), g, b, 0, st, u, y, H->d_map,
-                       H->d_G, c->d_D, L);
+                       H->d_G, c->d_D, L, Dk);
   else if (mode == semh::HEX_ACC)
     hipLaunchKernelGGL((semh::k_hex_poisson<N, semh::HEX_ACC>), g, b, 0, st, u, y, H->d_map,
-                       H->d_G, c->d_D, L);
+                       H->d_G, c->d_D, L, Dk);
   else
     hipLaunchKernelGGL((semh::k_hex_poisson<N, semh::HEX_DIAG>), g, b, 0, st, u, y, H->d_map,
-                       H->d_G, c->d_D, L);
+                       H->d_G, c->d_D, L, Dk);
   HIP_TRY(hipGetLastError());
   if (H->n_seam) {
     const dim3 gs(grid_for(H->n_seam, 256, 8192)), bs(256);
