@@ -616,6 +616,10 @@ def main():
                          "ids, values) to DIR/iface_rank<r>.npz after the timed steps")
     ap.add_argument("--traffic-json", default=None,
                     help="JSON with PMC-measured HBM bytes per launch (profiles/)")
+    ap.add_argument("--numbering", choices=["lex", "rcm"], default="lex",
+                    help="rcm: the reference DOFManager's default node order (reverse "
+                         "Cuthill-McKee of the element-clique graph, sem/discrete.py:169-178), "
+                         "element order unchanged; one GPU, Poisson")
     ap.add_argument("--dim", type=int, choices=[2, 3], default=2,
                     help="3: the hexahedral Poisson action (bench_hex)")
     ap.add_argument("--hex-ne", type=int, default=27, help="--dim 3: hexahedra per side")
@@ -674,6 +678,21 @@ def main():
     t0 = time.time()
     if kind == POISSON:
         nodes, e2n = part.local_mesh(args.warp)
+        if args.numbering == "rcm":
+            if world != 1:
+                raise SystemExit("--numbering rcm is single-GPU")
+            from scipy.sparse import csgraph
+            from spectralelementmethod_amd.discrete import _pair_graph
+            t0 = time.time()
+            # what DOFManager(mesh, ...) does by default (rcm_order=True):
+            # the clique graph of every cell's nodes, scipy RCM, nodes permuted
+            perm = csgraph.reverse_cuthill_mckee(
+                _pair_graph(e2n.reshape(e2n.shape[0], -1), nodes.shape[1]), True)
+            inv = np.empty_like(perm)
+            inv[perm] = np.arange(perm.size, dtype=perm.dtype)
+            nodes = nodes[:, perm].copy()
+            e2n = inv[e2n].astype(np.uint32)
+            log("RCM numbering (reference default): %.1fs" % (time.time() - t0))
     else:
         from spectralelementmethod_amd import meshgen
         if world != 1:
@@ -705,10 +724,13 @@ def main():
 
     if opname == "pcg":
         return bench_pcg(args, op, part, nodes, dev, world, rank, ndof_global, t_setup)
+    rcm_nodes, rcm_e2n = (nodes, e2n) if args.numbering == "rcm" else (None, None)
     del nodes, e2n
 
     # u from one global field so shared DOFs agree on both sides of an interface
     u = global_random_field(part, dpn, kind, op.ndof, dev)
+    if args.numbering == "rcm":  # the same field, renumbered
+        u = u[torch_index(perm, dev)].contiguous()
     y = torch.empty_like(u)
 
     for _ in range(args.warmup):
@@ -753,7 +775,18 @@ def main():
     kern_avg_s = (region_ms if region_ms is not None else float(np.mean(kern_ms))) / 1e3
 
     parity, parity_ranks, parity_iface = None, None, None
-    if not args.no_check:
+    if not args.no_check and args.numbering == "rcm":
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import sem_oracle
+        gll = np.load(os.path.join(ROOT, "tests", "golden", "gll.npz"))
+        P = sem_oracle.PoissonProblem(rcm_nodes, rcm_e2n, gll["half_%d" % p],
+                                      batched_geometry=True)
+        ref = P.apply(u.cpu().numpy())
+        parity = {"rel_l2": float(np.linalg.norm(y.cpu().numpy() - ref) / np.linalg.norm(ref)),
+                  "vs": "oracle on the whole RCM-numbered mesh", "tolerance": 1e-10}
+        log("parity %s" % parity)
+        assert parity["rel_l2"] < parity["tolerance"], parity
+    elif not args.no_check:
         assert torch.isfinite(y).all().item(), "non-finite output"
         if kind == POISSON:
             parity = parity_spot_check(op, y, u, part, p, args.warp)
@@ -785,7 +818,7 @@ def main():
     achieved = B / kern_avg_s / 1e9
     traffic, traffic_src = None, args.traffic_json
     if (traffic_src is None and kind == POISSON and plan["kernel"] == "column" and world == 1
-            and (p, args.nex, args.ney) == (8, 1024, 1024)):
+            and (p, args.nex, args.ney) == (8, 1024, 1024) and args.numbering == "lex"):
         traffic_src = os.path.join(ROOT, "bench_traffic", DEFAULT_TRAFFIC[geometry])
     if traffic_src and os.path.exists(traffic_src):
         with open(traffic_src) as f:
@@ -807,6 +840,7 @@ def main():
         "dtype": "f64",
         "data": "synthetic (structured warped quad mesh, u ~ N(0,1))",
         "config": {
+            "numbering": args.numbering,
             "workload": "%s p=%d, %dx%d elements %s (%s)" % (
                 opname, p, args.nex, args.ney,
                 "global mesh in %d strip(s)" % world if args.scaling == "strong"

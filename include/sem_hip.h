@@ -240,6 +240,17 @@ int sem_set_kernel(sem_ctx* ctx, int kernel);
 int sem_geom_from_nodes(sem_ctx* ctx, const double* d_nodes, const double* h_Veq_inv,
                         int op_kind, int64_t* n_bad_nodes, void* stream);
 
+/* Stored factors for op_kind from x_phys given per element (device, float64
+ * [n_elem][2][n][n], the FiniteElement.x_phys of each element,
+ * sem/discrete.py:582-585): J, det/inverse and detJxW as sem_geom_from_nodes
+ * computes them, without the equispaced->GLL transform.  With x_phys from the
+ * reference's own LU path (Mapping._compute_x_phys, sem/mapping.py:98-103),
+ * the factors carry the reference's float64 rounding of that transform --
+ * which dominates the action's error above p = 10.
+ * Quadrilaterals; SEM_E_DETJ as sem_geom_from_nodes. */
+int sem_geom_from_xphys(sem_ctx* ctx, const double* d_x_phys, int op_kind, int64_t* n_bad_nodes,
+                        void* stream);
+
 /* Reference-layout geometry fields for FiniteElement properties
  * (x_phys [E][2][n][n], J and invJ [E][2][2][n][n], detJ and detJxW
  * [E][n][n]; any output may be NULL).  sem/discrete.py:582-597. */

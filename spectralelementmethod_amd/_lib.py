@@ -60,6 +60,7 @@ SIGNATURES = {
     "sem_plan_info": (C.c_int, [_vp, C.POINTER(_i64), C.c_int]),
     "sem_geom_from_nodes": (C.c_int, [_vp, _vp, _dp, C.c_int, C.POINTER(_i64), _vp]),
     "sem_geom_fields": (C.c_int, [_vp, _vp, _dp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "sem_geom_from_xphys": (C.c_int, [_vp, _vp, C.c_int, C.POINTER(_i64), _vp]),
     "sem_set_geom": (C.c_int, [_vp, _vp, C.c_int, _vp]),
     "sem_set_geom_mode": (C.c_int, [_vp, C.c_int]),
     "sem_set_kernel": (C.c_int, [_vp, C.c_int]),

@@ -270,7 +270,7 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
 template <int N>
 int launch_geom_n(sem_ctx* c, const double* nodes, int op_kind, double* GP, double* xph,
                   double* J, double* iJ, double* dJ, double* dJW, double2* XG,
-                  const double2* XGin, hipStream_t st);
+                  const double2* XGin, hipStream_t st, const double* XEin = nullptr);
 template <int N>
 int upload_deo(sem_ctx* c);
 // one launch of the Poisson column kernel with D as compile-time constants

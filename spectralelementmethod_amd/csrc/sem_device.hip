@@ -1536,6 +1536,35 @@ int sem_geom_from_nodes(sem_ctx* c, const double* d_nodes, const double* h_Vinv,
   return SEM_OK;
 }
 
+int sem_geom_from_xphys(sem_ctx* c, const double* d_xphys, int op_kind, int64_t* n_bad_nodes,
+                        void* stream) {
+  if (!c || !d_xphys) return fail(SEM_E_INVALID, "null argument");
+  if (c->ndim == 3) return fail(SEM_E_NOTIMPL, "sem_geom_from_xphys: quadrilaterals only");
+  if (!c->have_basis) return fail(SEM_E_STATE, "sem_set_basis must precede geometry");
+  if (!c->d_e2n) return fail(SEM_E_STATE, "sem_set_map must precede geometry");
+  DeviceGuard g(c->device);
+  int rc;
+  if ((rc = check_op(c, op_kind))) return rc;
+  hipStream_t st = S(stream);
+  c->epoch++;
+  if ((rc = ensure_gp(c, op_kind, st))) return rc;
+  HIP_TRY(hipMemsetAsync(c->d_bad, 0, sizeof(unsigned long long), st));
+  SEM_DISPATCH_N(rc, c->n, launch_geom_n, c, nullptr, op_kind, c->d_GP[gp_slot(op_kind)], nullptr,
+                 nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, st, d_xphys);
+  if (rc) return rc;
+  HIP_TRY(hipGetLastError());
+  unsigned long long bad = 0;
+  HIP_TRY(hipMemcpyAsync(&bad, c->d_bad, sizeof(bad), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (n_bad_nodes) *n_bad_nodes = (int64_t)bad;
+  if (bad) return fail(SEM_E_DETJ, "detJ <= 0 at " + std::to_string(bad) + " quadrature nodes");
+  // the stored factors take over from any x_phys per node
+  if (op_kind == SEM_OP_POISSON) c->xg_valid = false;
+  if (op_kind == SEM_OP_AXISYM_STOKES) c->xg_axi = false;
+  if (gp_slot(op_kind) == 2) c->lin_valid = false;
+  return SEM_OK;
+}
+
 int sem_geom_fields(sem_ctx* c, const double* d_nodes, const double* h_Vinv, double* x_phys,
                     double* J, double* invJ, double* detJ, double* detJxW, void* stream) {
   if (!c) return fail(SEM_E_INVALID, "null ctx");

@@ -2612,7 +2612,8 @@ __global__ void __launch_bounds__(GeomShape<N>::THREADS)
                double* __restrict__ GP, double* __restrict__ xph, double* __restrict__ Jo,
                double* __restrict__ iJo, double* __restrict__ dJo, double* __restrict__ dJW,
                double2* __restrict__ XG, const uint32_t* __restrict__ owner,
-               const double2* __restrict__ XGin, unsigned long long* __restrict__ n_bad) {
+               const double2* __restrict__ XGin, const double* __restrict__ XEin,
+               unsigned long long* __restrict__ n_bad) {
   using S = GeomShape<N>;
   constexpr int NN = S::NN;
   constexpr int EPB = S::EPB;
@@ -2634,7 +2635,10 @@ __global__ void __launch_bounds__(GeomShape<N>::THREADS)
   uint32_t gi = 0;
   if (act) {
     gi = e2n[e * NN + node];
-    if (XGin) {  // x_phys already known per global node (NODAL mode re-derivation)
+    if (XEin) {  // x_phys given per element (sem_geom_from_xphys)
+      sx[el][0][node] = XEin[(e * 2 + 0) * NN + node];
+      sx[el][1][node] = XEin[(e * 2 + 1) * NN + node];
+    } else if (XGin) {  // x_phys already known per global node (NODAL mode re-derivation)
       const double2 xg = XGin[gi];
       sx[el][0][node] = xg.x;
       sx[el][1][node] = xg.y;
@@ -2654,7 +2658,8 @@ __global__ void __launch_bounds__(GeomShape<N>::THREADS)
   // measured on CPU emulation at p = 16: 6.8e-11 -> 1.2e-11 rel-L2 of the
   // action against the extended-precision oracle.
   double x0[2] = {0.0, 0.0};
-  if (act && !XGin) {
+  const bool given = XGin || XEin;  // x_phys given: no transform
+  if (act && !given) {
     x0[0] = sx[el][0][0];
     x0[1] = sx[el][1][0];
     for (int c = 0; c < 2; ++c) {
@@ -2668,7 +2673,7 @@ __global__ void __launch_bounds__(GeomShape<N>::THREADS)
   }
   __syncthreads();
   double xp[2] = {0.0, 0.0};
-  if (act && XGin) {
+  if (act && given) {
     x0[0] = sx[el][0][0];
     x0[1] = sx[el][1][0];
     xp[0] = sx[el][0][node] - x0[0];

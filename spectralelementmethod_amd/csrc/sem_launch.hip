@@ -175,12 +175,12 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
 template <int N>
 int launch_geom_n(sem_ctx* c, const double* nodes, int op_kind, double* GP, double* xph,
                   double* J, double* iJ, double* dJ, double* dJW, double2* XG,
-                  const double2* XGin, hipStream_t st) {
+                  const double2* XGin, hipStream_t st, const double* XEin) {
   using Sh = GeomShape<N>;
   const int grid = (int)((c->n_elem + Sh::EPB - 1) / Sh::EPB);
   hipLaunchKernelGGL((k_geometry<N>), dim3(grid), dim3(Sh::THREADS), 0, st, nodes, c->n_node,
                      c->d_e2n, c->n_elem, c->d_Vinv, c->d_D, c->d_w, op_kind, c->epw, c->d_epos, GP,
-                     xph, J, iJ, dJ, dJW, XG, XG ? c->d_owner : nullptr, XGin, c->d_bad);
+                     xph, J, iJ, dJ, dJW, XG, XG ? c->d_owner : nullptr, XGin, XEin, c->d_bad);
   return SEM_OK;
 }
 
@@ -195,7 +195,8 @@ int upload_deo(sem_ctx* c) {
   template int launch_apply_n<N>(sem_ctx*, int, const double*, double*, int, bool, hipStream_t, \
                                  double*);                                                     \
   template int launch_geom_n<N>(sem_ctx*, const double*, int, double*, double*, double*, double*, \
-                                double*, double*, double2*, const double2*, hipStream_t);        \
+                                double*, double*, double2*, const double2*, hipStream_t,         \
+                                const double*);                                                  \
   template int upload_deo<N>(sem_ctx*);
 
 #if SEM_N_LO <= 2 && 2 <= SEM_N_HI

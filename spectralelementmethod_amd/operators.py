@@ -73,6 +73,41 @@ def _basis_arrays(p, basis, ndim=2):
     return basis, D, w, Vinv
 
 
+def reference_x_phys(nodes, e2n, basis):
+    """x_phys [E, 2, n, n] of every element as the reference computes it:
+    Mapping._compute_x_phys (sem/mapping.py:98-103) calls
+    TensorProduct.compute_coeffs_grid_eq (sem/basis_functions.py:599-624) on
+    the element's equispaced nodes [2, n, n]: LAPACK LU solves with V_eq's
+    factors (sem/basis_functions.py:221-224), first with
+    the n x 2n right-hand side of columns (xi1 index, component), then with
+    the one of columns (xi0 index, component).  The calls are made element by
+    element with exactly those right-hand sides, because the LAPACK/BLAS
+    triangular solves round differently for other batchings (5e-11 at p = 16
+    when all elements go to one call)."""
+    import scipy.linalg as spla
+    sub = basis._subbases[0]
+    # V_eq with the reference's own float64 expression (the barycentric
+    # second form of BarycentricLagrange.__call__, sem/basis_functions.py:
+    # 226-255; the library's C twin can differ in the last bit above p = 10)
+    xn, bw = np.asarray(sub.nodes, dtype=np.float64), np.asarray(sub.bary_wts, dtype=np.float64)
+    x_eq = np.linspace(-1, 1, xn.size)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        kern = bw / (x_eq[:, None] - xn)
+        veq = kern / kern.sum(axis=-1)[:, None]
+    veq[np.isnan(veq)] = 1.0
+    lu = spla.lu_factor(veq)
+    X = np.asarray(nodes)[:, np.asarray(e2n).astype(np.int64)]  # [2, E, n, n]
+    E, n = X.shape[1], X.shape[2]
+    out = np.empty((E, 2, n, n))
+    for e in range(E):
+        v = np.moveaxis(X[:, e], 0, 2)                         # [i, j, c]
+        t = spla.lu_solve(lu, v.reshape(n, 2 * n))             # along xi0
+        t = np.moveaxis(t.reshape(n, n, 2), 0, 1)              # [j, i, c]
+        t = spla.lu_solve(lu, t.reshape(n, 2 * n))             # along xi1
+        out[e] = np.moveaxis(np.moveaxis(t.reshape(n, n, 2), 0, 1), 2, 0)
+    return out
+
+
 class SEMOperator(object):
     """Matrix-free spectral-element operators on one GPU.
 
@@ -97,7 +132,11 @@ class SEMOperator(object):
         traffic) or streamed from precomputed per-element factors ("stored");
         "auto" (default) picks per order (nodal at p = 1, 2, 4, 5, 8: the
         library's measured table).  See include/sem_hip.h
-        sem_set_geom_mode.
+        sem_set_geom_mode.  "reference": stored factors from x_phys computed
+        on the host exactly as the reference does it (LU solves of V_eq,
+        Mapping._compute_x_phys, sem/mapping.py:98-103), so that above p = 10
+        the action carries the reference's own float64 rounding of that
+        ill-conditioned transform; setup only, quadrilaterals.
     kernel : {"auto", "column", "mfma"}
         Kernel family of the Poisson action: the LDS column kernel or the
         fp64 matrix-core element kernel (p <= 15); "auto" (default) resolves
@@ -113,7 +152,7 @@ class SEMOperator(object):
     """
 
     GEOMETRY_MODES = {"stored": _lib.GEOM_STORED, "nodal": _lib.GEOM_NODAL,
-                      "auto": _lib.GEOM_AUTO}
+                      "auto": _lib.GEOM_AUTO, "reference": _lib.GEOM_STORED}
     KERNELS = {"column": _lib.KERNEL_COLUMN, "mfma": _lib.KERNEL_MFMA, "auto": _lib.KERNEL_AUTO}
 
     def __init__(self, p, e2n, nodes, dofs_per_node=1, basis=None, device=None,
@@ -135,7 +174,7 @@ class SEMOperator(object):
             raise ValueError("e2n must have shape [E, %d, %d] or [E, %d, %d, %d]"
                              % ((self.n,) * 5))
         if self.ndim == 3 and (self.dpn != 1 or node_state is not None or
-                               geometry == "nodal" or kernel == "mfma"):
+                               geometry in ("nodal", "reference") or kernel == "mfma"):
             raise NotImplementedError("hexahedral operators: Poisson (dofs_per_node = 1), "
                                       "stored geometry, column kernel, no node states")
         self.basis, self.D, self.w, self.Vinv = _basis_arrays(self.p, basis, self.ndim)
@@ -232,9 +271,17 @@ class SEMOperator(object):
         kind = op_kind(kind)
         bad = C.c_int64(0)
         with torch.cuda.device(self.device):
-            _lib.check(self._lib.sem_geom_from_nodes(self._ctx, _lib.tptr(self.nodes),
-                                                     _lib.dptr(self.Vinv), kind, C.byref(bad),
-                                                     self._stream(stream)))
+            if self.geometry == "reference":
+                xp = torch.from_numpy(reference_x_phys(self.nodes.cpu().numpy(),
+                                                       self.e2n.cpu().numpy().view(np.uint32),
+                                                       self.basis)).to(self.device)
+                _lib.check(self._lib.sem_geom_from_xphys(self._ctx, _lib.tptr(xp), kind,
+                                                         C.byref(bad), self._stream(stream)))
+                torch.cuda.current_stream().synchronize()
+            else:
+                _lib.check(self._lib.sem_geom_from_nodes(self._ctx, _lib.tptr(self.nodes),
+                                                         _lib.dptr(self.Vinv), kind, C.byref(bad),
+                                                         self._stream(stream)))
         self._geom_ready.add(_geom_key(kind))
         return self
 

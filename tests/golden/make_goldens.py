@@ -304,7 +304,7 @@ def gen_poisson_action():
         out[name + "_y"] = y
         out[name + "_p"] = np.array(p)
         print("  action %s ndof=%d |y|=%.6e" % (name, dm.ndof, np.linalg.norm(y)))
-        if name == "p8_8x8w" or name == "p4_4x4":
+        if name in ("p8_8x8w", "p4_4x4", "p12_3x3w", "p16_2x2w"):
             fields = {k: [] for k in ("x_phys", "J", "invJ", "detJ", "detJxW")}
             for fe in dm.finite_elements(x_phys=True, Jacobian=True):
                 fields["x_phys"].append(fe.x_phys)

@@ -148,3 +148,36 @@ def test_config4_device_geometry_vs_extended(gpu, gll, p, nex, kernel, geometry)
                                                   rel_l2(y[loc[inner]], ref[inner])))
     assert e_gpu < TOL, (p, geometry, e_gpu, e_ref)
     assert e_gpu <= e_ref, (p, geometry, e_gpu, e_ref)
+
+
+@pytest.mark.parametrize("name", ["p12_3x3w", "p16_2x2w", "p8_8x8w", "p4_4x4"])
+def test_reference_geometry_golden(gpu, poisson_action, name):
+    """geometry="reference": x_phys by the reference's own per-element LU
+    calls (operators.reference_x_phys, bitwise to FiniteElement.x_phys,
+    sem/finite_elements.py) handed to sem_geom_from_xphys; the action against
+    the reference's golden output."""
+    from spectralelementmethod_amd.operators import SEMOperator
+    p = int(poisson_action[name + "_p"])
+    op = SEMOperator(p, poisson_action[name + "_e2n"], poisson_action[name + "_nodes"],
+                     device=gpu, geometry="reference")
+    y = op.apply(torch.from_numpy(poisson_action[name + "_u"]).to(gpu)).cpu().numpy()
+    assert rel_l2(y, poisson_action[name + "_y"]) < 1e-12
+
+
+@pytest.mark.parametrize("p,nex", [(12, 263), (16, 198)])
+def test_config4_reference_geometry_vs_oracle(gpu, gll, p, nex):
+    """~1e7 DOF at p = 12 / 16 with geometry="reference": against the oracle
+    run with the reference's call pattern (batched_geometry=False, one LU
+    solve per element as sem/finite_elements.py does) at the north-star 1e-10."""
+    import sem_oracle
+    from spectralelementmethod_amd import meshgen
+    from spectralelementmethod_amd.operators import SEMOperator
+    nodes, e2n = meshgen.structured_square(nex, nex, p, warp=0.05)
+    u = np.random.default_rng(p).standard_normal(nodes.shape[1])
+    op = SEMOperator(p, e2n, nodes, device=gpu, geometry="reference")
+    y = op.apply(torch.from_numpy(u).to(gpu)).cpu().numpy()
+    op.close()
+    prob = sem_oracle.PoissonProblem(nodes, e2n, gll["half_%d" % p], batched_geometry=False)
+    e = rel_l2(y, prob.apply(u))
+    print("p=%d %dx%d reference geometry vs call-faithful oracle %.2e" % (p, nex, nex, e))
+    assert e < TOL, (p, e)
