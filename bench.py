@@ -620,6 +620,9 @@ def main():
                     help="rcm: the reference DOFManager's default node order (reverse "
                          "Cuthill-McKee of the element-clique graph, sem/discrete.py:169-178), "
                          "element order unchanged; one GPU, Poisson")
+    ap.add_argument("--renumber", choices=["auto", "off"], default="auto",
+                    help="--op pcg on one GPU: solve in the kernel's traversal numbering "
+                         "when it reads fewer lines (auto) or keep the caller's (off)")
     ap.add_argument("--dim", type=int, choices=[2, 3], default=2,
                     help="3: the hexahedral Poisson action (bench_hex)")
     ap.add_argument("--hex-ne", type=int, default=27, help="--dim 3: hexahedra per side")
@@ -681,13 +684,13 @@ def main():
         if args.numbering == "rcm":
             if world != 1:
                 raise SystemExit("--numbering rcm is single-GPU")
-            from scipy.sparse import csgraph
-            from spectralelementmethod_amd.discrete import _pair_graph
+            from spectralelementmethod_amd.discrete import rcm_permutation
             t0 = time.time()
             # what DOFManager(mesh, ...) does by default (rcm_order=True):
-            # the clique graph of every cell's nodes, scipy RCM, nodes permuted
-            perm = csgraph.reverse_cuthill_mckee(
-                _pair_graph(e2n.reshape(e2n.shape[0], -1), nodes.shape[1]), True)
+            # scipy's RCM of the graph joining every two nodes of a cell
+            # (sem/discrete.py:142-178), walked on the cell map natively
+            # (equal to scipy's permutation, tests/test_order.py)
+            perm = rcm_permutation(e2n.reshape(e2n.shape[0], -1), nodes.shape[1])
             inv = np.empty_like(perm)
             inv[perm] = np.arange(perm.size, dtype=perm.dtype)
             nodes = nodes[:, perm].copy()
@@ -1115,14 +1118,16 @@ def bench_pcg(args, op, part, nodes, dev, world, rank, ndof_global, t_setup):
     rtol = args.pcg_rtol
     iters = args.steps
     # warm-up (also builds the diagonal once per call, included in timing below)
-    op.pcg_solve(b, x.clone(), on, rtol=0.0, max_iter=max(1, args.warmup))
+    ren = "auto" if args.renumber == "auto" else False
+    op.pcg_solve(b, x.clone(), on, rtol=0.0, max_iter=max(1, args.warmup), renumber=ren)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     x_run = x.clone()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    _, its, rel = op.pcg_solve(b, x_run, on, rtol=rtol, max_iter=iters if rtol == 0 else 200000)
+    _, its, rel = op.pcg_solve(b, x_run, on, rtol=rtol, max_iter=iters if rtol == 0 else 200000,
+                               renumber=ren)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -1139,6 +1144,13 @@ def bench_pcg(args, op, part, nodes, dev, world, rank, ndof_global, t_setup):
         dist.all_reduce(t)
         err_num, err_den = t[0], t[1]
     err = float(torch.sqrt(err_num / err_den))
+    solver_numbering = None
+    sop = None if op.dd else op.ops[0]
+    if sop is not None and sop._solver is not None:
+        solver_numbering = {"row_lines_gain": sop.solver_gain,
+                            "renumbered": sop._solver[0] is not None,
+                            "rule": "traversal numbering when the caller's numbering reads "
+                                    ">= 1.3x the 64-byte lines per wavefront row"}
     result = {
         "metric": "assembled Poisson Jacobi-PCG, DOF-iterations/s, p=%d" % args.p,
         "value": ndof_global * its / elapsed, "unit": "DOF*iterations/s", "n_gpus": world,
@@ -1148,10 +1160,12 @@ def bench_pcg(args, op, part, nodes, dev, world, rank, ndof_global, t_setup):
         "config": {"workload": "pcg p=%d, %dx%d elements (%s)" % (
             args.p, args.nex, args.ney, "fixed iterations" if rtol == 0 else
             "solve to rtol %g" % rtol), "ndof_global": ndof_global, "ranks_seen": world,
+            "numbering": args.numbering,
             "transport": op.transport},
         "pcg": {"iterations": its, "iterations_per_s": its / elapsed, "seconds": elapsed,
                 "final_relres": rel, "rel_l2_error_vs_manufactured": err,
-                "check_every": 16, "gpu_setup_sec": t_setup},
+                "check_every": 16, "gpu_setup_sec": t_setup,
+                "solver_numbering": solver_numbering},
     }
     if rank == 0:
         print(json.dumps(result), file=JSON_OUT, flush=True)

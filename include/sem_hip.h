@@ -83,6 +83,23 @@ int sem_interp_eq_matrix(int n, const double* h_nodes, const double* h_bary,
 double sem_legeval(double x, unsigned n);
 double sem_barycentric_lagrange(const double* h_f, unsigned n, double x);
 
+/* Node orderings of a cell-node map (host, no device): the reverse
+ * Cuthill-McKee renumbering of DOFManager(mesh, rcm_order=True)
+ * (sem/discrete.py:169-178 -> scipy.sparse.csgraph.reverse_cuthill_mckee on
+ * the graph joining every two nodes of a cell, sem/discrete.py:142-167), run
+ * on the cell map itself instead of materialising that graph (5.5e9 entries
+ * at 1024^2 cells, p = 8).  h_cells: [n_cells][nloc] node ids.
+ *   sem_node_degrees: scipy's degree of each node (row length + 1 for the
+ *     diagonal; 0 for a node no cell references);
+ *   sem_cuthill_mckee: Cuthill-McKee order (h_order[k] = k-th node) from
+ *     h_seeds = argsort(degree) (the caller's sort, so ties follow numpy);
+ *     RCM is h_order reversed.  Equal to scipy's on the same graph
+ *     (tests/test_order.py). */
+int sem_node_degrees(const uint32_t* h_cells, int64_t n_cells, int nloc, int64_t n_node,
+                     int32_t* h_degree);
+int sem_cuthill_mckee(const uint32_t* h_cells, int64_t n_cells, int nloc, int64_t n_node,
+                      const int32_t* h_degree, const int64_t* h_seeds, int64_t* h_order);
+
 /* ------------------------------------------------------------------ */
 /* Operator context (one per GPU)                                      */
 /* ------------------------------------------------------------------ */

@@ -12,7 +12,8 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_NAME = "libsem_hip.so"
 LIB_PATH = os.environ.get("SEM_LIB_PATH", os.path.join(PKG_DIR, LIB_NAME))
-SOURCES = ["sem_device.hip", "sem_dd.hip", "sem_sc.hip", "sem_basis.cpp", "sem_hex.hip"]
+SOURCES = ["sem_device.hip", "sem_dd.hip", "sem_sc.hip", "sem_basis.cpp", "sem_hex.hip",
+           "sem_order.cpp"]
 # (lo, hi) order ranges of sem_launch.hip, balanced by compile time (the
 # unrolled column kernels grow with n)
 LAUNCH_RANGES = [(2, 5), (6, 8), (9, 9), (10, 11), (12, 13), (14, 15), (16, 16), (17, 17)]

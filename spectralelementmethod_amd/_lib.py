@@ -51,6 +51,8 @@ SIGNATURES = {
     "sem_interp_eq_matrix": (C.c_int, [C.c_int, _dp, _dp, _dp, _dp]),
     "sem_legeval": (C.c_double, [C.c_double, C.c_uint]),
     "sem_barycentric_lagrange": (C.c_double, [_dp, C.c_uint, C.c_double]),
+    "sem_node_degrees": (C.c_int, [_vp, _i64, C.c_int, _i64, _vp]),
+    "sem_cuthill_mckee": (C.c_int, [_vp, _i64, C.c_int, _i64, _vp, _vp, _vp]),
     "sem_ctx_create": (C.c_int, [C.POINTER(_vp), C.c_int, _i64, _i64, C.c_int, C.c_int]),
     "sem_ctx_create_nd": (C.c_int, [C.POINTER(_vp), C.c_int, C.c_int, _i64, _i64, C.c_int,
                                     C.c_int]),

@@ -28,7 +28,6 @@ from collections import namedtuple
 
 import numpy as np
 from scipy import sparse
-from scipy.sparse import csgraph
 
 from .geometry import Quadrilateral
 from .mapping import Mapping, OutsideDomain  # noqa: F401
@@ -338,6 +337,30 @@ def _pair_graph(maps, n):
     return g.tocsr()
 
 
+def rcm_permutation(maps, n):
+    """scipy.sparse.csgraph.reverse_cuthill_mckee(_pair_graph(maps, n), True)
+    without the pair graph (sem_node_degrees / sem_cuthill_mckee in
+    libsem_hip.so walk the cell map; the graph has sum_cells nloc^2 entries
+    and no longer fits a host at 1024^2 cells of order 8).  Degree ties are
+    broken by numpy's argsort, as scipy does; equal to scipy's permutation
+    (tests/test_order.py)."""
+    import ctypes as C
+    from . import _lib
+    lib = _lib.load()
+    cells = np.ascontiguousarray(maps, dtype=np.uint32)
+    E, k = cells.shape
+    deg = np.empty(n, dtype=np.int32)
+    _lib.check(lib.sem_node_degrees(cells.ctypes.data_as(C.c_void_p), E, k, n,
+                                    deg.ctypes.data_as(C.c_void_p)))
+    seeds = np.argsort(deg).astype(np.int64)
+    order = np.empty(n, dtype=np.int64)
+    _lib.check(lib.sem_cuthill_mckee(cells.ctypes.data_as(C.c_void_p), E, k, n,
+                                     deg.ctypes.data_as(C.c_void_p),
+                                     seeds.ctypes.data_as(C.c_void_p),
+                                     order.ctypes.data_as(C.c_void_p)))
+    return order[::-1].astype(np.int32)
+
+
 class DOFManager(object):
     """Degrees of freedom on a mesh (sem/discrete.py:44-280) plus the
     batched device operator path."""
@@ -389,9 +412,11 @@ class DOFManager(object):
         return _pair_graph(e2n.reshape(e2n.shape[0], -1), self._mesh.n_nodes)
 
     def _reorder_nodes_rcm(self):
-        """Reverse Cuthill-McKee node order (sem/discrete.py:169-178)."""
-        perm = csgraph.reverse_cuthill_mckee(self._get_connectivity_graph(), True)
-        self._mesh._permute_nodes(perm)
+        """Reverse Cuthill-McKee node order (sem/discrete.py:169-178), the
+        graph walked on the cell map natively (rcm_permutation)."""
+        e2n = self._mesh.element_map()
+        self._mesh._permute_nodes(rcm_permutation(e2n.reshape(e2n.shape[0], -1),
+                                                  self._mesh.n_nodes))
 
     # ------------------------------------------------------------------ device
     def operator(self):
@@ -560,7 +585,10 @@ class DOFManagerSC(DOFManager):
         mesh = self._mesh
         n_ext = mesh.n_nodes_cell_exterior
         perm = np.empty(mesh.n_nodes, np.uint32)
-        perm[:n_ext] = csgraph.reverse_cuthill_mckee(self._get_connectivity_graph(), True)
+        e2n = mesh.element_map()
+        geo = mesh._geometries[mesh._geom_ids[0]]
+        perm[:n_ext] = rcm_permutation(e2n.reshape(e2n.shape[0], -1)[:, geo.exterior_node_ind],
+                                       n_ext)
         perm[n_ext:] = np.arange(n_ext, mesh.n_nodes)
         mesh._permute_nodes(perm)
 

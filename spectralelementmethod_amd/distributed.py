@@ -645,10 +645,12 @@ class OverlappedOperator(object):
         return d
 
     def pcg_solve(self, rhs, x, dirichlet, rtol=1e-13, max_iter=20000,
-                  check_every=_lib.PCG_CHECK_EVERY):
+                  check_every=_lib.PCG_CHECK_EVERY, renumber="auto"):
         """Jacobi-PCG for K x = rhs on this rank's DOFs (dirichlet: bool mask;
         x holds the Dirichlet values and the initial guess, updated in place).
-        Returns (x, iterations executed, final relative residual)."""
+        Returns (x, iterations executed, final relative residual).  One rank
+        without the decomposition: SEMOperator.pcg_solve (renumber: its
+        solver numbering)."""
         if self.dd and self.world > 1 and self.plan.not_owned is None:
             # every rank would count its copies of the shared DOFs in the
             # global dot products: a wrong inner product, silently
@@ -661,9 +663,10 @@ class OverlappedOperator(object):
                 self.dd, self.kind, _lib.tptr(rhs), _lib.tptr(x), _lib.tptr(mask), float(rtol),
                 int(max_iter), int(check_every), C.byref(its), C.byref(rel), sp))
         else:
-            _lib.check(self._lib.sem_pcg_solve(self.ops[0]._ctx, self.kind, _lib.tptr(rhs),
-                                               _lib.tptr(x), _lib.tptr(mask), float(rtol),
-                                               int(max_iter), C.byref(its), C.byref(rel), sp))
+            return self.ops[0].pcg_solve(rhs, x, dirichlet, rtol=rtol, max_iter=max_iter,
+                                         kind=self.kind,
+                                         stream=torch.cuda.current_stream(self.device),
+                                         renumber=renumber)
         return x, its.value, rel.value
 
 

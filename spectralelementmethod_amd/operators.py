@@ -162,6 +162,10 @@ class SEMOperator(object):
         if kernel not in self.KERNELS:
             raise ValueError("kernel must be one of %s" % sorted(self.KERNELS))
         self.geometry = geometry
+        self.kernel = kernel
+        self._shared = node_state is not None
+        self._user_geom = False
+        self._solver = None  # (operator in the solver numbering | None, order, inverse)
         self._lib = _lib.load()
         self.p = int(p)
         self.n = self.p + 1
@@ -223,6 +227,9 @@ class SEMOperator(object):
 
     # ------------------------------------------------------------------
     def close(self):
+        if getattr(self, "_solver", None) and self._solver[0] is not None:
+            self._solver[0].close()
+        self._solver = None
         if getattr(self, "_ctx", None):
             self._lib.sem_ctx_destroy(self._ctx)
             self._ctx = None
@@ -298,6 +305,10 @@ class SEMOperator(object):
             _lib.check(self._lib.sem_set_geom(self._ctx, _lib.tptr(G), kind, self._stream(stream)))
             torch.cuda.current_stream().synchronize()
         self._geom_ready.add(_geom_key(kind))
+        self._user_geom = True
+        if self._solver is not None and self._solver[0] is not None:
+            self._solver[0].close()
+        self._solver = None
         return self
 
     def geometry_fields(self, stream=None):
@@ -336,12 +347,32 @@ class SEMOperator(object):
         _lib.check(self._lib.sem_set_reynolds(self._ctx, float(re)))
         return self
 
-    def apply(self, u, out=None, kind=POISSON, accumulate=False, stream=None, linearize=False):
+    def apply(self, u, out=None, kind=POISSON, accumulate=False, stream=None, linearize=False,
+              renumber=False):
         """out (=|+=) K u for all elements in one launch (device tensors).
         kind "axisym_ns": the Re > 0 residual at the state u = (psi, omega);
         with linearize=True the Newton linearisation at u is recorded for
-        kind "axisym_ns_jvp" (Jacobian times the direction u)."""
+        kind "axisym_ns_jvp" (Jacobian times the direction u).  renumber
+        (Poisson, "auto" / True): run the action on the solver numbering's
+        context, u gathered in and out gathered back (sem_gather, 2 x 20 B
+        per DOF; see row_lines)."""
         kind = op_kind(kind)
+        solver = self._solver_numbering(renumber) if (renumber and kind == POISSON) else None
+        if solver is not None:
+            if accumulate or linearize:
+                raise NotImplementedError("apply(renumber=...) with accumulate / linearize")
+            op, order, inv = solver
+            is_np = not isinstance(u, torch.Tensor)
+            u = self._vec(u, "u")
+            out = torch.empty_like(u) if out is None else out
+            if getattr(self, "_rn_buf", None) is None:
+                self._rn_buf = (torch.empty_like(u), torch.empty_like(u))
+            ui, yi = self._rn_buf
+            with torch.cuda.device(self.device):
+                self._gather(u, order, stream, out=ui)
+                op.apply(ui, out=yi, stream=stream)
+                self._gather(yi, inv, stream, out=out)
+            return out.cpu().numpy() if is_np else out
         if _geom_key(kind) not in self._geom_ready:
             self.compute_geometry(kind, stream=stream)
         is_np = not isinstance(u, torch.Tensor)
@@ -408,15 +439,117 @@ class SEMOperator(object):
             _lib.check(self._lib.sem_diag(self._ctx, kind, _lib.tptr(d), self._stream(stream)))
         return d
 
+    # ------------------------------------------------------------------
+    # Solver numbering.  The column kernel's gathers and stores are fast when
+    # the 7-9 elements of a wavefront read each node row from a few 64-byte
+    # lines (57 consecutive ids at p = 8 on a lexicographic mesh).  The
+    # reference's default numbering (DOFManager rcm_order=True) spreads a row
+    # over ~17 lines and the action runs at 0.64x (profiles/r05/rcm/).  A
+    # solve keeps its vectors for hundreds of actions, so pcg_solve may run on
+    # a second context whose nodes are numbered in the kernel's own traversal
+    # order, permuting rhs / x / mask once on entry and x once on exit
+    # (sem_gather).  A single apply() would pay two permutations (2 x 20 B
+    # per DOF) for a 0.36x gain and stays on the caller's numbering.
+    def row_lines(self, e2n=None):
+        """Mean count of 64-byte lines one wavefront row gather touches (the
+        plan's groups of consecutive elements, lanes = (element, column))."""
+        m = (self.e2n.cpu().numpy().view(np.uint32) if e2n is None else e2n).astype(np.int64)
+        epw = max(1, self.plan_info().get("elements_per_group", 1))
+        E = m.shape[0] // epw * epw
+        if E == 0:
+            return 0.0
+        g = m[:E].reshape(-1, epw, self.n, self.n)
+        tot = 0
+        for r in range(self.n):
+            x = np.sort(g[:, :, r, :].reshape(g.shape[0], -1) * self.dpn // 8, axis=1)
+            tot += int((np.diff(x, axis=1) != 0).sum()) + x.shape[0]
+        return tot / (g.shape[0] * self.n)
+
+    def traversal_order(self):
+        """Node numbering in the column kernel's traversal order: first touch
+        over (group of consecutive elements, row, lane).  Returns order
+        (order[k] = caller node of solver node k) and its inverse."""
+        m = self.e2n.cpu().numpy().view(np.uint32).astype(np.int64)
+        epw = max(1, self.plan_info().get("elements_per_group", 1))
+        E = m.shape[0]
+        G = -(-E // epw)
+        g = np.full((G * epw, self.n, self.n), -1, dtype=np.int64)
+        g[:E] = m
+        seq = g.reshape(G, epw, self.n, self.n).transpose(0, 2, 1, 3).reshape(-1)
+        seq = seq[seq >= 0]
+        _, first = np.unique(seq, return_index=True)
+        touched = seq[np.sort(first)]
+        rest = np.setdiff1d(np.arange(self.n_node), touched, assume_unique=True)
+        order = np.concatenate([touched, rest])
+        inv = np.empty(self.n_node, dtype=np.int64)
+        inv[order] = np.arange(self.n_node)
+        return order, inv
+
+    def _solver_numbering(self, renumber):
+        """(operator in the traversal numbering, order, inverse) as device
+        uint32 index tensors, or None when the caller's numbering is kept."""
+        force = renumber is True or renumber == "on"
+        if renumber is False or renumber == "off":
+            return None
+        if not (self.ndim == 2 and self.dpn == 1 and not self._shared and not self._user_geom):
+            if force:
+                raise NotImplementedError("solver renumbering: 2-D Poisson operators with "
+                                          "library geometry and no node states")
+            return None
+        if self._solver is None:
+            order, inv = self.traversal_order()
+            m = self.e2n.cpu().numpy().view(np.uint32).astype(np.int64)
+            self.solver_gain = self.row_lines(m) / max(self.row_lines(inv[m]), 1e-9)
+            self._solver = (None, order, inv)
+        op, order, inv = self._solver
+        if op is None:
+            if self.solver_gain < 1.3 and not force:
+                return None
+            m = self.e2n.cpu().numpy().view(np.uint32).astype(np.int64)
+            op = SEMOperator(self.p, inv[m].astype(np.uint32), self.nodes.cpu().numpy()[:, order],
+                             basis=self.basis, device=self.device, geometry=self.geometry,
+                             kernel=self.kernel)
+            self._solver = (op, torch.from_numpy(order.astype(np.uint32)).to(self.device),
+                            torch.from_numpy(inv.astype(np.uint32)).to(self.device))
+        return self._solver
+
+    def _gather(self, src, idx, stream, out=None):
+        """out[k] = src[idx[k]] (sem_gather)."""
+        out = torch.empty_like(src) if out is None else out
+        _lib.check(self._lib.sem_gather(_lib.tptr(src), _lib.tptr(idx), src.numel(),
+                                        _lib.tptr(out), self._stream(stream)))
+        return out
+
     def pcg_solve(self, rhs, x, dirichlet, rtol=1e-13, max_iter=20000, kind=POISSON,
-                  stream=None):
+                  stream=None, renumber="auto"):
         """Solve K x = rhs on the free DOFs (``dirichlet`` True => x fixed)
         with Jacobi-preconditioned CG on the device (sem_pcg_solve: every
         scalar stays on the device, convergence read every 16 iterations;
         rtol = 0 runs exactly max_iter iterations).  ``x`` (device tensor) is
         updated in place and returned with (iterations executed, relative
-        residual).  Raises ValueError when not converged."""
+        residual).  Raises ValueError when not converged.  renumber: "auto"
+        solves in the kernel's traversal numbering when the caller's
+        numbering reads >= 1.3x the 64-byte lines per row (row_lines; e.g.
+        the reference's RCM default), True forces it, False never."""
         kind = op_kind(kind)
+        solver = self._solver_numbering(renumber) if kind == POISSON else None
+        if solver is not None:
+            op, order, inv = solver
+            rhs = self._vec(rhs, "rhs")
+            if not isinstance(x, torch.Tensor) or x.device != self.device:
+                raise TypeError("x must be a device tensor on %s" % self.device)
+            x = self._vec(x, "x")
+            mask = torch.as_tensor(dirichlet, dtype=torch.float64).to(self.device)
+            if mask.numel() != self.ndof:
+                raise ValueError("dirichlet mask must have ndof entries")
+            with torch.cuda.device(self.device):
+                xi = self._gather(x, order, stream)
+                _, its, rel = op.pcg_solve(self._gather(rhs, order, stream), xi,
+                                           self._gather(mask, order, stream) != 0, rtol=rtol,
+                                           max_iter=max_iter, kind=kind, stream=stream,
+                                           renumber=False)
+                self._gather(xi, inv, stream, out=x)
+            return x, its, rel
         if _geom_key(kind) not in self._geom_ready:
             self.compute_geometry(kind, stream=stream)
         rhs = self._vec(rhs, "rhs")
