@@ -611,6 +611,10 @@ def main():
                     help="diagnostic: time rank R of the --gpus N strip decomposition ALONE on "
                          "this GPU (loopback transport: the exchange returns the rank's own "
                          "values; kernels, streams and host enqueue of the real step)")
+    ap.add_argument("--time-rank-transport", choices=["loopback", "rccl_self"],
+                    default="rccl_self",
+                    help="--time-rank: the exchange as RCCL send/recv to this rank itself on a "
+                         "one-rank communicator (default) or the loopback copy kernel")
     ap.add_argument("--dump-interface", default=None, metavar="DIR",
                     help="test hook: every rank writes y at its interface node lines (global "
                          "ids, values) to DIR/iface_rank<r>.npz after the timed steps")
@@ -951,9 +955,12 @@ def main():
 
 def time_rank(args):
     """One rank of the N-strip decomposition of the nex x ney mesh, alone on
-    this GPU (sem_dd_set_loopback: every exchange copies the rank's own send
-    buffer into its receive buffer -- the kernels, streams and host enqueue of
-    the real step, the values are NOT the global action).  Reports the step
+    this GPU.  --time-rank-transport rccl_self (default, sem_dd_set_rccl_self):
+    every exchange is RCCL send/recv per peer addressed to this rank itself on
+    a one-rank communicator -- RCCL's host enqueue and side-stream work in the
+    real step; loopback (sem_dd_set_loopback): a copy kernel in their place.
+    The kernels, streams and host enqueue are those of the real step, the
+    values are NOT the global action.  Reports the step
     (wall clock and HIP events on the caller's stream), the interior elements
     alone, the side-stream chain alone (gather, interface elements, pack),
     the exposed time of the side stream and the finish, the host enqueue split
@@ -965,12 +972,17 @@ def time_rank(args):
     N, R, p = args.gpus, args.time_rank, args.p
     if not (0 <= R < N):
         raise SystemExit("--time-rank needs 0 <= R < --gpus")
+    # keep stdout for the one JSON line: RCCL prints its banner on file
+    # descriptor 1 from C++ when the communicator is created (to stderr instead)
+    global JSON_OUT
+    JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     part = StripPartition(args.nex, args.ney, p, N, R)
     nodes, e2n = part.local_mesh(args.warp)
     op = OverlappedOperator(p, nodes, e2n, part.neighbors, 1, dev, owned=part.owned,
-                            transport="loopback", world=1, rank=0, decompose=True)
+                            transport=args.time_rank_transport, world=1, rank=0, decompose=True)
     del nodes, e2n
     u = global_random_field(part, 1, 0, op.ndof, dev)
     y = torch.empty_like(u)
@@ -1052,8 +1064,9 @@ def time_rank(args):
         op1.close()
     step_ms = step["wall_ms_per_step"]
     res = {
-        "mode": "time-rank (loopback transport: the exchange returns this rank's own values; "
-                "timing only, the result is NOT the global action)",
+        "mode": "time-rank (%s transport: the exchange returns this rank's own values; "
+                "timing only, the result is NOT the global action)" % args.time_rank_transport,
+        "transport": args.time_rank_transport,
         "rank": R, "of_ranks": N, "p": p, "mesh": "%dx%d" % (args.nex, args.ney),
         "strip_elements": "%d x %d" % (part.ex1 - part.ex0, part.ney), "ndof_rank": ndof,
         "peers": sorted(part.neighbors), "interface_elements": iface_elems,

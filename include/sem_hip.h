@@ -477,6 +477,15 @@ int sem_dd_set_transport(sem_dd* dd, sem_exchange_fn exchange, sem_allreduce_fn 
  * global action. */
 int sem_dd_set_loopback(sem_dd* dd);
 
+/* Transport, timing: RCCL on a one-rank communicator of this process, every
+ * exchange a ncclSend / ncclRecv pair per peer addressed to this rank itself
+ * inside one group on the side stream (RCCL's own host enqueue, proxy and
+ * copy kernels in place of the loopback kernel), all-reduces over one rank.
+ * Like sem_dd_set_loopback it times ONE rank of a decomposition alone
+ * (bench.py --time-rank --time-rank-transport rccl_self); values NOT the
+ * global action.  sem_dd_info [4] = 4. */
+int sem_dd_set_rccl_self(sem_dd* dd);
+
 /* hipMemcpyAsync(dst, src, nbytes, hipMemcpyDefault, stream): lets a
  * caller-supplied transport stage the library's device buffers. */
 int sem_copy_async(void* dst, const void* src, int64_t nbytes, void* stream);

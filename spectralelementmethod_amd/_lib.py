@@ -95,6 +95,7 @@ SIGNATURES = {
     "sem_dd_init_rccl": (C.c_int, [_vp, _vp, C.c_int, C.c_int]),
     "sem_dd_set_transport": (C.c_int, [_vp, _vp, _vp, _vp, C.c_int, C.c_int]),
     "sem_dd_set_loopback": (C.c_int, [_vp]),
+    "sem_dd_set_rccl_self": (C.c_int, [_vp]),
     "sem_dd_info": (C.c_int, [_vp, C.POINTER(_i64), C.c_int]),
     "sem_dd_set_graphs": (C.c_int, [_vp, C.c_int]),
     "sem_dd_apply": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp]),

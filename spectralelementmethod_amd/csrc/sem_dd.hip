@@ -492,6 +492,8 @@ struct sem_dd {
   int64_t n_rest = 0;
   uint64_t fin_epoch = ~0ull;
   bool loopback = false;        // diagnostic transport (sem_dd_set_loopback)
+  bool rccl_self = false;       // timing transport: RCCL send/recv to this rank itself
+                                // on a one-rank communicator (sem_dd_set_rccl_self)
   hipStream_t side = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // transport: native RCCL communicator, or caller callbacks
@@ -727,8 +729,9 @@ int dd_exchange_impl(sem_dd* d) {
     NCCL_TRY(ncclGroupStart());
     for (int k = 0; k < np; ++k) {
       const size_t cnt = (size_t)(d->off[k + 1] - d->off[k]);
-      NCCL_TRY(ncclSend(d->d_send + d->off[k], cnt, ncclFloat64, d->peer[k], d->comm, d->side));
-      NCCL_TRY(ncclRecv(d->d_recv + d->off[k], cnt, ncclFloat64, d->peer[k], d->comm, d->side));
+      const int peer = d->rccl_self ? 0 : d->peer[k];
+      NCCL_TRY(ncclSend(d->d_send + d->off[k], cnt, ncclFloat64, peer, d->comm, d->side));
+      NCCL_TRY(ncclRecv(d->d_recv + d->off[k], cnt, ncclFloat64, peer, d->comm, d->side));
     }
     NCCL_TRY(ncclGroupEnd());
     return SEM_OK;
@@ -1219,8 +1222,28 @@ int sem_dd_init_rccl(sem_dd* d, const void* h_id, int world, int rank) {
   if (d->comm) (void)ncclCommDestroy(d->comm);
   d->comm = comm;
   d->loopback = false;
+  d->rccl_self = false;
   d->world = world;
   d->rank = rank;
+  return SEM_OK;
+}
+
+int sem_dd_set_rccl_self(sem_dd* d) {
+  if (!d) return fail(SEM_E_INVALID, "null dd");
+  DeviceGuard g(d->device);
+  ncclUniqueId id;
+  NCCL_TRY(ncclGetUniqueId(&id));
+  ncclComm_t comm = nullptr;
+  NCCL_TRY(ncclCommInitRank(&comm, 1, id, 0));
+  if (d->comm) (void)ncclCommDestroy(d->comm);
+  d->comm = comm;
+  d->xfn = nullptr;
+  d->rfn = nullptr;
+  d->user = nullptr;
+  d->world = 1;
+  d->rank = 0;
+  d->loopback = false;
+  d->rccl_self = true;
   return SEM_OK;
 }
 
@@ -1237,6 +1260,7 @@ int sem_dd_set_loopback(sem_dd* d) {
   d->world = 1;
   d->rank = 0;
   d->loopback = true;
+  d->rccl_self = false;
   return SEM_OK;
 }
 
@@ -1245,6 +1269,7 @@ int sem_dd_set_transport(sem_dd* d, sem_exchange_fn xfn, sem_allreduce_fn rfn, v
   if (!d || world < 1 || rank < 0 || rank >= world)
     return fail(SEM_E_INVALID, "sem_dd_set_transport: bad arguments");
   d->loopback = false;
+  d->rccl_self = false;
   d->xfn = xfn;
   d->rfn = rfn;
   d->user = user;
@@ -1261,7 +1286,8 @@ int sem_dd_set_transport(sem_dd* d, sem_exchange_fn xfn, sem_allreduce_fn rfn, v
 int sem_dd_info(sem_dd* d, int64_t* info, int n_info) {
   if (!d || !info || n_info < 1) return fail(SEM_E_INVALID, "bad arguments");
   const int64_t v[16] = {d->ndof, d->nc, (int64_t)d->peer.size(), n_exchanged(d),
-                         d->loopback ? 3 : d->comm ? 1 : (d->xfn ? 2 : 0), d->interior ? 1 : 0,
+                         d->loopback ? 3 : d->rccl_self ? 4 : d->comm ? 1 : (d->xfn ? 2 : 0),
+                         d->interior ? 1 : 0,
                          d->graphs ? 1 : 0, d->n_captures, d->n_replays,
                          d->host_steps, d->host_ns, d->host_ns_transport,
                          d->host_ns_side, d->host_ns_main, d->host_ns_finish,

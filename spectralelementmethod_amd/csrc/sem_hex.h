@@ -127,8 +127,8 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
   // holds the same nodes in the same (a, b) order (the planner checked every
   // chain step); the merged node then has one writer fewer
   const bool give = (cf & 4) && c == 0;
-  const bool take = active && c == N - 1 && s + 1 < S && (P.cflag[w * S + s + 1] & 4);
-  bool wg_merge = false;
+  [[maybe_unused]] const bool take = active && c == N - 1 && s + 1 < S && (P.cflag[w * S + s + 1] & 4);
+  [[maybe_unused]] bool wg_merge = false;
 #if SEM_HEX_ZMERGE
 #pragma unroll
   for (int t = 1; t < S; ++t) wg_merge |= (P.cflag[w * S + t] & 4) != 0;

@@ -546,12 +546,17 @@ class OverlappedOperator(object):
 
     def _install_transport(self, transport, group):
         backend = str(dist.get_backend(group)).lower() if dist.is_initialized() else ""
-        if transport not in ("auto", "rccl", "torch", "loopback"):
-            raise ValueError("transport must be auto, rccl, torch or loopback")
+        if transport not in ("auto", "rccl", "torch", "loopback", "rccl_self"):
+            raise ValueError("transport must be auto, rccl, torch, loopback or rccl_self")
         if transport == "loopback":  # diagnostic: one rank timed alone (sem_dd_set_loopback)
             _lib.check(self._lib.sem_dd_set_loopback(self.dd))
             self.world, self.rank = 1, 0
             self.transport = "loopback"
+            return
+        if transport == "rccl_self":  # timing: RCCL send/recv to self (sem_dd_set_rccl_self)
+            _lib.check(self._lib.sem_dd_set_rccl_self(self.dd))
+            self.world, self.rank = 1, 0
+            self.transport = "rccl_self"
             return
         if transport == "rccl" or (transport == "auto" and "nccl" in backend):
             try:
@@ -596,7 +601,7 @@ class OverlappedOperator(object):
         _lib.check(self._lib.sem_dd_info(self.dd, v, 16))
         steps = max(1, v[9])
         return dict(ndof=v[0], iface_dofs=v[1], peers=v[2], exchanged=v[3],
-                    transport=("none", "rccl", "callbacks", "loopback")[v[4]],
+                    transport=("none", "rccl", "callbacks", "loopback", "rccl_self")[v[4]],
                     interior=bool(v[5]), graphs=bool(v[6]), captures=v[7], replays=v[8],
                     applies=v[9], host_ns=v[10], host_ns_transport=v[11],
                     host_us_per_apply=v[10] / steps / 1e3,

@@ -93,13 +93,16 @@ def test_cfg3_eight_strips_on_one_gpu(gpu, tmp_path):
 
 
 @pytest.mark.timeout(600)
-def test_time_rank_loopback(gpu):
-    """One interior rank (two peers) of the 8-strip split timed alone; the
-    values are meaningless by construction, the structure of the report is
-    what is checked here (the numbers are measured by the GPU calls and kept
-    under profiles/)."""
-    res, _ = _bench(["--gpus", "8", "--time-rank", "3", "--steps", "10", "--warmup", "3"],
-                    timeout=500)
+@pytest.mark.parametrize("transport", ["rccl_self", "loopback"])
+def test_time_rank(gpu, transport):
+    """One interior rank (two peers) of the 8-strip split timed alone, the
+    exchange as RCCL send/recv to itself or the loopback copy; the values are
+    meaningless by construction, the structure of the report is what is
+    checked here (the numbers are measured by the GPU calls and kept under
+    profiles/)."""
+    res, _ = _bench(["--gpus", "8", "--time-rank", "3", "--steps", "10", "--warmup", "3",
+                     "--time-rank-transport", transport], timeout=500)
+    assert res["transport"] == transport
     assert res["rank"] == 3 and res["of_ranks"] == 8 and res["peers"] == [2, 4]
     assert res["strip_elements"] == "128 x 1024"
     for k in ("step", "interior_alone", "side_chain_alone", "single_gpu_whole_mesh"):

@@ -198,3 +198,25 @@ def test_dd_fused_seam_finish_is_bitwise(gpu, monkeypatch, rank):
         op.close()
     assert out["1"][1]["seam_sum_in_finish"] and not out["0"][1]["seam_sum_in_finish"]
     assert torch.equal(out["1"][0], out["0"][0])
+
+
+def test_dd_rccl_self_transport_equals_loopback(gpu):
+    """The timing transport over RCCL (sem_dd_set_rccl_self: send/recv per
+    peer to this rank itself on a one-rank communicator, on the side stream)
+    moves the same bytes as the loopback copy: bitwise the same step."""
+    from spectralelementmethod_amd.distributed import OverlappedOperator, StripPartition
+    part = StripPartition(24, 112, 8, 4, 1)
+    nodes, e2n = part.local_mesh(0.05)
+    u = torch.from_numpy(np.random.default_rng(6).standard_normal(nodes.shape[1])).to(gpu)
+    out = {}
+    for tr in ("loopback", "rccl_self"):
+        op = OverlappedOperator(8, nodes, e2n, part.neighbors, 1, gpu, owned=part.owned,
+                                transport=tr, world=1, rank=0, decompose=True)
+        assert op.transport == tr and op.dd_info()["transport"] == tr
+        y = torch.full_like(u, 7.0)
+        for _ in range(3):
+            op.step(u, y)
+        torch.cuda.synchronize()
+        out[tr] = y.clone()
+        op.close()
+    assert torch.equal(out["loopback"], out["rccl_self"])
