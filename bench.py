@@ -345,9 +345,11 @@ def bench_hex(args):
     B = alg_bytes_hex(n_nodes, E, p)
     F = alg_flops_hex(E, p)
     achieved = B / kern_avg_s / 1e9
-    traffic = None
-    if args.traffic_json and os.path.exists(args.traffic_json):
-        with open(args.traffic_json) as f:
+    traffic, traffic_src = None, args.traffic_json
+    if traffic_src is None and (p, ne) == (8, 27):  # profiles/r05/hex/pmc/
+        traffic_src = os.path.join(ROOT, "bench_traffic", "pmc_traffic_hex_p8_27.json")
+    if traffic_src and os.path.exists(traffic_src):
+        with open(traffic_src) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
     result = {
         "metric": METRIC.replace("Poisson p=8", "Poisson p=%d on hexahedra" % p),
@@ -370,6 +372,7 @@ def bench_hex(args):
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "traffic_source": os.path.relpath(traffic_src, ROOT) if traffic is not None else None,
             "bytes_model": "16*ndof + 52*E*(p+1)^3 (u, y, 6 factors + uint32 map per element node)",
             "alg_bytes_per_launch": B, "kernel": "k_hex_poisson<%d,0> + k_hex_seam_sum" % (p + 1),
             "fp64_tflops": F / kern_avg_s / 1e12, "fp64_peak_tflops": FP64_PEAK_TFLOPS,
