@@ -63,7 +63,10 @@ struct HexLaunch {
 enum { HEX_SET = 0, HEX_ACC = 1, HEX_DIAG = 2 };
 
 // z-merge (xi2 faces between the slots of a workgroup summed in LDS): off by
-// default -- its exchange buffer pushes n = 9 past three workgroups per CU
+// default -- at n = 9 its exchange buffer (1.3 KB) takes the workgroup past
+// 54,272 bytes, the most that three 512-byte-granular allocations fit in the
+// 160 KB of a CU; measured with it on (profiles/r05/hex/): seam sum 47 -> 33
+// us, element kernel 225 -> 241 us at two workgroups per CU
 #ifndef SEM_HEX_ZMERGE
 #define SEM_HEX_ZMERGE 0
 #endif
@@ -106,7 +109,10 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
   __shared__ double sA[S * N3];
   __shared__ double sB[S * N3];
 #if SEM_HEX_ZMERGE
-  __shared__ double sX[S * N2];  // z-merge: xi2 = 0 face columns handed to slot s-1
+  // z-merge: the xi2 = 0 face of slot s (s >= 1) handed to slot s-1; slot 0
+  // never gives, so S-1 faces (n = 9: 1.3 KB, 54,456 bytes in all -- one
+  // 512-byte granule past three workgroups per CU)
+  __shared__ double sX[S > 1 ? (S - 1) * N2 : 1];
 #endif
   const int tid = threadIdx.x;
   for (int i = tid; i < N2; i += T) sD[i] = gD[i];
@@ -269,11 +275,11 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
     if (wg_merge) {  // workgroup-uniform
       if (give)
 #pragma unroll
-        for (int a = 0; a < N; ++a) sX[sl * N2 + a * N + b] = yv[a];
+        for (int a = 0; a < N; ++a) sX[(sl - 1) * N2 + a * N + b] = yv[a];
       __syncthreads();
       if (take)
 #pragma unroll
-        for (int a = 0; a < N; ++a) yv[a] += sX[(sl + 1) * N2 + a * N + b];
+        for (int a = 0; a < N; ++a) yv[a] += sX[sl * N2 + a * N + b];
     }
 #endif
     if (active && !give) {
