@@ -490,6 +490,11 @@ struct sem_dd {
   int32_t* d_seam_cj = nullptr;
   uint32_t* d_rest = nullptr;
   int64_t n_rest = 0;
+  // the interface context's seam sum fused with the pack (sem::ctx_seam_pack;
+  // SEM_DD_FUSE_PACK=0 keeps the two launches): d_pack_sj[k] = seam index of
+  // the k-th exchanged DOF in the interface plan, or -1
+  bool pack_fused = false;
+  int32_t* d_pack_sj = nullptr;
   uint64_t fin_epoch = ~0ull;
   bool loopback = false;        // diagnostic transport (sem_dd_set_loopback)
   bool rccl_self = false;       // timing transport: RCCL send/recv to this rank itself
@@ -592,11 +597,12 @@ int build_finish(sem_dd* d) {
   // allocation: a rebuild after a map change may be handed the same addresses
   for (void** pp : {(void**)&d->d_sidx, (void**)&d->d_seam_cj, (void**)&d->d_rest,
                     (void**)&d->d_fidx, (void**)&d->d_rp, (void**)&d->d_rpos,
-                    (void**)&d->d_fzero}) {
+                    (void**)&d->d_fzero, (void**)&d->d_pack_sj}) {
     (void)hipFree(*pp);
     *pp = nullptr;
   }
   d->n_rest = 0;
+  d->pack_fused = false;
   HIP_TRY(hipMalloc(&d->d_fidx, std::max<int64_t>(nc, 1) * sizeof(uint32_t)));
   HIP_TRY(hipMalloc(&d->d_rp, rp.size() * sizeof(int32_t)));
   HIP_TRY(hipMalloc(&d->d_rpos, rpos.size() * sizeof(uint32_t)));
@@ -651,6 +657,20 @@ int build_finish(sem_dd* d) {
     bool unref = false;
     SEM_TRY(sem::ctx_zero_list(d->iface, &zi, &unref));
     d->iface_skip_zero = unref;
+    const char* fp = std::getenv("SEM_DD_FUSE_PACK");
+    if (ne && sem::ctx_seam_fusable(d->iface) && !sem::ctx_seam_has_prior(d->iface) &&
+        !(fp && std::atoi(fp) == 0)) {
+      std::vector<uint32_t> sg;
+      SEM_TRY(sem::ctx_seam_gids(d->iface, &sg));
+      std::vector<int32_t> seam_of((size_t)d->ndof, -1);
+      for (size_t t = 0; t < sg.size(); ++t) seam_of[sg[t]] = (int32_t)t;
+      std::vector<int32_t> sj((size_t)ne);
+      for (int64_t t = 0; t < ne; ++t) sj[t] = seam_of[sidx[t]];
+      HIP_TRY(hipMalloc(&d->d_pack_sj, sj.size() * sizeof(int32_t)));
+      HIP_TRY(hipMemcpy(d->d_pack_sj, sj.data(), sj.size() * sizeof(int32_t),
+                        hipMemcpyHostToDevice));
+      d->pack_fused = true;
+    }
   }
   d->fin_epoch = ep;
   return SEM_OK;
@@ -662,6 +682,15 @@ int dd_side(sem_dd* d, int op_kind, bool diag, const double* u, hipStream_t sd) 
   if (!d->iface) return SEM_OK;
   if (diag) {
     SEM_TRY(sem_diag(d->iface, op_kind, d->d_yc, sd));
+  } else if (d->iface_local && d->pack_fused) {
+    // interface elements, then their seam sum and the pack in one launch
+    sem::ctx_set_defer_seam_sum(d->iface, true);
+    const int rc = sem_apply(d->iface, op_kind, u, d->d_yc,
+                             d->iface_skip_zero ? SEM_APPLY_SKIP_ZERO : 0, sd);
+    sem::ctx_set_defer_seam_sum(d->iface, false);
+    SEM_TRY(rc);
+    return sem::ctx_seam_pack(d->iface, d->d_yc, d->d_send, d->d_sidx, d->d_pack_sj,
+                              n_exchanged(d), sd);
   } else if (d->iface_local) {
     SEM_TRY(sem_apply(d->iface, op_kind, u, d->d_yc, d->iface_skip_zero ? SEM_APPLY_SKIP_ZERO : 0,
                       sd));
@@ -1203,6 +1232,7 @@ void sem_dd_destroy(sem_dd* d) {
   (void)hipFree(d->d_sidx);
   (void)hipFree(d->d_seam_cj);
   (void)hipFree(d->d_rest);
+  (void)hipFree(d->d_pack_sj);
   if (d->ev0) (void)hipEventDestroy(d->ev0);
   if (d->ev1) (void)hipEventDestroy(d->ev1);
   if (d->side) (void)hipStreamDestroy(d->side);
@@ -1291,7 +1321,8 @@ int sem_dd_info(sem_dd* d, int64_t* info, int n_info) {
                          d->graphs ? 1 : 0, d->n_captures, d->n_replays,
                          d->host_steps, d->host_ns, d->host_ns_transport,
                          d->host_ns_side, d->host_ns_main, d->host_ns_finish,
-                         (d->defer_zero ? 1 : 0) | (d->seam_fused ? 2 : 0)};
+                         (d->defer_zero ? 1 : 0) | (d->seam_fused ? 2 : 0) |
+                             (d->pack_fused ? 4 : 0)};
   for (int i = 0; i < n_info && i < 16; ++i) info[i] = v[i];
   return SEM_OK;
 }

@@ -181,6 +181,18 @@ int ctx_seam_gids(const sem_ctx* c, std::vector<uint32_t>* gids) {
   return SEM_OK;
 }
 void ctx_set_defer_seam_sum(sem_ctx* c, bool defer) { c->defer_seam_sum = defer; }
+bool ctx_seam_has_prior(const sem_ctx* c) {
+  if (!c->n_seam) return false;
+  std::vector<uint16_t> m((size_t)c->n_seam);
+  if (hipMemcpy(m.data(), c->d_seam_mask, c->n_seam * sizeof(uint16_t), hipMemcpyDeviceToHost) !=
+      hipSuccess) {
+    (void)hipGetLastError();
+    return true;  // unknown: treated as not fusable
+  }
+  for (uint16_t v : m)
+    if (v & 0x100u) return true;
+  return false;
+}
 int ctx_zero_list(const sem_ctx* c, std::vector<uint32_t>* nodes, bool* only_unreferenced) {
   if (c->ndim == 3) return semh::zero_list(c, nodes, only_unreferenced);
   nodes->assign((size_t)c->n_zero, 0u);
@@ -1796,6 +1808,27 @@ int sem_det_inv_2x2(int64_t n, const double* d_mat, double* d_det, double* d_inv
 }  // extern "C"
 
 namespace sem {
+int ctx_seam_pack(sem_ctx* c, double* y, double* send, const uint32_t* sidx, const int32_t* sj,
+                  int64_t ne, hipStream_t st) {
+  const int64_t tot = c->n_seam + ne;
+  if (!tot) return SEM_OK;
+  const dim3 g(semd::grid_for(tot)), b(BLOCK);
+  switch (c->seam_ns) {
+#define SEAM_PACK(K)                                                                        \
+  case K:                                                                                 \
+    hipLaunchKernelGGL(k_seam_pack<K>, g, b, 0, st, y, c->d_seam_gid, c->d_seam_mask,      \
+                       c->n_seam, c->d_seam_buf, c->n_node, send, sidx, sj, ne);          \
+    break;
+    SEAM_PACK(1) SEAM_PACK(2) SEAM_PACK(3) SEAM_PACK(4) SEAM_PACK(5) SEAM_PACK(6) SEAM_PACK(7)
+    SEAM_PACK(8)
+#undef SEAM_PACK
+    default:
+      return fail(SEM_E_STATE, "seam plan with more than 8 colours");
+  }
+  HIP_TRY(hipGetLastError());
+  return SEM_OK;
+}
+
 int ctx_seam_finish(sem_ctx* c, double* y, const DDFinish& f, hipStream_t st) {
   const int64_t tot = c->n_seam + f.n_rest + f.nz;
   if (!tot) return SEM_OK;

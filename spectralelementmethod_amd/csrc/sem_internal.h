@@ -70,4 +70,11 @@ bool ctx_seam_fusable(const sem_ctx* c);
 int ctx_seam_gids(const sem_ctx* c, std::vector<uint32_t>* gids);
 void ctx_set_defer_seam_sum(sem_ctx* c, bool defer);
 int ctx_seam_finish(sem_ctx* c, double* y, const DDFinish& f, hipStream_t st);
+// any seam node with a prior value (SEM_NODE_PRIOR): such a plan is not
+// fused with the pack
+bool ctx_seam_has_prior(const sem_ctx* c);
+// the context's seam sum (deferred by sem_apply) fused with the pack of
+// send[k] = y[sidx[k]], k < ne (sj[k]: seam index of that DOF, or -1)
+int ctx_seam_pack(sem_ctx* c, double* y, double* send, const uint32_t* sidx, const int32_t* sj,
+                  int64_t ne, hipStream_t st);
 }  // namespace sem

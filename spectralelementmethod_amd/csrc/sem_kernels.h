@@ -1557,6 +1557,57 @@ __global__ void __launch_bounds__(BLOCK)
   }
 }
 
+// The interface context's seam sum fused with the pack of the send buffer
+// (sem::ctx_seam_pack, sem_dd.hip dd_side): t < n: seam node g of the
+// interface plan, y_c[g] = its colour slots in colour order (k_seam_sum,
+// overwrite mode); then send[k] = y_c[sidx[k]] for every exchanged DOF, the
+// value of a seam node formed again from its slots (sj[k] = its seam index)
+// rather than read back, so no thread waits for another.  Bitwise equal to
+// the seam-sum launch followed by the gather; seam nodes with a prior value
+// (SEM_NODE_PRIOR) are not fused (the caller checks).
+template <int NS>
+__global__ void __launch_bounds__(BLOCK)
+    k_seam_pack(double* __restrict__ y, const uint32_t* __restrict__ gid,
+                const uint16_t* __restrict__ mask, int64_t n, const double* __restrict__ buf,
+                int64_t n_node, double* __restrict__ send, const uint32_t* __restrict__ sidx,
+                const int32_t* __restrict__ sj, int64_t ne) {
+  __amdgpu_buffer_rsrc_t rb[NS];
+#pragma unroll
+  for (int c = 0; c < NS; ++c)
+    rb[c] = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(buf + c * n_node), 0, 0x80000000,
+                                              0x00020000);
+  auto seam_value = [&](int64_t t, uint32_t g) {
+    const uint32_t m = mask[t];
+    double b[NS];
+#pragma unroll
+    for (int c = 0; c < NS; ++c) {
+      const uint32_t off = (m & (1u << c)) ? g * 8u : 0x80000000u;
+      b[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rb[c], off, 0, CPOL_NT));
+    }
+    double s = 0.0;
+    bool first = true;
+#pragma unroll
+    for (int c = 0; c < NS; ++c)
+      if (m & (1u << c)) {
+        s = first ? b[c] : s + b[c];
+        first = false;
+      }
+    return s;
+  };
+  const int64_t tot = n + ne;
+  for (int64_t t = blockIdx.x * (int64_t)BLOCK + threadIdx.x; t < tot;
+       t += (int64_t)gridDim.x * BLOCK) {
+    if (t < n) {
+      const uint32_t g = gid[t];
+      y[g] = seam_value(t, g);
+    } else {
+      const int64_t k = t - n;
+      const int32_t j = sj[k];
+      send[k] = j >= 0 ? seam_value(j, gid[j]) : y[sidx[k]];
+    }
+  }
+}
+
 // fixed-order sum of the DOT partials of an action: na chain partials, then
 // nb seam-sum partials -> *out
 [[maybe_unused]] static __global__ void __launch_bounds__(BLOCK)

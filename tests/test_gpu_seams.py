@@ -220,3 +220,29 @@ def test_dd_rccl_self_transport_equals_loopback(gpu):
         out[tr] = y.clone()
         op.close()
     assert torch.equal(out["loopback"], out["rccl_self"])
+
+
+@pytest.mark.parametrize("rank", [0, 2])
+@pytest.mark.parametrize("transport", ["loopback", "rccl_self"])
+def test_dd_fused_seam_pack_is_bitwise(gpu, monkeypatch, rank, transport):
+    """The interface context's seam sum fused with the pack of the send
+    buffer (one launch on the side stream) equals its own seam-sum launch
+    followed by the gather, bit for bit, on one rank of a 4-strip split."""
+    from spectralelementmethod_amd.distributed import OverlappedOperator, StripPartition
+    part = StripPartition(24, 112, 8, 4, rank)
+    nodes, e2n = part.local_mesh(0.05)
+    u = torch.from_numpy(np.random.default_rng(7).standard_normal(nodes.shape[1])).to(gpu)
+    monkeypatch.setenv("SEM_SEAM", "1")
+    out = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("SEM_DD_FUSE_PACK", fuse)
+        op = OverlappedOperator(8, nodes, e2n, part.neighbors, 1, gpu, owned=part.owned,
+                                transport=transport, world=1, rank=0, decompose=True)
+        y = torch.full_like(u, 7.0)
+        op.step(u, y)
+        op.step(u, y)
+        torch.cuda.synchronize()
+        out[fuse] = (y.clone(), op.dd_info())
+        op.close()
+    assert out["1"][1]["seam_sum_in_pack"] and not out["0"][1]["seam_sum_in_pack"]
+    assert torch.equal(out["1"][0], out["0"][0])
