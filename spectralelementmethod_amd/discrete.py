@@ -29,7 +29,7 @@ from collections import namedtuple
 import numpy as np
 from scipy import sparse
 
-from .geometry import Quadrilateral
+from .geometry import NCube, Quadrilateral
 from .mapping import Mapping, OutsideDomain  # noqa: F401
 
 _CELL_CHUNK = 4096
@@ -164,12 +164,17 @@ class Mesh(object):
 
     @classmethod
     def from_arrays(cls, nodes, e2n, region="*"):
-        """Mesh of identical quadrilateral cells from nodes [2, N] and an
-        element map [E, n0, n1] (the batched form of add_cell)."""
-        e2n = np.ascontiguousarray(e2n, dtype=np.uint32)
-        mesh = cls(2)
-        mesh.set_nodes(np.array(nodes, dtype=np.float64))
-        gid = mesh.add_geometry(Quadrilateral(*e2n.shape[1:]))
+        """Mesh of identical cells from nodes [d, N] and an element map [E,
+        n0, .., n_{d-1}] (the batched form of add_cell): quadrilaterals for
+        d = 2, hexahedra (NCube of three axes) for d = 3."""
+        e2n = np.array(e2n, dtype=np.uint32, order="C")  # a copy: node permutations
+        nodes = np.array(nodes, dtype=np.float64)         # must not reach the caller's
+        d = nodes.shape[0]
+        if e2n.ndim != d + 1 or d not in (2, 3):
+            raise ValueError("nodes [d, N] with d = 2 or 3 and an element map [E] + [n] * d")
+        mesh = cls(d)
+        mesh.set_nodes(nodes)
+        gid = mesh.add_geometry(Quadrilateral(*e2n.shape[1:]) if d == 2 else NCube(*e2n.shape[1:]))
         rid = mesh.new_region(region)
         mesh.add_cells(e2n, gid, rid)
         return mesh

@@ -58,3 +58,24 @@ def test_rcm_rejects_bad_map():
     with pytest.raises(ValueError):
         rcm_permutation(np.array([[0, 1, 5]]), 3)
 
+
+
+def test_dofmanager_hex_rcm_numbering():
+    """DOFManager's default RCM on a hexahedral mesh built with
+    Mesh.from_arrays: scipy's permutation of the 3-D pair graph; the caller's
+    arrays are left alone."""
+    from spectralelementmethod_amd.basis_functions import LagrangeGaussLobatto, TensorProductQS
+    from spectralelementmethod_amd.discrete import DOFManager, Mesh
+    p = 3
+    nodes, e2n = meshgen.structured_cube(3, 2, 2, p, warp=0.05)
+    e2n0, nodes0 = e2n.copy(), nodes.copy()
+    mesh = Mesh.from_arrays(nodes, e2n)
+    b = LagrangeGaussLobatto(p)
+    DOFManager(mesh, 1, TensorProductQS(b, b, b))
+    perm = csgraph.reverse_cuthill_mckee(_pair_graph(e2n.reshape(e2n.shape[0], -1),
+                                                     nodes.shape[1]), True)
+    inv = np.empty_like(perm)
+    inv[perm] = np.arange(perm.size, dtype=perm.dtype)
+    assert np.array_equal(e2n, e2n0) and np.array_equal(nodes, nodes0)
+    assert np.array_equal(mesh.nodes, nodes[:, perm])
+    assert np.array_equal(mesh.element_map(), inv[e2n])
