@@ -1,0 +1,14 @@
+#!/bin/bash
+# Where the hexahedral element kernel's cycles go: SQ counters, one pass per set.
+#   tools/gpu_hex_ctr.sh OUT
+set -o pipefail
+export TMPDIR=/tmp
+O=$1; mkdir -p $O
+i=0
+for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD" \
+           "SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_WR" \
+           "GRBM_GUI_ACTIVE GRBM_COUNT"; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --pmc $set --kernel-include-regex k_hex_poisson --output-format csv -d $O/p$i -o run -- python3 bench.py --dim 3 --no-cpu-baseline --no-check --steps 4 --warmup 1 > $O/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $O/p$i.log; exit 1; }
+done
+python3 tools/ctr_summary.py $O
