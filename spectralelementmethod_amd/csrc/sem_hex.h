@@ -72,13 +72,13 @@ enum { HEX_SET = 0, HEX_ACC = 1, HEX_DIAG = 2 };
 #endif
 constexpr bool HEX_ZMERGE = SEM_HEX_ZMERGE != 0;
 
-// D and D^T as a kernel argument: the wave-uniform coefficients of the
-// register-direction contractions are read with scalar loads (SGPR operands)
-// instead of LDS broadcasts, which cost the LDS pipe as much as data reads.
+// D as a kernel argument: the wave-uniform coefficients of the
+// register-direction contractions (row a of D, for d0 = D u and y += D^T w0
+// along xi0) are read with scalar loads (SGPR operands) instead of LDS
+// broadcasts, which cost the LDS pipe as much as data reads.
 template <int N>
 struct HexD {
-  double dt[N * N];  // dt[r*N + a] = D[a][r]: column r of D, contiguous
-  double d[N * N];   // d[q*N + a] = D[q][a]: row q of D
+  double d[N * N];  // d[q*N + a] = D[q][a]: row q of D
 };
 
 // boundary-column index of (b, c) in [0, 4(n-1)), -1 for an interior column
@@ -157,9 +157,9 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
 #pragma unroll
     for (int a = 0; a < N; ++a) m[a] = mn[a];
     const double* g = G + ((int64_t)e * N3 + bc) * 6;
+    double uc[MODE != HEX_DIAG ? N : 1];
     if (active) {
       if constexpr (MODE != HEX_DIAG) {
-        double uc[N];
 #pragma unroll
         for (int a = 0; a < N; ++a) {
 #ifdef SEM_HEX_DIAG_NOGATHER  // diagnostic builds only: no u gather
@@ -195,51 +195,41 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
 #pragma unroll
     for (int a = 0; a < N; ++a) yv[a] = 0.0;
     if constexpr (MODE != HEX_DIAG) {
-      double w0[N];
       if (active) {
-        double d0[N], d1[N], d2[N];
-#pragma unroll
-        for (int a = 0; a < N; ++a) d0[a] = d1[a] = d2[a] = 0.0;
+        // Node row a (outer, not unrolled): d = (D u)_a along xi0 / xi1 /
+        // xi2, w = G d; w1 / w2 to LDS; y += D[a][.] w0, the D^T contraction
+        // along xi0, in registers (D row a read once per row with scalar
+        // loads: it serves both xi0 contractions).  w0 never goes through
+        // LDS, and su is free for the next step's u after the barrier.
+        // (The r-outer form with d0 / d1 / d2 arrays: 223.6 against
+        // 218-220 us, profiles/r05/hex/a_outer/.)
 #pragma unroll 1
-        for (int r = 0; r < N; ++r) {
-          const double ur = su[r * N2 + bc];
-          const double dbr = sD[b * N + r], dcr = sD[c * N + r];
-#pragma unroll
-          for (int a = 0; a < N; ++a) {
-            d0[a] = fma(Dk.dt[r * N + a], ur, d0[a]);
-            d1[a] = fma(dbr, su[a * N2 + r * N + c], d1[a]);
-            d2[a] = fma(dcr, su[a * N2 + b * N + r], d2[a]);
-          }
-        }
-#pragma unroll
         for (int a = 0; a < N; ++a) {
+          double d0 = 0.0, d1 = 0.0, d2 = 0.0;
+#pragma unroll
+          for (int r = 0; r < N; ++r) {
+            d0 = fma(Dk.d[a * N + r], uc[r], d0);
+            const double dbr = sD[b * N + r], dcr = sD[c * N + r];
+            d1 = fma(dbr, su[a * N2 + r * N + c], d1);
+            d2 = fma(dcr, su[a * N2 + b * N + r], d2);
+          }
           const double2* ga = reinterpret_cast<const double2*>(g + a * N2 * 6);
-#ifdef SEM_HEX_DIAG_NOG  // diagnostic builds only: no factor stream
-          const double2 q0 = make_double2(1.0, 0.1 * a), q1 = make_double2(0.2, 1.0),
-                        q2 = make_double2(0.3 * c, 1.0);
-          (void)ga;
-#else
           const double2 q0 = ga[0], q1 = ga[1], q2 = ga[2];
-#endif
           const double g00 = q0.x, g01 = q0.y, g02 = q1.x, g11 = q1.y, g12 = q2.x, g22 = q2.y;
-          w0[a] = g00 * d0[a] + g01 * d1[a] + g02 * d2[a];
-          sa[a * N2 + bc] = g01 * d0[a] + g11 * d1[a] + g12 * d2[a];
-          sb[a * N2 + bc] = g02 * d0[a] + g12 * d1[a] + g22 * d2[a];
+          const double w0 = g00 * d0 + g01 * d1 + g02 * d2;
+          sa[a * N2 + bc] = g01 * d0 + g11 * d1 + g12 * d2;
+          sb[a * N2 + bc] = g02 * d0 + g12 * d1 + g22 * d2;
+#pragma unroll
+          for (int q = 0; q < N; ++q) yv[q] = fma(Dk.d[a * N + q], w0, yv[q]);
         }
       }
-      __syncthreads();
+      __syncthreads();  // w1 / w2 complete; su is free for the next step's u
       if (active) {
-        // w0 into this thread's own column of su (no other thread reads it
-        // until the next element's first barrier)
-#pragma unroll
-        for (int a = 0; a < N; ++a) su[a * N2 + bc] = w0[a];
 #pragma unroll 1
         for (int q = 0; q < N; ++q) {
-          const double wq = su[q * N2 + bc];
           const double dqb = sD[q * N + b], dqc = sD[q * N + c];
 #pragma unroll
           for (int a = 0; a < N; ++a) {
-            yv[a] = fma(Dk.d[q * N + a], wq, yv[a]);
             yv[a] = fma(dqb, sa[a * N2 + q * N + c], yv[a]);
             yv[a] = fma(dqc, sb[a * N2 + b * N + q], yv[a]);
           }

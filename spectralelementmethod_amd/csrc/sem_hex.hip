@@ -377,11 +377,7 @@ int launch_hex_apply(sem_ctx* c, int mode, const double* u, double* y, hipStream
                           H->d_cflag,  H->d_slot,   H->face_base};
   const dim3 g((unsigned)H->n_wg), b(semh::hex_threads(N));
   semh::HexD<N> Dk;
-  for (int i = 0; i < N; ++i)
-    for (int j = 0; j < N; ++j) {
-      Dk.dt[j * N + i] = c->hD[i * N + j];
-      Dk.d[i * N + j] = c->hD[i * N + j];
-    }
+  for (int i = 0; i < N * N; ++i) Dk.d[i] = c->hD[i];
   if (mode == semh::HEX_SET)
     hipLaunchKernelGGL((semh::k_hex_poisson<N, semh::HEX_SET>), g, b, 0, st, u, y, H->d_map,
                        H->d_G, c->d_D, L, Dk);
