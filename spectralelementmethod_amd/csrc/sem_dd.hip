@@ -74,12 +74,22 @@ namespace {
 
 constexpr int BLK = 256;
 constexpr int WV = 64;
-constexpr int RED_BLOCKS = 2048;  // partial sums per dot (fixed: deterministic order)
+// 512 workgroups (2 per CU, 8 waves per CU) stream the vectors fastest: at
+// 1024^2 p = 8 the PCG iteration takes 1.42 ms against 1.46 / 1.50 / 1.54 /
+// 1.57-1.66 with 384 / 768 / 1024 / 2048 workgroups and 1.53-1.59 with 256
+// (profiles/r05/pcg/grid_ab/): fewer concurrent streams per array
+#ifndef SEM_PCG_RED_BLOCKS
+#define SEM_PCG_RED_BLOCKS 512
+#endif
+constexpr int RED_BLOCKS = SEM_PCG_RED_BLOCKS;  // partial sums per dot (fixed: deterministic order)
 // The PCG vector kernels stream 5-9 vectors of n doubles per iteration: each
 // thread walks the grid-stride sequence UNR entries at a time with all their
 // loads issued before any use (memory-level parallelism: one load per array
 // in flight per thread measured ~4 TB/s at 67M DOF, round 2).
-constexpr int UNR = 4;
+#ifndef SEM_PCG_UNR
+#define SEM_PCG_UNR 4
+#endif
+constexpr int UNR = SEM_PCG_UNR;
 
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
