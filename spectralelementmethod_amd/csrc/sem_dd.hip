@@ -505,6 +505,14 @@ struct sem_dd {
   // the k-th exchanged DOF in the interface plan, or -1
   bool pack_fused = false;
   int32_t* d_pack_sj = nullptr;
+  // split finish (SEM_DD_SPLIT_FINISH, default on with the fused seam sum):
+  // the interior's seam nodes no interface DOF touches, and the deferred
+  // zero list, are finished on the caller's stream BEFORE the join with the
+  // side stream (they do not need the exchange); the rest after it
+  bool split_finish = false, split_pre_done = false;
+  uint32_t* d_seam_pre = nullptr;
+  uint32_t* d_seam_post = nullptr;
+  int64_t n_seam_pre = 0, n_seam_post = 0;
   uint64_t fin_epoch = ~0ull;
   bool loopback = false;        // diagnostic transport (sem_dd_set_loopback)
   bool rccl_self = false;       // timing transport: RCCL send/recv to this rank itself
@@ -607,12 +615,15 @@ int build_finish(sem_dd* d) {
   // allocation: a rebuild after a map change may be handed the same addresses
   for (void** pp : {(void**)&d->d_sidx, (void**)&d->d_seam_cj, (void**)&d->d_rest,
                     (void**)&d->d_fidx, (void**)&d->d_rp, (void**)&d->d_rpos,
-                    (void**)&d->d_fzero, (void**)&d->d_pack_sj}) {
+                    (void**)&d->d_fzero, (void**)&d->d_pack_sj, (void**)&d->d_seam_pre,
+                    (void**)&d->d_seam_post}) {
     (void)hipFree(*pp);
     *pp = nullptr;
   }
   d->n_rest = 0;
   d->pack_fused = false;
+  d->split_finish = false;
+  d->n_seam_pre = d->n_seam_post = 0;
   HIP_TRY(hipMalloc(&d->d_fidx, std::max<int64_t>(nc, 1) * sizeof(uint32_t)));
   HIP_TRY(hipMalloc(&d->d_rp, rp.size() * sizeof(int32_t)));
   HIP_TRY(hipMalloc(&d->d_rpos, rpos.size() * sizeof(uint32_t)));
@@ -653,6 +664,22 @@ int build_finish(sem_dd* d) {
       HIP_TRY(hipMemcpy(d->d_rest, rest.data(), rest.size() * sizeof(uint32_t),
                         hipMemcpyHostToDevice));
     d->n_rest = (int64_t)rest.size();
+    const char* fs = std::getenv("SEM_DD_SPLIT_FINISH");
+    if (!(fs && std::atoi(fs) == 0)) {
+      std::vector<uint32_t> pre, post;
+      for (size_t t = 0; t < cj.size(); ++t) (cj[t] >= 0 ? post : pre).push_back((uint32_t)t);
+      HIP_TRY(hipMalloc(&d->d_seam_pre, std::max<size_t>(pre.size(), 1) * sizeof(uint32_t)));
+      HIP_TRY(hipMalloc(&d->d_seam_post, std::max<size_t>(post.size(), 1) * sizeof(uint32_t)));
+      if (!pre.empty())
+        HIP_TRY(hipMemcpy(d->d_seam_pre, pre.data(), pre.size() * sizeof(uint32_t),
+                          hipMemcpyHostToDevice));
+      if (!post.empty())
+        HIP_TRY(hipMemcpy(d->d_seam_post, post.data(), post.size() * sizeof(uint32_t),
+                          hipMemcpyHostToDevice));
+      d->n_seam_pre = (int64_t)pre.size();
+      d->n_seam_post = (int64_t)post.size();
+      d->split_finish = true;
+    }
   }
   if (d->iface_local) {
     // pack reads y_c at the local DOF of every exchanged compact DOF; the
@@ -786,23 +813,47 @@ int dd_exchange_impl(sem_dd* d) {
 
 // unpack + final add + deferred zero list in one launch on `st` (with the
 // interior's seam sum when it was deferred)
+sem::DDFinish dd_finish_args(const sem_dd* d) {
+  sem::DDFinish f{};
+  f.fidx = d->d_fidx;
+  f.nc = d->nc;
+  f.yc = d->d_yc;
+  f.yc_local = d->iface_local ? 1 : 0;
+  f.rp = d->d_rp;
+  f.rpos = d->d_rpos;
+  f.recv = d->d_recv;
+  f.fzero = d->d_fzero;
+  f.nz = d->defer_zero ? d->n_fzero : 0;
+  f.seam_cj = d->d_seam_cj;
+  f.rest = d->d_rest;
+  f.n_rest = d->n_rest;
+  return f;
+}
+
+// split finish, before the join: the interior's seam nodes off the
+// interface and the deferred zero list (no received value needed)
+int dd_finish_pre(sem_dd* d, double* y, hipStream_t st) {
+  d->split_pre_done = false;
+  if (!(d->seam_deferred && d->split_finish)) return SEM_OK;
+  sem::DDFinish f = dd_finish_args(d);
+  f.sel = d->d_seam_pre;
+  f.n_sel = d->n_seam_pre;
+  f.skip_rest = 1;
+  SEM_TRY(sem::ctx_seam_finish(d->interior, y, f, st));
+  d->split_pre_done = true;
+  return SEM_OK;
+}
+
 int dd_add(sem_dd* d, double* y, hipStream_t st) {
-  if (d->seam_deferred) {
-    sem::DDFinish f{};
-    f.fidx = d->d_fidx;
-    f.nc = d->nc;
-    f.yc = d->d_yc;
-    f.yc_local = d->iface_local ? 1 : 0;
-    f.rp = d->d_rp;
-    f.rpos = d->d_rpos;
-    f.recv = d->d_recv;
-    f.fzero = d->d_fzero;
-    f.nz = d->defer_zero ? d->n_fzero : 0;
-    f.seam_cj = d->d_seam_cj;
-    f.rest = d->d_rest;
-    f.n_rest = d->n_rest;
+  if (d->seam_deferred && d->split_finish && d->split_pre_done) {
+    // the part that needs the exchange (the pre part ran before the join)
+    sem::DDFinish f = dd_finish_args(d);
+    f.sel = d->d_seam_post;
+    f.n_sel = d->n_seam_post;
+    f.skip_zero = 1;
     return sem::ctx_seam_finish(d->interior, y, f, st);
   }
+  if (d->seam_deferred) return sem::ctx_seam_finish(d->interior, y, dd_finish_args(d), st);
   const int64_t tot = d->nc + (d->defer_zero ? d->n_fzero : 0);
   if (!tot) return SEM_OK;
   hipLaunchKernelGGL(k_dd_finish, dim3(grid_for(tot)), dim3(BLK), 0, st, y, d->d_fidx, d->nc,
@@ -824,8 +875,10 @@ int dd_join(sem_dd* d, hipStream_t st) {
 
 int dd_finish(sem_dd* d, double* y, hipStream_t st) {
   const auto t0 = Clock::now();
+  SEM_TRY(dd_finish_pre(d, y, st));
   SEM_TRY(dd_join(d, st));
   const int rc = dd_add(d, y, st);
+  d->split_pre_done = false;
   d->host_ns_finish += ns_since(t0);
   return rc;
 }
@@ -1332,7 +1385,8 @@ int sem_dd_info(sem_dd* d, int64_t* info, int n_info) {
                          d->host_steps, d->host_ns, d->host_ns_transport,
                          d->host_ns_side, d->host_ns_main, d->host_ns_finish,
                          (d->defer_zero ? 1 : 0) | (d->seam_fused ? 2 : 0) |
-                             (d->pack_fused ? 4 : 0)};
+                             (d->pack_fused ? 4 : 0) |
+                             (d->split_finish ? 8 : 0)};
   for (int i = 0; i < n_info && i < 16; ++i) info[i] = v[i];
   return SEM_OK;
 }

@@ -1830,7 +1830,8 @@ int ctx_seam_pack(sem_ctx* c, double* y, double* send, const uint32_t* sidx, con
 }
 
 int ctx_seam_finish(sem_ctx* c, double* y, const DDFinish& f, hipStream_t st) {
-  const int64_t tot = c->n_seam + f.n_rest + f.nz;
+  const int64_t tot = (f.sel ? f.n_sel : c->n_seam) + (f.skip_rest ? 0 : f.n_rest) +
+                      (f.skip_zero ? 0 : f.nz);
   if (!tot) return SEM_OK;
   const dim3 g(semd::grid_for(tot)), b(BLOCK);
   switch (c->seam_ns) {

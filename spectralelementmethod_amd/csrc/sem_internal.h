@@ -63,6 +63,12 @@ struct DDFinish {
   const int32_t* seam_cj;  // [n_seam] compact DOF of the seam node, or -1
   const uint32_t* rest;    // compact DOFs that are not seam nodes
   int64_t n_rest;
+  // split finish (sem_dd.hip dd_finish): sel = the seam nodes this launch
+  // handles (null: all); rest handled unless skip_rest, the zero list
+  // unless skip_zero
+  const uint32_t* sel = nullptr;
+  int64_t n_sel = 0;
+  int skip_rest = 0, skip_zero = 0;
 };
 // seam plan of a one-DOF-per-node context: true when sem_apply can leave its
 // seam sum to ctx_seam_finish; the seam nodes' ids copied to the host

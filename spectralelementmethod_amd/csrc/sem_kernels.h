@@ -1521,10 +1521,14 @@ __global__ void __launch_bounds__(BLOCK)
   for (int c = 0; c < NS; ++c)
     rb[c] = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(buf + c * n_node), 0, 0x80000000,
                                               0x00020000);
-  const int64_t tot = n + f.n_rest + f.nz;
-  for (int64_t t = blockIdx.x * (int64_t)BLOCK + threadIdx.x; t < tot;
-       t += (int64_t)gridDim.x * BLOCK) {
-    if (t < n) {
+  const int64_t ns = f.sel ? f.n_sel : n;
+  const int64_t nr = f.skip_rest ? 0 : f.n_rest;
+  const int64_t nzl = f.skip_zero ? 0 : f.nz;
+  const int64_t tot = ns + nr + nzl;
+  for (int64_t ti = blockIdx.x * (int64_t)BLOCK + threadIdx.x; ti < tot;
+       ti += (int64_t)gridDim.x * BLOCK) {
+    if (ti < ns) {
+      const int64_t t = f.sel ? (int64_t)f.sel[ti] : ti;
       const uint32_t g = gid[t];
       const uint32_t m = mask[t];
       const bool prior = (m & 0x100u) != 0;
@@ -1545,14 +1549,14 @@ __global__ void __launch_bounds__(BLOCK)
       const int32_t j = f.seam_cj[t];
       if (j >= 0) s = s + iface_value(j, g);
       y[g] = s;
-    } else if (t < n + f.n_rest) {
-      const uint32_t j = f.rest[t - n];
+    } else if (ti < ns + nr) {
+      const uint32_t j = f.rest[ti - ns];
       const uint32_t e = f.fidx[j];
       const uint32_t i = e & 0x7fffffffu;
       const double v = iface_value(j, i);
       y[i] = ((e >> 31) ? 0.0 : y[i]) + v;
     } else {
-      y[f.fzero[t - n - f.n_rest]] = 0.0;
+      y[f.fzero[ti - ns - nr]] = 0.0;
     }
   }
 }

@@ -609,7 +609,8 @@ class OverlappedOperator(object):
                     host_ns_side=v[12], host_ns_interior=v[13], host_ns_finish=v[14],
                     host_us_side=v[12] / steps / 1e3, host_us_interior=v[13] / steps / 1e3,
                     host_us_finish=v[14] / steps / 1e3, zero_list_in_finish=bool(v[15] & 1),
-                    seam_sum_in_finish=bool(v[15] & 2), seam_sum_in_pack=bool(v[15] & 4))
+                    seam_sum_in_finish=bool(v[15] & 2), seam_sum_in_pack=bool(v[15] & 4),
+                    split_finish=bool(v[15] & 8))
 
     def set_graphs(self, enable):
         """Captured step on / off (sem_dd_set_graphs)."""

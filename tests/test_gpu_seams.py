@@ -246,3 +246,29 @@ def test_dd_fused_seam_pack_is_bitwise(gpu, monkeypatch, rank, transport):
         op.close()
     assert out["1"][1]["seam_sum_in_pack"] and not out["0"][1]["seam_sum_in_pack"]
     assert torch.equal(out["1"][0], out["0"][0])
+
+
+@pytest.mark.parametrize("rank", [0, 2])
+def test_dd_split_finish_is_bitwise(gpu, monkeypatch, rank):
+    """The fused finish split around the join (the interior's seam nodes off
+    the interface and the zero list before the side stream is waited for, the
+    rest after it) equals the one-launch finish bit for bit."""
+    from spectralelementmethod_amd.distributed import OverlappedOperator, StripPartition
+    part = StripPartition(24, 112, 8, 4, rank)
+    nodes, e2n = part.local_mesh(0.05)
+    u = torch.from_numpy(np.random.default_rng(8).standard_normal(nodes.shape[1])).to(gpu)
+    monkeypatch.setenv("SEM_SEAM", "1")
+    out = {}
+    for split in ("1", "0"):
+        monkeypatch.setenv("SEM_DD_SPLIT_FINISH", split)
+        op = OverlappedOperator(8, nodes, e2n, part.neighbors, 1, gpu, owned=part.owned,
+                                transport="rccl_self", world=1, rank=0, decompose=True)
+        y = torch.full_like(u, 7.0)
+        op.step(u, y)
+        op.step(u, y)
+        torch.cuda.synchronize()
+        out[split] = (y.clone(), op.dd_info())
+        op.close()
+    assert out["1"][1]["split_finish"] and not out["0"][1]["split_finish"]
+    assert out["1"][1]["seam_sum_in_finish"]
+    assert torch.equal(out["1"][0], out["0"][0])
