@@ -107,7 +107,7 @@ struct HexPlanHost {
 };
 
 int hex_build_plan(const std::vector<uint32_t>& h, int64_t E, int64_t n_node, int N,
-                   int64_t target_wgs, HexPlanHost& P) {
+                   int64_t resident, HexPlanHost& P) {
   const int N2 = N * N;
   const int64_t N3 = (int64_t)N2 * N;
   const int S = semh::hex_slots(N), NBC = semh::hex_nbc(N);
@@ -154,9 +154,33 @@ int hex_build_plan(const std::vector<uint32_t>& h, int64_t E, int64_t n_node, in
     chain_start.push_back((int64_t)order.size());
   }
   const int64_t n_chains = (int64_t)chain_start.size() - 1;
-  // 3. sub-chains of near-equal length <= lc
-  int64_t lc = E / std::max<int64_t>(1, (int64_t)S * target_wgs);
-  lc = std::max<int64_t>(1, std::min<int64_t>(lc, 16));
+  // 3. sub-chains of near-equal length <= lc.  A workgroup's time grows
+  //    with its sub-chain length and the launch runs in generations of
+  //    `resident` workgroups, so lc minimises generations x sub-chain length
+  //    (ties: the longer sub-chains, fewer seam nodes).  27^3 at p = 8: lc = 9,
+  //    729 workgroups in one generation -- 0.271 against 0.278 ms per step
+  //    for the round's first rule (lc = 3, 2.85 generations) and 0.275 /
+  //    0.288 / 0.305 for lc = 5 / 4 / 7 (profiles/r05/hex/chain_length/).
+  int64_t lc = 1;
+  {
+    double best = 0.0;
+    for (int64_t c = 1; c <= 16; ++c) {
+      int64_t nsub = 0, maxlen = 0;
+      for (int64_t ch = 0; ch < n_chains; ++ch) {
+        const int64_t M = chain_start[ch + 1] - chain_start[ch];
+        const int64_t parts = (M + c - 1) / c;
+        nsub += parts;
+        maxlen = std::max(maxlen, (M + parts - 1) / parts);
+      }
+      const int64_t nwg = (nsub + S - 1) / S;
+      const int64_t gens = resident > 0 ? (nwg + resident - 1) / resident : 1;
+      const double cost = (double)gens * (double)maxlen;
+      if (c == 1 || cost <= best) {
+        best = cost;
+        lc = c;
+      }
+    }
+  }
   if (const char* s = std::getenv("SEM_HEX_CHAIN")) lc = std::max(1, std::atoi(s));
   struct Sub {
     int64_t start, len;
@@ -431,6 +455,20 @@ int launch_hex_geom(sem_ctx* c, const double* nodes, double* GP, double* xph, do
   }
 static_assert(semh::HEX_MAX_N == 12, "HEX_DISPATCH lists n = 2..12");
 
+// workgroups of the element kernel resident per CU (LDS and VGPR bound)
+template <int N>
+int hex_wgs_per_cu(int* out) {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &nb, reinterpret_cast<const void*>(&semh::k_hex_poisson<N, semh::HEX_SET>),
+          semh::hex_threads(N), 0) != hipSuccess) {
+    (void)hipGetLastError();
+    nb = 0;
+  }
+  *out = nb;
+  return SEM_OK;
+}
+
 int need_map(const sem_ctx* c) {
   if (!c->have_basis) return fail(SEM_E_STATE, "sem_set_basis must precede this call");
   if (!c->hex->d_map) return fail(SEM_E_STATE, "sem_set_map must precede this call");
@@ -477,9 +515,12 @@ int set_map(sem_ctx* c, const uint32_t* d_e2n, hipStream_t st) {
         ncu > 0)
       c->n_cu = ncu;
   }
-  const int64_t target = 8 * std::max(c->n_cu, 256);
+  int wpc = 0, rc = SEM_OK;
+  HEX_DISPATCH(rc, N, hex_wgs_per_cu, &wpc);
+  if (rc) return rc;
+  const int64_t resident = (int64_t)std::max(c->n_cu, 1) * std::max(wpc, 1);
   HexPlanHost P;
-  int rc = hex_build_plan(h, c->n_elem, c->n_node, N, target, P);
+  rc = hex_build_plan(h, c->n_elem, c->n_node, N, resident, P);
   if (rc) return rc;
   c->epoch++;
   c->map_epoch++;
