@@ -79,3 +79,12 @@ def test_dofmanager_hex_rcm_numbering():
     assert np.array_equal(e2n, e2n0) and np.array_equal(nodes, nodes0)
     assert np.array_equal(mesh.nodes, nodes[:, perm])
     assert np.array_equal(mesh.element_map(), inv[e2n])
+
+
+def test_rcm_equals_scipy_cfg2_size():
+    """BASELINE config 2's mesh (256^2 cells, p = 8, 4.2M nodes): the native
+    walk still reproduces scipy's permutation exactly."""
+    nodes, e2n = meshgen.structured_square(256, 256, 8, warp=0.05)
+    maps = e2n.reshape(e2n.shape[0], -1)
+    ref = csgraph.reverse_cuthill_mckee(_pair_graph(maps, nodes.shape[1]), True)
+    np.testing.assert_array_equal(rcm_permutation(maps, nodes.shape[1]), ref)
