@@ -2,6 +2,8 @@
 # One rank of the 8-strip split timed alone: RCCL send/recv to itself vs the
 # loopback copy, side stream at high / normal priority, RCCL protocol LL.
 #   tools/gpu_dd_rccl.sh OUT [tests]
+# (SEM_DD_SIDE_PRIORITY / NCCL_PROTO were measured with the build of that call; the
+#  priority switch was removed afterwards: no effect, profiles/r05/dd/.)
 set -o pipefail
 export TMPDIR=/tmp
 O=$1; mkdir -p $O

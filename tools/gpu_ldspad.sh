@@ -2,6 +2,8 @@
 # Occupancy probe of the constant-D column kernels: SEM_LDS_PAD bytes of
 # dynamic LDS per workgroup (fewer workgroups per CU), p = 12 / 14 / 16.
 #   tools/gpu_ldspad.sh OUT pad...
+# (SEM_LDS_PAD existed only in the probe build of that call -- the launch padding
+#  was removed afterwards; results in profiles/r05/high_order_lds_pad/.)
 set -o pipefail
 export TMPDIR=/tmp
 O=$1; shift; mkdir -p $O
