@@ -1684,7 +1684,7 @@ int sem_apply_dot(sem_ctx* c, int op_kind, const double* u, double* y, double* d
     const int nb = grid_for(n, BLOCK, 2048);
     if ((rc = ensure_dot(c, nb))) return rc;
     hipLaunchKernelGGL(k_dot_plain, dim3(nb), dim3(BLOCK), 0, st, u, y, n, c->d_dot);
-    hipLaunchKernelGGL(k_dot_finish, dim3(1), dim3(BLOCK), 0, st, c->d_dot, (int64_t)nb,
+    hipLaunchKernelGGL(k_dot_finish, dim3(1), dim3(DOT_FIN_THREADS), 0, st, c->d_dot, (int64_t)nb,
                        c->d_dot, (int64_t)0, d_dot);
     HIP_TRY(hipGetLastError());
     return SEM_OK;

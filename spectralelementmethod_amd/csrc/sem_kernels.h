@@ -1613,15 +1613,19 @@ __global__ void __launch_bounds__(BLOCK)
 }
 
 // fixed-order sum of the DOT partials of an action: na chain partials, then
-// nb seam-sum partials -> *out
-[[maybe_unused]] static __global__ void __launch_bounds__(BLOCK)
+// nb seam-sum partials -> *out.  One workgroup of DOT_FIN_THREADS: thread t
+// sums entries t, t + T, ... in order (17.7K partials at 1024^2, 17 each),
+// then a fixed-order workgroup sum.  (256 threads, 69 entries each: 22.9 us
+// per PCG iteration, profiles/r05/pcg/.)
+constexpr int DOT_FIN_THREADS = 1024;
+[[maybe_unused]] static __global__ void __launch_bounds__(DOT_FIN_THREADS)
     k_dot_finish(const double* __restrict__ a, int64_t na, const double* __restrict__ b,
                  int64_t nb, double* __restrict__ out) {
   double v = 0.0;
-  for (int64_t i = threadIdx.x; i < na; i += BLOCK) v += a[i];
-  for (int64_t i = threadIdx.x; i < nb; i += BLOCK) v += b[i];
-  __shared__ double sh[BLOCK / WAVE];
-  const double t = block_sum_fixed<BLOCK / WAVE>(v, sh);
+  for (int64_t i = threadIdx.x; i < na; i += DOT_FIN_THREADS) v += a[i];
+  for (int64_t i = threadIdx.x; i < nb; i += DOT_FIN_THREADS) v += b[i];
+  __shared__ double sh[DOT_FIN_THREADS / WAVE];
+  const double t = block_sum_fixed<DOT_FIN_THREADS / WAVE>(v, sh);
   if (threadIdx.x == 0) *out = t;
 }
 

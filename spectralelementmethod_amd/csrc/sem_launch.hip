@@ -140,7 +140,7 @@ int launch_apply_n(sem_ctx* c, int op_kind, const double* u, double* y, int acc,
     const int rc = launch_seam_sum(c, y, acc, st, dot_out ? u : nullptr,
                                    part ? part + (c1 - c0) : nullptr);
     if (rc || !dot_out) return rc;
-    hipLaunchKernelGGL(k_dot_finish, dim3(1), dim3(BLOCK), 0, st, part, c1 - c0,
+    hipLaunchKernelGGL(k_dot_finish, dim3(1), dim3(DOT_FIN_THREADS), 0, st, part, c1 - c0,
                        part + (c1 - c0), seam_sum_blocks(c), dot_out);
     return SEM_OK;
   }
