@@ -374,7 +374,8 @@ def bench_hex(args):
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
             "traffic_source": os.path.relpath(traffic_src, ROOT) if traffic is not None else None,
             "bytes_model": "16*ndof + 52*E*(p+1)^3 (u, y, 6 factors + uint32 map per element node)",
-            "alg_bytes_per_launch": B, "kernel": "k_hex_poisson<%d,0> + k_hex_seam_sum" % (p + 1),
+            "alg_bytes_per_launch": B, "kernel": "%s<%d,0> + k_hex_seam_sum" % (
+                "k_hex_rows" if plan.get("hex_kernel") == "rows" else "k_hex_poisson", p + 1),
             "fp64_tflops": F / kern_avg_s / 1e12, "fp64_peak_tflops": FP64_PEAK_TFLOPS,
         },
     }

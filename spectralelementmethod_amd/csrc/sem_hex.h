@@ -108,12 +108,12 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
   __shared__ double sU[S * N3];
   __shared__ double sA[S * N3];
   __shared__ double sB[S * N3];
-#if SEM_HEX_ZMERGE
   // z-merge: the xi2 = 0 face of slot s (s >= 1) handed to slot s-1; slot 0
   // never gives, so S-1 faces (n = 9: 1.3 KB, 54,456 bytes in all -- one
-  // 512-byte granule past three workgroups per CU)
-  __shared__ double sX[S > 1 ? (S - 1) * N2 : 1];
-#endif
+  // 512-byte granule past three workgroups per CU).  Always in the diagonal
+  // (setup) kernel, which runs on the row form's z-merged plans.
+  constexpr bool ZM = HEX_ZMERGE || MODE == HEX_DIAG;
+  __shared__ double sX[ZM && S > 1 ? (S - 1) * N2 : 1];
   const int tid = threadIdx.x;
   for (int i = tid; i < N2; i += T) sD[i] = gD[i];
   const int w = blockIdx.x;
@@ -135,10 +135,9 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
   const bool give = (cf & 4) && c == 0;
   [[maybe_unused]] const bool take = active && c == N - 1 && s + 1 < S && (P.cflag[w * S + s + 1] & 4);
   [[maybe_unused]] bool wg_merge = false;
-#if SEM_HEX_ZMERGE
+  if constexpr (ZM)
 #pragma unroll
-  for (int t = 1; t < S; ++t) wg_merge |= (P.cflag[w * S + t] & 4) != 0;
-#endif
+    for (int t = 1; t < S; ++t) wg_merge |= (P.cflag[w * S + t] & 4) != 0;
   double* const face = P.slot + P.face_base + (int64_t)(w * S + sl) * 2 * N2 + bc;
   __syncthreads();  // sD
   double carry = 0.0;
@@ -261,8 +260,7 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
       }
       __syncthreads();  // su / sa / sb are rewritten by the next element
     }
-#if SEM_HEX_ZMERGE
-    if (wg_merge) {  // workgroup-uniform
+    if (ZM && wg_merge) {  // workgroup-uniform
       if (give)
 #pragma unroll
         for (int a = 0; a < N; ++a) sX[(sl - 1) * N2 + a * N + b] = yv[a];
@@ -271,7 +269,6 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
 #pragma unroll
         for (int a = 0; a < N; ++a) yv[a] += sX[sl * N2 + a * N + b];
     }
-#endif
     if (active && !give) {
       if (k > 0) yv[0] += carry;
       const bool last = k == L - 1;
@@ -285,6 +282,159 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
 #ifdef SEM_HEX_DIAG_NOSTORE  // diagnostic builds only: no stores
         if (!(v != v)) continue;
 #endif
+        if (a == 0 && k == 0 && (cf & 1)) {
+          face[0] = v;
+        } else if (a == N - 1 && last && (cf & 2)) {
+          face[N2] = v;
+        } else if (colslot) {
+          cs[a * NBC] = v;
+        } else {
+          if constexpr (MODE == HEX_ACC)
+            y[m[a]] += v;
+          else
+            y[m[a]] = v;
+        }
+      }
+    }
+  }
+}
+
+// Row form of the action (HEX_SET / HEX_ACC): the same
+// thread / slot / chain layout, with the xi1 / xi2 transposed contractions
+// done row by row.  Node row a of y needs only row a of w1 and w2, and row a
+// of u is read only while row a is formed, so per row: d = D u along the
+// three axes, w = G d, w1 / w2 of row a into a two-row LDS ring, barrier,
+// then t_a = the xi1 / xi2 D^T contractions of row a, parked in the thread's
+// own row-a entry of the u block (dead after that row's barrier); y += D[a][.]
+// w0 stays in registers.  LDS per slot: u (n^3) + the ring (4 n^2) instead of
+// three n^3 blocks (n = 9: 22 KB per workgroup against 53 KB), and no
+// loop-invariant LDS operand can be hoisted across the row barriers.
+// four waves per SIMD (<= 128 VGPRs) up to n = 9; above, the allocator
+// would spill at that bound, and three waves per SIMD are what the
+// three-block kernel gets there
+constexpr int hex_rows_min_waves(int n) { return n <= 9 ? 4 : n <= 11 ? 3 : 2; }
+
+template <int N, int MODE>
+__global__ void __launch_bounds__(hex_threads(N), hex_rows_min_waves(N))
+    k_hex_rows(const double* __restrict__ u, double* __restrict__ y,
+               const uint32_t* __restrict__ map, const double* __restrict__ G,
+               const double* __restrict__ gD, HexLaunch P, const HexD<N> Dk) {
+  static_assert(MODE == HEX_SET || MODE == HEX_ACC, "row form: the action only");
+  constexpr int N2 = N * N, N3 = N2 * N, S = hex_slots(N), T = hex_threads(N), NBC = hex_nbc(N);
+  constexpr int SW = S * N2;  // one plane of the ring: [slot][b*n + c]
+  __shared__ double sD[N2];
+  __shared__ double sU[S * N3];
+  __shared__ double sW[4 * SW];  // [row parity][w1, w2][slot][b*n + c]
+  // z-merge: the xi2 = 0 face of slot s (s >= 1) handed to slot s-1
+  __shared__ double sX[S > 1 ? (S - 1) * N2 : 1];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < N2; i += T) sD[i] = gD[i];
+  const int w = blockIdx.x;
+  const int L = P.wg_len[w];
+  const int base = P.wg_off[w];
+  const int s = tid / N2;
+  const int bc = tid - s * N2;
+  const int b = bc / N, c = bc - b * N;
+  const bool active = s < S && P.elist[base + s] >= 0;
+  const int sl = active ? s : 0;
+  double* const su = sU + sl * N3;
+  const int bcol = hex_bcol<N>(b, c);
+  const uint8_t cf = active ? P.cflag[w * S + s] : 0;
+  // z-merge (planner, cflag bit 2): this slot's xi2 = 0 face is slot s-1's
+  // xi2 = n-1 face at every chain step, node for node
+  const bool give = (cf & 4) && c == 0;
+  const bool take = active && c == N - 1 && s + 1 < S && (P.cflag[w * S + s + 1] & 4);
+  bool wg_merge = false;
+#pragma unroll
+  for (int t = 1; t < S; ++t) wg_merge |= (P.cflag[w * S + t] & 4) != 0;
+  double* const face = P.slot + P.face_base + (int64_t)(w * S + sl) * 2 * N2 + bc;
+  __syncthreads();  // sD
+  double carry = 0.0;
+  uint32_t mn[N];
+  int en = active ? P.elist[base + s] : 0;
+  if (active) {
+#pragma unroll
+    for (int a = 0; a < N; ++a) mn[a] = map[(int64_t)en * N3 + a * N2 + bc];
+  }
+#pragma unroll 1
+  for (int k = 0; k < L; ++k) {
+    const int pos = base + k * S + s;
+    const int e = en;
+    uint32_t m[N];
+#pragma unroll
+    for (int a = 0; a < N; ++a) m[a] = mn[a];
+    const double* g = G + ((int64_t)e * N3 + bc) * 6;
+    double uc[N];
+    if (active) {
+#pragma unroll
+      for (int a = 0; a < N; ++a) uc[a] = u[m[a]];
+#pragma unroll
+      for (int a = 0; a < N; ++a) su[a * N2 + bc] = uc[a];
+    }
+    __syncthreads();  // u complete; the previous element's ring / sX reads are done
+    if (active && k + 1 < L) {
+      en = P.elist[pos + S];
+#pragma unroll
+      for (int a = 0; a < N; ++a) mn[a] = map[(int64_t)en * N3 + a * N2 + bc];
+    }
+    double yv[N];
+#pragma unroll
+    for (int a = 0; a < N; ++a) yv[a] = 0.0;
+#pragma unroll 1
+    for (int a = 0; a < N; ++a) {
+      double* const w1p = sW + (a & 1) * 2 * SW + sl * N2;
+      double* const w2p = w1p + SW;
+      if (active) {
+        double d0 = 0.0, d1 = 0.0, d2 = 0.0;
+#pragma unroll
+        for (int r = 0; r < N; ++r) {
+          d0 = fma(Dk.d[a * N + r], uc[r], d0);
+          d1 = fma(sD[b * N + r], su[a * N2 + r * N + c], d1);
+          d2 = fma(sD[c * N + r], su[a * N2 + b * N + r], d2);
+        }
+        const double2* ga = reinterpret_cast<const double2*>(g + a * N2 * 6);
+        const double2 q0 = ga[0], q1 = ga[1], q2 = ga[2];
+        const double g00 = q0.x, g01 = q0.y, g02 = q1.x, g11 = q1.y, g12 = q2.x, g22 = q2.y;
+        const double w0 = g00 * d0 + g01 * d1 + g02 * d2;
+        w1p[bc] = g01 * d0 + g11 * d1 + g12 * d2;
+        w2p[bc] = g02 * d0 + g12 * d1 + g22 * d2;
+#pragma unroll
+        for (int q = 0; q < N; ++q) yv[q] = fma(Dk.d[a * N + q], w0, yv[q]);
+      }
+      __syncthreads();  // row a of w1 / w2 complete; row a of u is dead
+      if (active) {
+        double t = 0.0;
+#pragma unroll
+        for (int q = 0; q < N; ++q) {
+          t = fma(sD[q * N + b], w1p[q * N + c], t);
+          t = fma(sD[q * N + c], w2p[b * N + q], t);
+        }
+        su[a * N2 + bc] = t;
+      }
+    }
+    if (active) {
+#pragma unroll
+      for (int a = 0; a < N; ++a) yv[a] += su[a * N2 + bc];  // the thread's own entries
+    }
+    if (wg_merge) {  // workgroup-uniform
+      if (active && give)
+#pragma unroll
+        for (int a = 0; a < N; ++a) sX[(sl - 1) * N2 + a * N + b] = yv[a];
+      __syncthreads();
+      if (take)
+#pragma unroll
+        for (int a = 0; a < N; ++a) yv[a] += sX[sl * N2 + a * N + b];
+    }
+    if (active && !give) {
+      if (k > 0) yv[0] += carry;
+      const bool last = k == L - 1;
+      if (!last) carry = yv[N - 1];
+      const bool colslot = bcol >= 0 && ((P.cmask[pos] >> bcol) & 1ull);
+      double* const cs = P.slot + ((int64_t)pos * N) * NBC + bcol;
+#pragma unroll
+      for (int a = 0; a < N; ++a) {
+        if (a == N - 1 && !last) continue;  // carried into the next element's row 0
+        const double v = yv[a];
         if (a == 0 && k == 0 && (cf & 1)) {
           face[0] = v;
         } else if (a == N - 1 && last && (cf & 2)) {

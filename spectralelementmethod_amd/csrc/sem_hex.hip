@@ -36,6 +36,12 @@ struct HexState {
   uint32_t* d_map = nullptr;   // the library's copy of the caller's map [E][n][n][n]
   double* d_G = nullptr;       // stored factors [E][n^3][6]
   bool have_G = false;
+  // the action's kernel: k_hex_rows (row form; p <= 7) or k_hex_poisson
+  // (always for the diagonal)
+  bool rows = true;
+  // xi2 faces between the slots of a workgroup summed in LDS (the row form
+  // by default; the three-block kernel only when built with SEM_HEX_ZMERGE)
+  bool zmerge = false;
   // diagnostics (sem_plan_info)
   int64_t n_chains = 0, n_subchains = 0, chain_len = 0, n_direct = 0;
 
@@ -107,7 +113,7 @@ struct HexPlanHost {
 };
 
 int hex_build_plan(const std::vector<uint32_t>& h, int64_t E, int64_t n_node, int N,
-                   int64_t resident, HexPlanHost& P) {
+                   int64_t resident, bool zmerge, HexPlanHost& P) {
   const int N2 = N * N;
   const int64_t N3 = (int64_t)N2 * N;
   const int S = semh::hex_slots(N), NBC = semh::hex_nbc(N);
@@ -247,8 +253,7 @@ int hex_build_plan(const std::vector<uint32_t>& h, int64_t E, int64_t n_node, in
   //     when, at every chain step, that face IS slot s-1's xi2 = n-1 face
   //     node for node (same (a, b)); the kernel sums it in LDS
   std::vector<uint8_t> zm(n_wg * S, 0);
-  const char* zenv = std::getenv("SEM_HEX_ZMERGE");
-  if (semh::HEX_ZMERGE && !(zenv && std::atoi(zenv) == 0))
+  if (zmerge)
     for (int64_t w = 0; w < n_wg; ++w)
       for (int s = 1; s < S; ++s) {
         bool ok = true;
@@ -402,7 +407,13 @@ int launch_hex_apply(sem_ctx* c, int mode, const double* u, double* y, hipStream
   const dim3 g((unsigned)H->n_wg), b(semh::hex_threads(N));
   semh::HexD<N> Dk;
   for (int i = 0; i < N * N; ++i) Dk.d[i] = c->hD[i];
-  if (mode == semh::HEX_SET)
+  if (H->rows && mode == semh::HEX_SET)
+    hipLaunchKernelGGL((semh::k_hex_rows<N, semh::HEX_SET>), g, b, 0, st, u, y, H->d_map, H->d_G,
+                       c->d_D, L, Dk);
+  else if (H->rows && mode == semh::HEX_ACC)
+    hipLaunchKernelGGL((semh::k_hex_rows<N, semh::HEX_ACC>), g, b, 0, st, u, y, H->d_map, H->d_G,
+                       c->d_D, L, Dk);
+  else if (mode == semh::HEX_SET)
     hipLaunchKernelGGL((semh::k_hex_poisson<N, semh::HEX_SET>), g, b, 0, st, u, y, H->d_map,
                        H->d_G, c->d_D, L, Dk);
   else if (mode == semh::HEX_ACC)
@@ -457,11 +468,12 @@ static_assert(semh::HEX_MAX_N == 12, "HEX_DISPATCH lists n = 2..12");
 
 // workgroups of the element kernel resident per CU (LDS and VGPR bound)
 template <int N>
-int hex_wgs_per_cu(int* out) {
+int hex_wgs_per_cu(bool rows, int* out) {
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-          &nb, reinterpret_cast<const void*>(&semh::k_hex_poisson<N, semh::HEX_SET>),
-          semh::hex_threads(N), 0) != hipSuccess) {
+  const void* k = rows ? reinterpret_cast<const void*>(&semh::k_hex_rows<N, semh::HEX_SET>)
+                       : reinterpret_cast<const void*>(&semh::k_hex_poisson<N, semh::HEX_SET>);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, semh::hex_threads(N), 0) !=
+      hipSuccess) {
     (void)hipGetLastError();
     nb = 0;
   }
@@ -488,6 +500,14 @@ int ctx_init(sem_ctx* c) {
   c->hex->slots = hex_slots(c->n);
   c->hex->threads = hex_threads(c->n);
   c->hex->nbc = hex_nbc(c->n);
+  // the row form needs the z-merge off (it has no face exchange)
+  // measured per order (profiles/r05/hex/rows/): the row form
+  // with the z-merge is 8-10 % faster at p = 2 / 4 / 6, ties at p = 8 and
+  // loses at p = 10; SEM_HEX_ROWS=0 / 1 overrides
+  const char* re = std::getenv("SEM_HEX_ROWS");
+  c->hex->rows = re ? std::atoi(re) != 0 : c->n <= 8;
+  const char* ze = std::getenv("SEM_HEX_ZMERGE");
+  c->hex->zmerge = (c->hex->rows || HEX_ZMERGE) && !(ze && std::atoi(ze) == 0);
   return SEM_OK;
 }
 
@@ -516,11 +536,11 @@ int set_map(sem_ctx* c, const uint32_t* d_e2n, hipStream_t st) {
       c->n_cu = ncu;
   }
   int wpc = 0, rc = SEM_OK;
-  HEX_DISPATCH(rc, N, hex_wgs_per_cu, &wpc);
+  HEX_DISPATCH(rc, N, hex_wgs_per_cu, H->rows, &wpc);
   if (rc) return rc;
   const int64_t resident = (int64_t)std::max(c->n_cu, 1) * std::max(wpc, 1);
   HexPlanHost P;
-  rc = hex_build_plan(h, c->n_elem, c->n_node, N, resident, P);
+  rc = hex_build_plan(h, c->n_elem, c->n_node, N, resident, H->zmerge, P);
   if (rc) return rc;
   c->epoch++;
   c->map_epoch++;
@@ -658,12 +678,14 @@ int plan_info(const sem_ctx* c, int64_t* info, int n_info) {
   // [4] element slots per workgroup, [5] chains (maximal), [6] sub-chain
   // length cap, [7] launch positions, [8] sub-chains, [9] seam nodes,
   // [10] slotted writes, [11] plain stores, [12] threads per workgroup,
-  // [13] ndim (3), [14] geometry ready
+  // [13] ndim (3), [14] geometry ready, [15] action kernel (1 row form,
+  // 0 three-block), [16] z-merge in the plan
   const int64_t v[] = {H->n_wg,        H->n_zero, 0,
                        1,              H->slots,  H->n_chains,
                        H->chain_len,   H->n_pos,  H->n_subchains,
                        H->n_seam,      H->n_seam_writes, H->n_direct,
-                       H->threads,     3,         H->have_G ? 1 : 0};
+                       H->threads,     3,         H->have_G ? 1 : 0,
+                       H->rows ? 1 : 0, H->zmerge ? 1 : 0};
   const int nv = (int)(sizeof(v) / sizeof(v[0]));
   for (int i = 0; i < n_info; ++i) info[i] = i < nv ? v[i] : 0;
   return SEM_OK;

@@ -253,7 +253,8 @@ class SEMOperator(object):
                         slots_per_workgroup=v[4], chains=v[5], chain_length_cap=v[6],
                         positions=v[7], subchains=v[8], seam_nodes=v[9], slotted_writes=v[10],
                         plain_stores=v[11], threads=v[12], geometry="stored",
-                        kernel="column", plan="chains-seams")
+                        kernel="column", plan="chains-seams",
+                        hex_kernel="rows" if v[15] else "three_block", zmerge=bool(v[16]))
         counts = [x for x in v[8:8 + v[5]]]
         while counts and counts[-1] == 0:
             counts.pop()

@@ -95,6 +95,31 @@ def test_hex_orders_vs_oracle(sem, gll, p):
     assert info["ndim"] == 3 and info["chains"] == ne * (ne - 1 if ne > 2 else 2)
 
 
+@pytest.mark.parametrize("p", [3, 6, 8, 10])
+@pytest.mark.parametrize("form", ["rows_zmerge", "rows", "three_block"])
+def test_hex_kernel_forms_vs_oracle(sem, gll, monkeypatch, p, form):
+    """Both action kernels at every order class, whatever AUTO picks: the row
+    form (with and without the xi2-face z-merge) and the three-block kernel,
+    overwrite and accumulate, on a warped mesh with several slots per
+    workgroup and broken sub-chains."""
+    from spectralelementmethod_amd import meshgen
+    monkeypatch.setenv("SEM_HEX_ROWS", "0" if form == "three_block" else "1")
+    monkeypatch.setenv("SEM_HEX_ZMERGE", "1" if form == "rows_zmerge" else "0")
+    ne = {3: 4, 6: 3}.get(p, 2)
+    nodes, e2n = meshgen.structured_cube(ne + 2, ne + 1, ne, p, warp=0.05)
+    P = _oracle(gll, nodes, e2n, p)
+    op = sem.SEMOperator(p, e2n, nodes)
+    rng = np.random.default_rng(10 + p)
+    u = rng.standard_normal(P.ndof)
+    y0 = rng.standard_normal(P.ndof)
+    ref = P.apply(u)
+    y = op.apply(torch.from_numpy(u).cuda()).cpu().numpy()
+    assert rel_l2(y, ref) < TOL
+    yt = torch.from_numpy(y0.copy()).cuda()
+    op.apply(torch.from_numpy(u).cuda(), out=yt, accumulate=True)
+    assert rel_l2(yt.cpu().numpy(), y0 + ref) < TOL
+
+
 def _permute_local(e2n, rng, frac=0.5):
     """Re-orient a fraction of the elements (swap / reverse local axes): the
     mesh is the same, the xi0 chains break wherever orientations differ."""
