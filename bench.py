@@ -317,16 +317,31 @@ def bench_hex(args):
         op.apply(u, out=y)
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     events = [(ev(), ev()) for _ in range(args.steps)]
+    region = (ev(), ev())
+    each = args.step_events == "each"
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for k in range(args.steps):
-        events[k][0].record()
+        if each:
+            events[k][0].record()
+        elif k == 0:
+            region[0].record()
         op.apply(u, out=y)
-        events[k][1].record()
+        if each:
+            events[k][1].record()
+        elif k == args.steps - 1:
+            region[1].record()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
+    if not each:  # untimed: per-action quartiles
+        for k in range(args.steps):
+            events[k][0].record()
+            op.apply(u, out=y)
+            events[k][1].record()
+        torch.cuda.synchronize()
     kern_ms = [a.elapsed_time(b) for a, b in events]
-    kern_avg_s = float(np.mean(kern_ms)) / 1e3
+    kern_avg_s = (float(np.mean(kern_ms)) if each else
+                  region[0].elapsed_time(region[1]) / args.steps) / 1e3
     parity = None
     if not args.no_check:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -364,8 +379,12 @@ def bench_hex(args):
             "parallelism": "single GPU" if world == 1 else "%d independent replicas" % world,
             "kernel_ms_avg": kern_avg_s * 1e3, "kernel_ms_min": float(np.min(kern_ms)),
             "kernel_ms_quartiles": [float(q) for q in np.percentile(kern_ms, [25, 50, 75])],
-            "kernel_ms_note": "HIP events around each sem_apply on the launch stream: the "
-                              "element kernel + the seam-sum kernel",
+            "kernel_ms_note": ("HIP events around each sem_apply on the launch stream: the "
+                               "element kernel + the seam-sum kernel" if each else
+                               "HIP events around the K timed sem_apply calls / K (element "
+                               "kernel + seam sum + the gaps); min / quartiles from per-action "
+                               "events of a second, untimed pass"),
+            "step_events": args.step_events,
             "gflops_kernel": F / kern_avg_s / 1e9, "gpu_setup_sec": t_setup,
             "plan": plan,
         },
@@ -594,9 +613,13 @@ def main():
                     help="interface sum with several ranks: native RCCL or torch.distributed")
     ap.add_argument("--pcg-rtol", type=float, default=0.0,
                     help="--op pcg: 0 = time exactly --steps iterations; > 0 = solve to it")
-    ap.add_argument("--step-events", choices=["each", "region"], default="each",
-                    help="HIP events around every timed action, or one pair around the "
-                         "timed region (per-action quartiles then from an untimed pass)")
+    # region (default): one HIP event pair around the K timed actions; a pair
+    # around every action costs the step ~10 us of queue markers (one rank of
+    # the 8-strip split: 0.107 against 0.095-0.098 ms per step; the driver
+    # command 0.636-0.644 against 0.622-0.637, profiles/r05/step_events/)
+    ap.add_argument("--step-events", choices=["each", "region"], default="region",
+                    help="one HIP event pair around the timed region (per-action quartiles "
+                         "then from an untimed pass), or a pair around every timed action")
     ap.add_argument("--kernel-series", action="store_true",
                     help="also write every timed action's HIP-event time into the JSON")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -1002,15 +1025,19 @@ def time_rank(args):
             after_warmup()
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(steps)]
+        each = args.step_events == "each"  # region: one pair around the steps
         t0 = time.perf_counter()
-        for a, b in ev:
-            a.record(main)
+        for k, (a, b) in enumerate(ev):
+            if each or k == 0:
+                a.record(main)
             fn()
-            b.record(main)
+            if each or k == steps - 1:
+                b.record(main)
         t_enq = time.perf_counter() - t0
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
-        ms = [a.elapsed_time(b) for a, b in ev]
+        ms = ([a.elapsed_time(b) for a, b in ev] if each else
+              [ev[0][0].elapsed_time(ev[-1][1]) / steps])
         return dict(wall_ms_per_step=wall / steps * 1e3, event_ms_avg=float(np.mean(ms)),
                     event_ms_quartiles=[float(q) for q in np.percentile(ms, [25, 50, 75])],
                     host_enqueue_ms_per_step=t_enq / steps * 1e3)
