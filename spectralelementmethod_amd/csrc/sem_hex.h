@@ -62,13 +62,13 @@ struct HexLaunch {
 
 enum { HEX_SET = 0, HEX_ACC = 1, HEX_DIAG = 2 };
 
-// z-merge (xi2 faces between the slots of a workgroup summed in LDS): off by
-// default -- at n = 9 its exchange buffer (1.3 KB) takes the workgroup past
-// 54,272 bytes, the most that three 512-byte-granular allocations fit in the
-// 160 KB of a CU; measured with it on (profiles/r05/hex/): seam sum 47 -> 33
-// us, element kernel 225 -> 241 us at two workgroups per CU
+// z-merge (xi2 faces between the slots of a workgroup summed in LDS, one
+// writer fewer per merged node) in the three-block kernel: the exchange
+// goes through its w1 block (no LDS of its own); the plan decides at run
+// time (SEM_HEX_ZMERGE=0 in the environment turns it off); building with
+// -DSEM_HEX_ZMERGE=0 removes the code
 #ifndef SEM_HEX_ZMERGE
-#define SEM_HEX_ZMERGE 0
+#define SEM_HEX_ZMERGE 1
 #endif
 constexpr bool HEX_ZMERGE = SEM_HEX_ZMERGE != 0;
 
@@ -108,12 +108,11 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
   __shared__ double sU[S * N3];
   __shared__ double sA[S * N3];
   __shared__ double sB[S * N3];
-  // z-merge: the xi2 = 0 face of slot s (s >= 1) handed to slot s-1; slot 0
-  // never gives, so S-1 faces (n = 9: 1.3 KB, 54,456 bytes in all -- one
-  // 512-byte granule past three workgroups per CU).  Always in the diagonal
-  // (setup) kernel, which runs on the row form's z-merged plans.
-  constexpr bool ZM = HEX_ZMERGE || MODE == HEX_DIAG;
-  __shared__ double sX[ZM && S > 1 ? (S - 1) * N2 : 1];
+  // z-merge: the xi2 = 0 face of slot s (s >= 1) handed to slot s-1 through
+  // the w1 block, free once every thread has finished the transposed pass
+  // (a buffer of its own, 1.3 KB at n = 9, took the workgroup one 512-byte
+  // granule past three per CU: element kernel 225 -> 241 us)
+  constexpr bool ZM = HEX_ZMERGE;
   const int tid = threadIdx.x;
   for (int i = tid; i < N2; i += T) sD[i] = gD[i];
   const int w = blockIdx.x;
@@ -261,13 +260,15 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
       __syncthreads();  // su / sa / sb are rewritten by the next element
     }
     if (ZM && wg_merge) {  // workgroup-uniform
+      // the diagonal branch ends on a barrier already
+      if constexpr (MODE != HEX_DIAG) __syncthreads();  // sA / sB reads done
       if (give)
 #pragma unroll
-        for (int a = 0; a < N; ++a) sX[(sl - 1) * N2 + a * N + b] = yv[a];
+        for (int a = 0; a < N; ++a) sA[(sl - 1) * N2 + a * N + b] = yv[a];
       __syncthreads();
       if (take)
 #pragma unroll
-        for (int a = 0; a < N; ++a) yv[a] += sX[sl * N2 + a * N + b];
+        for (int a = 0; a < N; ++a) yv[a] += sA[sl * N2 + a * N + b];
     }
     if (active && !give) {
       if (k > 0) yv[0] += carry;

@@ -36,11 +36,11 @@ struct HexState {
   uint32_t* d_map = nullptr;   // the library's copy of the caller's map [E][n][n][n]
   double* d_G = nullptr;       // stored factors [E][n^3][6]
   bool have_G = false;
-  // the action's kernel: k_hex_rows (row form; p <= 7) or k_hex_poisson
-  // (always for the diagonal)
+  // the action's kernel: k_hex_poisson (three-block, default) or k_hex_rows
+  // (row form, SEM_HEX_ROWS=1; the diagonal always runs k_hex_poisson)
   bool rows = true;
-  // xi2 faces between the slots of a workgroup summed in LDS (the row form
-  // by default; the three-block kernel only when built with SEM_HEX_ZMERGE)
+  // xi2 faces between the slots of a workgroup summed in LDS (both kernels;
+  // SEM_HEX_ZMERGE=0 turns it off)
   bool zmerge = false;
   // diagnostics (sem_plan_info)
   int64_t n_chains = 0, n_subchains = 0, chain_len = 0, n_direct = 0;
@@ -501,13 +501,13 @@ int ctx_init(sem_ctx* c) {
   c->hex->threads = hex_threads(c->n);
   c->hex->nbc = hex_nbc(c->n);
   // the row form needs the z-merge off (it has no face exchange)
-  // measured per order (profiles/r05/hex/rows/): the row form
-  // with the z-merge is 8-10 % faster at p = 2 / 4 / 6, ties at p = 8 and
-  // loses at p = 10; SEM_HEX_ROWS=0 / 1 overrides
+  // the row form only on request (SEM_HEX_ROWS=1): with the z-merge in both
+  // kernels the three-block kernel is as fast or faster at every order
+  // measured (p = 2 / 4 / 6, DESIGN.md §4.9, profiles/r05/hex/zmerge_w1/)
   const char* re = std::getenv("SEM_HEX_ROWS");
-  c->hex->rows = re ? std::atoi(re) != 0 : c->n <= 8;
+  c->hex->rows = re && std::atoi(re) != 0;
   const char* ze = std::getenv("SEM_HEX_ZMERGE");
-  c->hex->zmerge = (c->hex->rows || HEX_ZMERGE) && !(ze && std::atoi(ze) == 0);
+  c->hex->zmerge = HEX_ZMERGE && !(ze && std::atoi(ze) == 0);
   return SEM_OK;
 }
 

@@ -96,15 +96,15 @@ def test_hex_orders_vs_oracle(sem, gll, p):
 
 
 @pytest.mark.parametrize("p", [3, 6, 8, 10])
-@pytest.mark.parametrize("form", ["rows_zmerge", "rows", "three_block"])
+@pytest.mark.parametrize("form", ["rows_zmerge", "rows", "three_block_zmerge", "three_block"])
 def test_hex_kernel_forms_vs_oracle(sem, gll, monkeypatch, p, form):
     """Both action kernels at every order class, whatever AUTO picks: the row
-    form (with and without the xi2-face z-merge) and the three-block kernel,
-    overwrite and accumulate, on a warped mesh with several slots per
-    workgroup and broken sub-chains."""
+    form and the three-block kernel, each with and without the xi2-face
+    z-merge, overwrite and accumulate, on a warped mesh with several slots
+    per workgroup and broken sub-chains."""
     from spectralelementmethod_amd import meshgen
-    monkeypatch.setenv("SEM_HEX_ROWS", "0" if form == "three_block" else "1")
-    monkeypatch.setenv("SEM_HEX_ZMERGE", "1" if form == "rows_zmerge" else "0")
+    monkeypatch.setenv("SEM_HEX_ROWS", "1" if form.startswith("rows") else "0")
+    monkeypatch.setenv("SEM_HEX_ZMERGE", "1" if form.endswith("zmerge") else "0")
     ne = {3: 4, 6: 3}.get(p, 2)
     nodes, e2n = meshgen.structured_cube(ne + 2, ne + 1, ne, p, warp=0.05)
     P = _oracle(gll, nodes, e2n, p)
@@ -113,11 +113,19 @@ def test_hex_kernel_forms_vs_oracle(sem, gll, monkeypatch, p, form):
     u = rng.standard_normal(P.ndof)
     y0 = rng.standard_normal(P.ndof)
     ref = P.apply(u)
+    info = op.plan_info()
+    assert info["hex_kernel"] == ("rows" if form.startswith("rows") else "three_block")
+    assert info["zmerge"] == form.endswith("zmerge")
     y = op.apply(torch.from_numpy(u).cuda()).cpu().numpy()
     assert rel_l2(y, ref) < TOL
     yt = torch.from_numpy(y0.copy()).cuda()
     op.apply(torch.from_numpy(u).cuda(), out=yt, accumulate=True)
     assert rel_l2(yt.cpu().numpy(), y0 + ref) < TOL
+    if form.endswith("zmerge") and p <= 6:  # the diagonal runs on the z-merged plan too
+        L = P.element_matrices()
+        dref = np.bincount(P.e2n.reshape(P.e2n.shape[0], -1).ravel(),
+                           weights=np.einsum("eii->ei", L).ravel(), minlength=P.ndof)
+        assert rel_l2(op.diag().cpu().numpy(), dref) < TOL
 
 
 def _permute_local(e2n, rng, frac=0.5):
