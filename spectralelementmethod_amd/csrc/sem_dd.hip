@@ -1200,6 +1200,19 @@ int sem_rccl_unique_id(void* h_id, int nbytes) {
   return SEM_OK;
 }
 
+// the events that order the side stream against the caller's stream (one
+// device) are recorded without the system-scope fence
+// (hipEventDisableSystemFence): every buffer they order is written and read
+// by kernels of this device (RCCL's kernel copies into d_recv itself), whose
+// own end-of-kernel release publishes their stores device-wide.  One rank
+// of the 8-strip split: 0.0924 against 0.0944-0.0961 ms per step
+// (profiles/r05/dd/event_fence/); SEM_DD_EVENT_FENCE=system restores it.
+static unsigned dd_event_flags() {
+  const char* e = std::getenv("SEM_DD_EVENT_FENCE");
+  const bool system = e && std::string(e) == "system";
+  return hipEventDisableTiming | (system ? 0u : hipEventDisableSystemFence);
+}
+
 int sem_dd_create(sem_dd** out, sem_ctx* iface, sem_ctx* interior, int64_t ndof_local,
                   const uint32_t* d_iface_dofs, int64_t n_iface_dofs, int n_peers,
                   const int* h_peers, const int64_t* h_peer_counts, const uint32_t* d_peer_dofs,
@@ -1253,8 +1266,8 @@ int sem_dd_create(sem_dd** out, sem_ctx* iface, sem_ctx* interior, int64_t ndof_
       bad(hipMalloc(&d->d_send, std::max<int64_t>(ne, 1) * sizeof(double))) ||
       bad(hipMalloc(&d->d_recv, std::max<int64_t>(ne, 1) * sizeof(double))) ||
       bad(hipStreamCreateWithFlags(&d->side, hipStreamNonBlocking)) ||
-      bad(hipEventCreateWithFlags(&d->ev0, hipEventDisableTiming)) ||
-      bad(hipEventCreateWithFlags(&d->ev1, hipEventDisableTiming)))
+      bad(hipEventCreateWithFlags(&d->ev0, dd_event_flags())) ||
+      bad(hipEventCreateWithFlags(&d->ev1, dd_event_flags())))
     return fail(SEM_E_HIP, "sem_dd_create: HIP allocation failed");
   if (n_iface_dofs && bad(hipMemcpy(d->d_cidx, d_iface_dofs, n_iface_dofs * sizeof(uint32_t),
                                     hipMemcpyDeviceToDevice)))
