@@ -1,4 +1,6 @@
 #!/bin/bash
+# (SEM_DD_CU_SIDE was removed after this measurement, profiles/r05/dd/cu_split/;
+#  the script documents how it was run)
 # CU split of the decomposition step (SEM_DD_CU_SIDE = K CUs for the side
 # stream), one rank of the 8-strip split timed alone with RCCL to itself,
 # alternating with K = 0.   tools/gpu_dd_cu.sh OUT K...

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (SEM_DD_IFACE_FIRST was removed after this measurement, profiles/r05/dd/iface_first/;
+#  the script documents how it was run)
 # Interface elements before the interior (SEM_DD_IFACE_FIRST): tests, then one rank of the 8-strip split
 # timed alone (RCCL to itself) with it on / off, alternating.
 #   tools/gpu_dd_ifirst.sh OUT (tests with it on)

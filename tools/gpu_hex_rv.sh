@@ -1,4 +1,6 @@
 #!/bin/bash
+# (SEM_HEX_RV existed only in the variant build of that measurement,
+#  profiles/r05/hex/rows/rows_per_barrier/; the script documents how it was run)
 # Row-form variants (SEM_HEX_RV = 10 * rows per barrier + map reload at the
 # store) against the three-block kernel, alternating:
 #   tools/gpu_hex_rv.sh OUT p...
