@@ -11,7 +11,8 @@ region.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--p 8] [--nex 1024] [--ney 1024]
                   [--scaling strong|weak] [--op poisson|axisym_stokes|axisym_ns|pcg]
-  python bench.py --dim 3 [--p 8] [--hex-ne 27]     (hexahedra, one GPU; bench_hex)
+  python bench.py --dim 3 [--p 8] [--hex-ne 27] [--hex-nex L] [--gpus N]
+                  (hexahedra; N ranks = slabs of element layers along x, bench_hex)
 
 --gpus N without a launcher: this process starts N rank processes (before
 touching the GPU) and waits for them; under torchrun (WORLD_SIZE set) each
@@ -284,107 +285,198 @@ def cpu_baseline_hex(p, warp, budget_s=20.0, workers=16):
     return out
 
 
+def _hex_partition(args, world, rank):
+    """The hexahedral workload split into `world` slabs of element layers
+    along x (distributed.SlabPartition, row N3): --hex-ne^3 warped hexahedra
+    (--hex-nex layers along x if given); --scaling weak gives every rank that
+    many layers."""
+    from spectralelementmethod_amd.distributed import SlabPartition
+    ne = args.hex_ne
+    nex = args.hex_nex or ne
+    if args.scaling == "weak":
+        nex *= world
+    return SlabPartition(nex, ne, ne, args.p, world, rank)
+
+
+def hex_parity_checks(op, y, u, part, p, warp, dev, world):
+    """Parity of the timed hexahedral output against the NumPy oracle
+    (HexPoissonProblem).  One rank: the whole mesh.  Several ranks: (a) two
+    element layers in the middle of the rank's slab, compared on the inner
+    node layers of the block; (b) the two layers across the rank's right
+    face, [ex1 - 1, ex1 + 1) (the neighbour's u regenerated from the global
+    field), compared on this rank's node layers of the block, the last being
+    the shared face whose value exists only after the exchange."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import sem_oracle
+    from spectralelementmethod_amd import meshgen
+    gll = np.load(os.path.join(ROOT, "tests", "golden", "gll.npz"))
+    half = gll["half_%d" % p]
+
+    def rel(a, b):
+        return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+    t0 = time.perf_counter()
+    if world == 1:
+        nodes, e2n = part.local_mesh(warp)
+        ref = sem_oracle.HexPoissonProblem(nodes, e2n, half).apply(u.cpu().numpy())
+        return {"rel_l2": rel(y.cpu().numpy(), ref), "tolerance": 1e-10,
+                "vs": "oracle/sem_oracle.py HexPoissonProblem (whole mesh)",
+                "oracle_sec": time.perf_counter() - t0}, None
+    face = part.face
+    nl = part.ex1 - part.ex0
+    c0 = part.ex0 + max(0, (nl - 2) // 2)
+    c1 = min(part.ex1, c0 + 2)
+    nodes, e2n, off = meshgen.structured_slab(part.nex, part.ney, part.nez, p, c0, c1, warp)
+    loc = off - part.node_offset + np.arange(nodes.shape[1])
+    y_ref = sem_oracle.HexPoissonProblem(nodes, e2n, half).apply(
+        u[torch_index(loc, dev)].cpu().numpy())
+    inner = np.arange(face, nodes.shape[1] - face)
+    block = {"rel_l2": rel(y[torch_index(loc[inner], dev)].cpu().numpy(), y_ref[inner]),
+             "tolerance": 1e-10, "nodes_checked": int(inner.size),
+             "block": "element layers [%d, %d) of the slab" % (c0, c1),
+             "vs": "oracle/sem_oracle.py HexPoissonProblem"}
+    iface = None
+    if part.rank < world - 1:
+        c0 = part.ex1 - 1
+        nodes, e2n, off = meshgen.structured_slab(part.nex, part.ney, part.nez, p, c0, c0 + 2,
+                                                  warp)
+        gids = off + np.arange(nodes.shape[1])
+        y_ref = sem_oracle.HexPoissonProblem(nodes, e2n, half).apply(
+            global_field_at(part, gids, dev).cpu().numpy())
+        own = np.arange(face, (p + 1) * face)
+        iface = {"rel_l2": rel(y[torch_index(gids[own] - part.node_offset, dev)].cpu().numpy(),
+                               y_ref[own]),
+                 "tolerance": 1e-10, "nodes_checked": int(own.size), "interface_nodes": face,
+                 "block": "element layers [%d, %d) across the face shared with rank %d" % (
+                     c0, c0 + 2, part.rank + 1)}
+    return block, iface
+
+
 def bench_hex(args):
-    """Hexahedral Poisson action on one GPU (row N2: north_star's "structured
-    quad/hex meshes"): --hex-ne^3 warped hexahedra of order p (default p = 8,
-    27^3 = 19,683 elements, 10,218,313 DOF, ~1e7 DOF like config 4).  A step
-    = one sem_apply (element kernel + seam sum).  --gpus N > 1 runs N
-    independent replicas (the hex path has no multi-GPU decomposition yet)."""
+    """Hexahedral Poisson action (rows N2 / N3: north_star's "structured
+    quad/hex meshes ... at 1/2/4/8 GPUs"): --hex-ne^3 warped hexahedra of
+    order p (default p = 8, 27^3 = 19,683 elements, 10,218,313 DOF, ~1e7 DOF
+    like config 4).  One GPU: a step = one sem_apply (element kernel + seam
+    sum).  N ranks: the mesh in N slabs along x (SlabPartition), a step = one
+    sem_dd_apply per rank (interface elements + RCCL face exchange on a side
+    stream, interior elements on the caller's stream, the finish)."""
     import torch
-    from spectralelementmethod_amd import operators, meshgen
+    import torch.distributed as dist
+    from spectralelementmethod_amd.distributed import OverlappedOperator
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.rehearse_one_gpu:
+        local_rank = 0
+        args.transport = "torch"
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    p, ne = args.p, args.hex_ne
+    if world > 1:
+        _init_process_group(args, dev)
+    p = args.p
+    part = _hex_partition(args, world, rank)
     t0 = time.time()
-    nodes, e2n = meshgen.structured_cube(ne, ne, ne, p, warp=args.warp)
-    log("hex mesh %d^3 p=%d: %d elements, %d nodes (%.1fs)" % (ne, p, e2n.shape[0],
-                                                               nodes.shape[1], time.time() - t0))
+    nodes, e2n = part.local_mesh(args.warp)
+    log("rank %d: hex slab %d layers of %dx%dx%d p=%d: %d elements, %d nodes (%.1fs)" % (
+        rank, part.ex1 - part.ex0, part.nex, part.ney, part.nez, p, e2n.shape[0],
+        nodes.shape[1], time.time() - t0))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    op = operators.SEMOperator(p, e2n, nodes, device=dev)
-    op.compute_geometry()
+    op = OverlappedOperator(p, nodes, e2n, part.neighbors if world > 1 else {}, 1, dev,
+                            owned=part.owned, transport=args.transport, world=world, rank=rank)
     torch.cuda.synchronize()
     t_setup = time.perf_counter() - t0
+    del nodes, e2n
     plan = op.plan_info()
-    log("hex plan %s; setup %.2fs" % (plan, t_setup))
-    g = torch.Generator(device=dev).manual_seed(1234)
-    u = torch.randn(op.ndof, dtype=torch.float64, device=dev, generator=g)
+    log("rank %d: hex plan %s; %d interface + %d interior elements; transport %s; setup %.2fs"
+        % (rank, plan, op.n_iface_elem, op.n_interior_elem, op.transport, t_setup))
+    u = global_random_field(part, 1, 0, op.ndof, dev)
     y = torch.empty_like(u)
     for _ in range(args.warmup):
-        op.apply(u, out=y)
+        op.step(u, y)
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     events = [(ev(), ev()) for _ in range(args.steps)]
     region = (ev(), ev())
     each = args.step_events == "each"
+    if world > 1:
+        dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for k in range(args.steps):
         if each:
-            events[k][0].record()
-        elif k == 0:
-            region[0].record()
-        op.apply(u, out=y)
-        if each:
-            events[k][1].record()
-        elif k == args.steps - 1:
-            region[1].record()
+            op.step(u, y, events[k])
+        else:
+            op.step(u, y, (region[0] if k == 0 else None,
+                           region[1] if k == args.steps - 1 else None))
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     elapsed = time.perf_counter() - t_start
     if not each:  # untimed: per-action quartiles
         for k in range(args.steps):
-            events[k][0].record()
-            op.apply(u, out=y)
-            events[k][1].record()
+            op.step(u, y, events[k])
         torch.cuda.synchronize()
     kern_ms = [a.elapsed_time(b) for a, b in events]
     kern_avg_s = (float(np.mean(kern_ms)) if each else
                   region[0].elapsed_time(region[1]) / args.steps) / 1e3
-    parity = None
+    per_rank_ms = [elapsed / args.steps * 1e3]
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+        gathered = [None] * world
+        dist.all_gather_object(gathered, per_rank_ms[0])
+        per_rank_ms = gathered
+    parity, parity_iface, parity_ranks = None, None, None
     if not args.no_check:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import sem_oracle
-        gll = np.load(os.path.join(ROOT, "tests", "golden", "gll.npz"))
-        t0 = time.perf_counter()
-        P = sem_oracle.HexPoissonProblem(nodes, e2n, gll["half_%d" % p])
-        ref = P.apply(u.cpu().numpy())
-        got = y.cpu().numpy()
-        parity = {"rel_l2": float(np.linalg.norm(got - ref) / np.linalg.norm(ref)),
-                  "vs": "oracle/sem_oracle.py HexPoissonProblem (whole mesh)",
-                  "tolerance": 1e-10, "oracle_sec": time.perf_counter() - t0}
-        log("hex parity %s" % parity)
+        parity, parity_iface = hex_parity_checks(op, y, u, part, p, args.warp, dev, world)
+        log("rank %d: hex parity %s; interface %s" % (rank, parity, parity_iface))
         assert parity["rel_l2"] < parity["tolerance"], parity
+        if parity_iface is not None:
+            assert parity_iface["rel_l2"] < parity_iface["tolerance"], parity_iface
+        if world > 1:
+            parity_ranks = [None] * world
+            dist.all_gather_object(parity_ranks, (parity["rel_l2"], None if parity_iface is None
+                                                  else parity_iface["rel_l2"]))
     n_nodes, E = op.ndof, op.n_elem
+    ndof_global = part.global_nodes
     B = alg_bytes_hex(n_nodes, E, p)
     F = alg_flops_hex(E, p)
     achieved = B / kern_avg_s / 1e9
     traffic, traffic_src = None, args.traffic_json
-    if traffic_src is None and (p, ne) == (8, 27):  # profiles/r05/hex/pmc/
+    if traffic_src is None and (p, part.nex, part.ney) == (8, 27, 27) and world == 1:
         traffic_src = os.path.join(ROOT, "bench_traffic", "pmc_traffic_hex_p8_27.json")
     if traffic_src and os.path.exists(traffic_src):
         with open(traffic_src) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
+    hk = plan.get("hex_kernel", "three_block")
     result = {
         "metric": METRIC.replace("Poisson p=8", "Poisson p=%d on hexahedra" % p),
-        "value": n_nodes * world * args.steps / elapsed, "unit": "DOF/s", "n_gpus": world,
+        "value": ndof_global * args.steps / elapsed, "unit": "DOF/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (structured warped hexahedral mesh, u ~ N(0,1))",
         "config": {
-            "workload": "poisson hex p=%d, %d^3 hexahedra (row N2, north_star 'quad/hex')"
-                        % (p, ne),
-            "p": p, "ndim": 3, "geometry": "stored", "n_elem": E, "ndof": n_nodes,
-            "parallelism": "single GPU" if world == 1 else "%d independent replicas" % world,
+            "workload": "poisson hex p=%d, %dx%dx%d hexahedra%s (rows N2/N3, north_star "
+                        "'quad/hex')" % (p, part.nex, part.ney, part.nez,
+                                         " in %d slabs" % world if world > 1 else ""),
+            "p": p, "ndim": 3, "geometry": "stored", "n_elem_global": part.nex * part.ney *
+            part.nez, "n_elem_per_gpu": E, "ndof_global": ndof_global, "ndof_per_gpu": n_nodes,
+            "ranks_seen": world,
+            "parallelism": "single GPU" if world == 1 else (
+                "slabs of element layers along x x%d; interface elements on a side stream, "
+                "face exchange (transport %s) overlapped with the interior elements" % (
+                    world, op.transport)),
+            "per_rank_ms_per_step": per_rank_ms,
+            "exchange_bytes_per_step_per_rank": 2 * op.exchange_bytes,
+            "interface_elements": op.n_iface_elem,
             "kernel_ms_avg": kern_avg_s * 1e3, "kernel_ms_min": float(np.min(kern_ms)),
             "kernel_ms_quartiles": [float(q) for q in np.percentile(kern_ms, [25, 50, 75])],
-            "kernel_ms_note": ("HIP events around each sem_apply on the launch stream: the "
-                               "element kernel + the seam-sum kernel" if each else
-                               "HIP events around the K timed sem_apply calls / K (element "
-                               "kernel + seam sum + the gaps); min / quartiles from per-action "
-                               "events of a second, untimed pass"),
+            "kernel_ms_note": ("HIP events around each step on the launch stream" if each else
+                               "HIP events around the K timed steps / K (element kernel + seam "
+                               "sum + the gaps); min / quartiles from per-step events of a "
+                               "second, untimed pass"),
             "step_events": args.step_events,
+            "decomposition": op.dd_info(),
             "gflops_kernel": F / kern_avg_s / 1e9, "gpu_setup_sec": t_setup,
             "plan": plan,
         },
@@ -394,12 +486,15 @@ def bench_hex(args):
             "traffic_source": os.path.relpath(traffic_src, ROOT) if traffic is not None else None,
             "bytes_model": "16*ndof + 52*E*(p+1)^3 (u, y, 6 factors + uint32 map per element node)",
             "alg_bytes_per_launch": B, "kernel": "%s<%d,0> + k_hex_seam_sum" % (
-                "k_hex_rows" if plan.get("hex_kernel") == "rows" else "k_hex_poisson", p + 1),
+                "k_hex_rows" if hk == "rows" else "k_hex_poisson", p + 1),
             "fp64_tflops": F / kern_avg_s / 1e12, "fp64_peak_tflops": FP64_PEAK_TFLOPS,
         },
     }
     if parity is not None:
         result["parity"] = parity
+    if parity_iface is not None or parity_ranks is not None:
+        result["parity_interface"] = parity_iface
+        result["parity_per_rank"] = parity_ranks
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("timing CPU baseline (hexahedral NumPy oracle, child process)...")
         env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1",
@@ -423,7 +518,27 @@ def bench_hex(args):
     if rank == 0:
         print(json.dumps(result), file=JSON_OUT, flush=True)
     op.close()
+    if world > 1:
+        dist.destroy_process_group()
     return 0
+
+
+def _init_process_group(args, dev):
+    """One rank's process group (gloo for CPU-side objects, NCCL = RCCL for
+    device tensors), stdout kept for the JSON line."""
+    import datetime
+    import torch.distributed as dist
+    # keep stdout for the one JSON line: gloo / RCCL print connection
+    # banners on file descriptor 1 from C++ (they go to stderr instead)
+    global JSON_OUT
+    JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    pg_timeout = datetime.timedelta(seconds=args.deadline)
+    if args.rehearse_one_gpu:
+        dist.init_process_group("gloo", timeout=pg_timeout)
+    else:
+        dist.init_process_group("cpu:gloo,cuda:nccl", device_id=dev, timeout=pg_timeout)
+    dist.barrier()
 
 
 # ---------------------------------------------------------------- launcher
@@ -657,18 +772,21 @@ def main():
     ap.add_argument("--dim", type=int, choices=[2, 3], default=2,
                     help="3: the hexahedral Poisson action (bench_hex)")
     ap.add_argument("--hex-ne", type=int, default=27, help="--dim 3: hexahedra per side")
+    ap.add_argument("--hex-nex", type=int, default=None,
+                    help="--dim 3: element layers along x (the slab axis; default --hex-ne), "
+                         "per rank with --scaling weak")
     args = ap.parse_args()
 
     if args.cpu_baseline_only:  # child process: no GPU
         fn = cpu_baseline_hex if args.dim == 3 else cpu_baseline
         print(json.dumps(fn(args.p, args.warp, args.cpu_budget, args.cpu_workers)))
         return 0
-    if args.dim == 3:
-        return bench_hex(args)
     if args.time_rank is not None:
         return time_rank(args)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return launch_ranks(args.gpus, args.deadline)
+    if args.dim == 3:
+        return bench_hex(args)
 
     import torch
     import torch.distributed as dist
@@ -688,18 +806,7 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
-        # keep stdout for the one JSON line: gloo / RCCL print connection
-        # banners on file descriptor 1 from C++ (they go to stderr instead)
-        global JSON_OUT
-        JSON_OUT = os.fdopen(os.dup(1), "w")
-        os.dup2(2, 1)
-        import datetime
-        pg_timeout = datetime.timedelta(seconds=args.deadline)
-        if args.rehearse_one_gpu:
-            dist.init_process_group("gloo", timeout=pg_timeout)
-        else:
-            dist.init_process_group("cpu:gloo,cuda:nccl", device_id=dev, timeout=pg_timeout)
-        dist.barrier()
+        _init_process_group(args, dev)
 
     opname = args.op
     kind = {"poisson": POISSON, "pcg": POISSON, "axisym_stokes": AXISYM_STOKES,
@@ -1006,7 +1113,8 @@ def time_rank(args):
     os.dup2(2, 1)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    part = StripPartition(args.nex, args.ney, p, N, R)
+    hexa = args.dim == 3
+    part = _hex_partition(args, N, R) if hexa else StripPartition(args.nex, args.ney, p, N, R)
     nodes, e2n = part.local_mesh(args.warp)
     op = OverlappedOperator(p, nodes, e2n, part.neighbors, 1, dev, owned=part.owned,
                             transport=args.time_rank_transport, world=1, rank=0, decompose=True)
@@ -1076,6 +1184,7 @@ def time_rank(args):
                                       _lib.tptr(send), sp))
         side = timed(side_chain, K, W)
     iface_elems, interior_elems = op.n_iface_elem, op.n_interior_elem
+    exch_bytes = op.exchange_bytes
     plan_int = op.interior.plan_info() if op.interior is not None else None
     plan_if = op.iface.plan_info() if op.iface is not None else None
     ndof = op.ndof
@@ -1085,7 +1194,7 @@ def time_rank(args):
     # the single-GPU step of the whole mesh on this box (the strong-scaling base)
     single = None
     if not args.no_check:
-        full = StripPartition(args.nex, args.ney, p, 1, 0)
+        full = _hex_partition(args, 1, 0) if hexa else StripPartition(args.nex, args.ney, p, 1, 0)
         nodes, e2n = full.local_mesh(args.warp)
         op1 = OverlappedOperator(p, nodes, e2n, {}, 1, dev, world=1, rank=0)
         del nodes, e2n
@@ -1098,8 +1207,12 @@ def time_rank(args):
         "mode": "time-rank (%s transport: the exchange returns this rank's own values; "
                 "timing only, the result is NOT the global action)" % args.time_rank_transport,
         "transport": args.time_rank_transport,
-        "rank": R, "of_ranks": N, "p": p, "mesh": "%dx%d" % (args.nex, args.ney),
-        "strip_elements": "%d x %d" % (part.ex1 - part.ex0, part.ney), "ndof_rank": ndof,
+        "rank": R, "of_ranks": N, "p": p,
+        "mesh": ("%dx%dx%d hexahedra (%s scaling)" % (part.nex, part.ney, part.nez, args.scaling)
+                 if hexa else "%dx%d" % (args.nex, args.ney)),
+        "strip_elements": ("%d x %d x %d" % (part.ex1 - part.ex0, part.ney, part.nez) if hexa
+                           else "%d x %d" % (part.ex1 - part.ex0, part.ney)), "ndof_rank": ndof,
+        "exchange_bytes_per_step": 2 * exch_bytes,
         "peers": sorted(part.neighbors), "interface_elements": iface_elems,
         "interior_elements": interior_elems, "steps": K, "warmup": W,
         "step": step, "interior_alone": interior, "side_chain_alone": side,

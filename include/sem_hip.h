@@ -500,7 +500,13 @@ int sem_copy_async(void* dst, const void* src, int64_t nbytes, void* stream);
  * exchange), eager steps only: [12] enqueueing the side-stream part (gather,
  * interface elements, pack), [13] the interior elements, [14] the finish;
  * [15] bit 0: the interior's zero list folded into the finish, bit 1: the
- * interior's seam sum fused with the finish (one launch). */
+ * interior's seam sum fused with the finish (one launch), bit 2: the
+ * interface seam sum fused with the pack, bit 3: the finish split around the
+ * join, bit 4: the stream-join events are recorded without the system-scope
+ * fence (only the one-device transports, loopback and RCCL to self, unless
+ * SEM_DD_EVENT_FENCE=system|device forces a scope).
+ * Hexahedral contexts (sem_ctx_create_nd, ndim 3) are accepted for both
+ * iface and interior (interface context over the local numbering). */
 int sem_dd_info(sem_dd* dd, int64_t* info, int n_info);
 
 /* Captured step (default off; SEM_DD_GRAPH=1 in the environment turns it

@@ -519,6 +519,7 @@ struct sem_dd {
                                 // on a one-rank communicator (sem_dd_set_rccl_self)
   hipStream_t side = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool ev_system = true;  // the events carry the system-scope fence (dd_fence_system)
   // transport: native RCCL communicator, or caller callbacks
   ncclComm_t comm = nullptr;
   sem_exchange_fn xfn = nullptr;
@@ -875,9 +876,11 @@ int dd_join(sem_dd* d, hipStream_t st) {
 
 int dd_finish(sem_dd* d, double* y, hipStream_t st) {
   const auto t0 = Clock::now();
-  SEM_TRY(dd_finish_pre(d, y, st));
-  SEM_TRY(dd_join(d, st));
-  const int rc = dd_add(d, y, st);
+  int rc = dd_finish_pre(d, y, st);
+  if (!rc) rc = dd_join(d, st);
+  if (!rc) rc = dd_add(d, y, st);
+  // cleared on every exit: a flag left set by a failed
+  // join would make the next captured finish run only its post part
   d->split_pre_done = false;
   d->host_ns_finish += ns_since(t0);
   return rc;
@@ -913,6 +916,7 @@ int capture(hipStream_t s, F body, hipGraphExec_t* out) {
 
 int dd_capture(sem_dd* d, int op_kind, const double* u, double* y) {
   drop_graphs(d);
+  d->split_pre_done = false;  // the captured finish is the whole finish
   if (!d->cap) HIP_TRY(hipStreamCreateWithFlags(&d->cap, hipStreamNonBlocking));
   if (d->iface) SEM_TRY(capture(d->side, [&] { return dd_side(d, op_kind, false, u, d->side); }, &d->gS));
   SEM_TRY(capture(d->cap, [&] { return dd_main(d, op_kind, false, u, y, d->cap); }, &d->gM));
@@ -1200,17 +1204,43 @@ int sem_rccl_unique_id(void* h_id, int nbytes) {
   return SEM_OK;
 }
 
-// the events that order the side stream against the caller's stream (one
-// device) are recorded without the system-scope fence
-// (hipEventDisableSystemFence): every buffer they order is written and read
-// by kernels of this device (RCCL's kernel copies into d_recv itself), whose
-// own end-of-kernel release publishes their stores device-wide.  One rank
-// of the 8-strip split: 0.0924 against 0.0944-0.0961 ms per step
-// (profiles/r05/dd/event_fence/); SEM_DD_EVENT_FENCE=system restores it.
-static unsigned dd_event_flags() {
+// Scope of the fence of the two events that order the side stream against
+// the caller's stream.  Device scope (hipEventDisableSystemFence)
+// only for the one-device transports -- the loopback copy and RCCL to this
+// rank itself -- where every store into the buffers the events order is made
+// by a kernel of this device and published device-wide by its own
+// end-of-kernel release (one rank of the 8-strip split: 0.0924 against
+// 0.0944-0.0961 ms per step, profiles/r05/dd/event_fence/).  A real peer
+// exchange keeps the system-scope fence: with several ranks, RCCL's P2P
+// transport may have the PEER's kernel or a copy engine write the receive
+// side over xGMI, and the callback transport's host-staged copies land
+// through the copy engines; what the device-scope release orders there is
+// not established, so it is not assumed.  SEM_DD_EVENT_FENCE=system /
+// device forces either scope for every transport (A/B and tests).
+static bool dd_fence_system(const sem_dd* d) {
   const char* e = std::getenv("SEM_DD_EVENT_FENCE");
-  const bool system = e && std::string(e) == "system";
+  if (e && std::string(e) == "system") return true;
+  if (e && std::string(e) == "device") return false;
+  return !(d->loopback || d->rccl_self);
+}
+
+static unsigned dd_event_flags(bool system) {
   return hipEventDisableTiming | (system ? 0u : hipEventDisableSystemFence);
+}
+
+// (re)creates ev0 / ev1 with the fence scope the current transport needs
+// (transports are set up before the first step; nothing may be in flight)
+static int dd_make_events(sem_dd* d) {
+  const bool sys = dd_fence_system(d);
+  if (d->ev0 && d->ev1 && d->ev_system == sys) return SEM_OK;
+  HIP_TRY(hipDeviceSynchronize());
+  if (d->ev0) (void)hipEventDestroy(d->ev0);
+  if (d->ev1) (void)hipEventDestroy(d->ev1);
+  d->ev0 = d->ev1 = nullptr;
+  HIP_TRY(hipEventCreateWithFlags(&d->ev0, dd_event_flags(sys)));
+  HIP_TRY(hipEventCreateWithFlags(&d->ev1, dd_event_flags(sys)));
+  d->ev_system = sys;
+  return SEM_OK;
 }
 
 int sem_dd_create(sem_dd** out, sem_ctx* iface, sem_ctx* interior, int64_t ndof_local,
@@ -1266,9 +1296,10 @@ int sem_dd_create(sem_dd** out, sem_ctx* iface, sem_ctx* interior, int64_t ndof_
       bad(hipMalloc(&d->d_send, std::max<int64_t>(ne, 1) * sizeof(double))) ||
       bad(hipMalloc(&d->d_recv, std::max<int64_t>(ne, 1) * sizeof(double))) ||
       bad(hipStreamCreateWithFlags(&d->side, hipStreamNonBlocking)) ||
-      bad(hipEventCreateWithFlags(&d->ev0, dd_event_flags())) ||
-      bad(hipEventCreateWithFlags(&d->ev1, dd_event_flags())))
+      bad(hipEventCreateWithFlags(&d->ev0, dd_event_flags(true))) ||
+      bad(hipEventCreateWithFlags(&d->ev1, dd_event_flags(true))))
     return fail(SEM_E_HIP, "sem_dd_create: HIP allocation failed");
+  d->ev_system = true;  // no transport yet: the system scope
   if (n_iface_dofs && bad(hipMemcpy(d->d_cidx, d_iface_dofs, n_iface_dofs * sizeof(uint32_t),
                                     hipMemcpyDeviceToDevice)))
     return fail(SEM_E_HIP, "sem_dd_create: copy failed");
@@ -1309,6 +1340,8 @@ void sem_dd_destroy(sem_dd* d) {
   (void)hipFree(d->d_seam_cj);
   (void)hipFree(d->d_rest);
   (void)hipFree(d->d_pack_sj);
+  (void)hipFree(d->d_seam_pre);
+  (void)hipFree(d->d_seam_post);
   if (d->ev0) (void)hipEventDestroy(d->ev0);
   if (d->ev1) (void)hipEventDestroy(d->ev1);
   if (d->side) (void)hipStreamDestroy(d->side);
@@ -1331,7 +1364,7 @@ int sem_dd_init_rccl(sem_dd* d, const void* h_id, int world, int rank) {
   d->rccl_self = false;
   d->world = world;
   d->rank = rank;
-  return SEM_OK;
+  return dd_make_events(d);
 }
 
 int sem_dd_set_rccl_self(sem_dd* d) {
@@ -1350,7 +1383,7 @@ int sem_dd_set_rccl_self(sem_dd* d) {
   d->rank = 0;
   d->loopback = false;
   d->rccl_self = true;
-  return SEM_OK;
+  return dd_make_events(d);
 }
 
 int sem_dd_set_loopback(sem_dd* d) {
@@ -1367,7 +1400,7 @@ int sem_dd_set_loopback(sem_dd* d) {
   d->rank = 0;
   d->loopback = true;
   d->rccl_self = false;
-  return SEM_OK;
+  return dd_make_events(d);
 }
 
 int sem_dd_set_transport(sem_dd* d, sem_exchange_fn xfn, sem_allreduce_fn rfn, void* user,
@@ -1381,12 +1414,12 @@ int sem_dd_set_transport(sem_dd* d, sem_exchange_fn xfn, sem_allreduce_fn rfn, v
   d->user = user;
   d->world = world;
   d->rank = rank;
+  DeviceGuard g(d->device);
   if (d->comm) {
-    DeviceGuard g(d->device);
     (void)ncclCommDestroy(d->comm);
     d->comm = nullptr;
   }
-  return SEM_OK;
+  return dd_make_events(d);
 }
 
 int sem_dd_info(sem_dd* d, int64_t* info, int n_info) {
@@ -1399,7 +1432,7 @@ int sem_dd_info(sem_dd* d, int64_t* info, int n_info) {
                          d->host_ns_side, d->host_ns_main, d->host_ns_finish,
                          (d->defer_zero ? 1 : 0) | (d->seam_fused ? 2 : 0) |
                              (d->pack_fused ? 4 : 0) |
-                             (d->split_finish ? 8 : 0)};
+                             (d->split_finish ? 8 : 0) | (d->ev_system ? 0 : 16)};
   for (int i = 0; i < n_info && i < 16; ++i) info[i] = v[i];
   return SEM_OK;
 }

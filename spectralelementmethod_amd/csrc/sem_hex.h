@@ -269,6 +269,10 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
       if (take)
 #pragma unroll
         for (int a = 0; a < N; ++a) yv[a] += sA[sl * N2 + a * N + b];
+      // the diagonal writes sA (G11) at the top of the next step before any
+      // barrier: every take must have read the merged face first (the
+      // action writes sA only after that step's first barrier)
+      if constexpr (MODE == HEX_DIAG) __syncthreads();
     }
     if (active && !give) {
       if (k > 0) yv[0] += carry;

@@ -500,7 +500,6 @@ int ctx_init(sem_ctx* c) {
   c->hex->slots = hex_slots(c->n);
   c->hex->threads = hex_threads(c->n);
   c->hex->nbc = hex_nbc(c->n);
-  // the row form needs the z-merge off (it has no face exchange)
   // the row form only on request (SEM_HEX_ROWS=1): with the z-merge in both
   // kernels the three-block kernel is as fast or faster at every order
   // measured (p = 2 / 4 / 6, DESIGN.md §4.9, profiles/r05/hex/zmerge_w1/)

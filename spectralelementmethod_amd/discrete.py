@@ -348,10 +348,15 @@ def rcm_permutation(maps, n):
     libsem_hip.so walk the cell map; the graph has sum_cells nloc^2 entries
     and no longer fits a host at 1024^2 cells of order 8).  Degree ties are
     broken by numpy's argsort, as scipy does; equal to scipy's permutation
-    (tests/test_order.py)."""
+    (tests/test_order.py).  Without the built library (host-only use of
+    DOFManager) scipy's RCM of the pair graph gives the same permutation."""
     import ctypes as C
     from . import _lib
-    lib = _lib.load()
+    try:
+        lib = _lib.load()
+    except (ImportError, OSError):
+        from scipy.sparse import csgraph
+        return csgraph.reverse_cuthill_mckee(_pair_graph(np.asarray(maps), n), True)
     cells = np.ascontiguousarray(maps, dtype=np.uint32)
     E, k = cells.shape
     deg = np.empty(n, dtype=np.int32)

@@ -75,6 +75,59 @@ class StripPartition(object):
         return self.node_offset + np.arange(self.n_nodes, dtype=np.int64)
 
 
+class SlabPartition(object):
+    """Hexahedral twin of StripPartition (row N3): contiguous slabs of element
+    layers along x of a structured nex x ney x nez cube
+    (meshgen.structured_cube numbering): rank r owns layers [ex0, ex1), the
+    contiguous global node range [node_offset, node_offset + n_nodes), and
+    shares one node face of Ny*Nz nodes with each neighbouring slab.  The
+    reference's loop this splits is the serial ``for cell in
+    self._mesh.cells`` (sem/discrete.py:189-209) over its N-D tensor layer
+    (sem/basis_functions.py:626-650).  The hexahedral chains run along xi0 =
+    x, so a slab of L layers gives chains of L elements (the planner cuts
+    longer ones anyway, csrc/sem_hex.hip hex_build_plan)."""
+
+    def __init__(self, nex, ney, nez, p, world, rank):
+        if world < 1 or not (0 <= rank < world):
+            raise ValueError("bad world/rank")
+        if nex < world:
+            raise ValueError("fewer element layers than ranks")
+        self.nex, self.ney, self.nez, self.p = nex, ney, nez, p
+        self.world, self.rank, self.dpn = world, rank, 1
+        base, extra = divmod(nex, world)
+        layers = [base + (1 if r < extra else 0) for r in range(world)]
+        starts = np.concatenate([[0], np.cumsum(layers)])
+        self.ex0, self.ex1 = int(starts[rank]), int(starts[rank + 1])
+        self.Ny, self.Nz = ney * p + 1, nez * p + 1
+        self.face = self.Ny * self.Nz
+        self.n_nodes = ((self.ex1 - self.ex0) * p + 1) * self.face
+        self.node_offset = self.ex0 * p * self.face
+        self.n_elem = (self.ex1 - self.ex0) * ney * nez
+        self.neighbors = {}
+        face = np.arange(self.face, dtype=np.int64)
+        if rank > 0:
+            self.neighbors[rank - 1] = face.copy()
+        if rank < world - 1:
+            self.neighbors[rank + 1] = self.n_nodes - self.face + face
+        # a shared node belongs to the lower rank (global dot products)
+        self.owned = np.ones(self.n_nodes, dtype=bool)
+        if rank > 0:
+            self.owned[:self.face] = False
+
+    @property
+    def global_nodes(self):
+        return (self.nex * self.p + 1) * self.face
+
+    def local_mesh(self, warp=0.0):
+        nodes, e2n, off = meshgen.structured_slab(self.nex, self.ney, self.nez, self.p, self.ex0,
+                                                  self.ex1, warp)
+        assert off == self.node_offset and nodes.shape[1] == self.n_nodes
+        return nodes, e2n
+
+    def local_to_global(self):
+        return self.node_offset + np.arange(self.n_nodes, dtype=np.int64)
+
+
 def partition_elements(e2n, nodes, world, method="sfc"):
     """Element -> rank assignment of an arbitrary mesh in equal contiguous
     pieces of a locality-preserving element order:
@@ -92,17 +145,30 @@ def partition_elements(e2n, nodes, world, method="sfc"):
         raise ValueError("need 1 <= world <= number of elements")
     flat = e2n.reshape(E, -1).astype(np.int64)
     if method == "sfc":
-        c = np.asarray(nodes, dtype=np.float64)[:, flat].mean(axis=2)  # [2, E]
+        c = np.asarray(nodes, dtype=np.float64)[:, flat].mean(axis=2)  # [ndim, E]
         lo = c.min(axis=1, keepdims=True)
         span = np.maximum(c.max(axis=1, keepdims=True) - lo, 1e-300)
-        q = np.minimum((c - lo) / span * 65535.0, 65535.0).astype(np.uint64)
+        U = np.uint64
+        if c.shape[0] == 3:  # hexahedra: 21 bits per axis, every third of 63
+            q = np.minimum((c - lo) / span * 2097151.0, 2097151.0).astype(np.uint64)
 
-        def spread(v):  # 16 bits -> every other of 32
-            v = (v | (v << np.uint64(8))) & np.uint64(0x00FF00FF)
-            v = (v | (v << np.uint64(4))) & np.uint64(0x0F0F0F0F)
-            v = (v | (v << np.uint64(2))) & np.uint64(0x33333333)
-            return (v | (v << np.uint64(1))) & np.uint64(0x55555555)
-        order = np.argsort(spread(q[0]) | (spread(q[1]) << np.uint64(1)), kind="stable")
+            def spread3(v):
+                v = (v | (v << U(32))) & U(0x1F00000000FFFF)
+                v = (v | (v << U(16))) & U(0x1F0000FF0000FF)
+                v = (v | (v << U(8))) & U(0x100F00F00F00F00F)
+                v = (v | (v << U(4))) & U(0x10C30C30C30C30C3)
+                return (v | (v << U(2))) & U(0x1249249249249249)
+            key = spread3(q[0]) | (spread3(q[1]) << U(1)) | (spread3(q[2]) << U(2))
+        else:
+            q = np.minimum((c - lo) / span * 65535.0, 65535.0).astype(np.uint64)
+
+            def spread(v):  # 16 bits -> every other of 32
+                v = (v | (v << U(8))) & U(0x00FF00FF)
+                v = (v | (v << U(4))) & U(0x0F0F0F0F)
+                v = (v | (v << U(2))) & U(0x33333333)
+                return (v | (v << U(1))) & U(0x55555555)
+            key = spread(q[0]) | (spread(q[1]) << U(1))
+        order = np.argsort(key, kind="stable")
     elif method == "rcm":
         from scipy import sparse
         from scipy.sparse import csgraph
@@ -610,7 +676,8 @@ class OverlappedOperator(object):
                     host_us_side=v[12] / steps / 1e3, host_us_interior=v[13] / steps / 1e3,
                     host_us_finish=v[14] / steps / 1e3, zero_list_in_finish=bool(v[15] & 1),
                     seam_sum_in_finish=bool(v[15] & 2), seam_sum_in_pack=bool(v[15] & 4),
-                    split_finish=bool(v[15] & 8))
+                    split_finish=bool(v[15] & 8),
+                    event_fence="device" if v[15] & 16 else "system")
 
     def set_graphs(self, enable):
         """Captured step on / off (sem_dd_set_graphs)."""

@@ -93,6 +93,32 @@ def structured_cube(nex, ney, nez, p, warp=0.0, lo=-1.0, hi=1.0):
     return nodes, _element_map3(nex, ney, nez, p, Ny, Nz)
 
 
+def structured_slab(nex, ney, nez, p, ex0, ex1, warp=0.0, lo=-1.0, hi=1.0):
+    """Element layers [ex0, ex1) along x of ``structured_cube(nex, ney, nez,
+    p, warp, lo, hi)`` with the nodes renumbered locally: local id = global id
+    - ex0*p*Ny*Nz (the slab's nodes are one contiguous global range, x-major).
+    The coordinates are slices of the same global linspaces with the same
+    warp expression, so a node on a slab face has bit-identical coordinates
+    in both neighbouring slabs.  Returns nodes [3, n_local], e2n
+    [E_local, n, n, n] (element (ex - ex0, ey, ez) -> id ((ex - ex0)*ney +
+    ey)*nez + ez, as in the cube) and node_offset."""
+    if not (0 <= ex0 < ex1 <= nex):
+        raise ValueError("bad slab [%d, %d) of %d layers" % (ex0, ex1, nex))
+    Nx, Ny, Nz = nex * p + 1, ney * p + 1, nez * p + 1
+    if Nx * Ny * Nz >= 2 ** 32:
+        raise ValueError("mesh too large for a uint32 element map")
+    ix0, ix1 = ex0 * p, ex1 * p + 1
+    X, Y, Z = np.meshgrid(np.linspace(lo, hi, Nx)[ix0:ix1], np.linspace(lo, hi, Ny),
+                          np.linspace(lo, hi, Nz), indexing="ij")
+    if warp:
+        s = warp * np.sin(np.pi * X) * np.sin(np.pi * Y) * np.sin(np.pi * Z)
+        X = X + s
+        Y = Y + 0.5 * s
+        Z = Z - s
+    nodes = np.stack([X.ravel(), Y.ravel(), Z.ravel()])
+    return nodes, _element_map3(ex1 - ex0, ney, nez, p, Ny, Nz), ix0 * Ny * Nz
+
+
 def extrude(nodes2, e2n2, nez, p, z0=0.0, z1=1.0):
     """Sweep a quad mesh (nodes2 [2, N2], e2n2 [E2, n, n]) along z in nez
     uniform layers of order-p elements over [z0, z1].  Node (i2, kz) -> id

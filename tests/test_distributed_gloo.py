@@ -317,3 +317,117 @@ def test_overlapped_protocol_unstructured_sfc_gloo():
     for rank, err, npeer in res:
         assert err < 1e-14, (rank, err)
         assert npeer >= 1
+
+
+# ---------------------------------------------------------------- hexahedra (row N3)
+def test_slab_partition_bookkeeping():
+    """SlabPartition (hexahedral slabs along x): element and owned-node
+    counts add up to the cube, neighbouring slabs agree on their shared face
+    in global numbering, and every slab's local mesh is the global cube's
+    nodes and element map at its global ids, bit for bit."""
+    from spectralelementmethod_amd import meshgen
+    from spectralelementmethod_amd.distributed import SlabPartition
+    nex, ney, nez, p, world = 7, 3, 2, 3, 3
+    gnodes, ge2n = meshgen.structured_cube(nex, ney, nez, p, warp=0.05)
+    parts = [SlabPartition(nex, ney, nez, p, world, r) for r in range(world)]
+    assert sum(pt.n_elem for pt in parts) == nex * ney * nez
+    assert sum(int(pt.owned.sum()) for pt in parts) == parts[0].global_nodes == gnodes.shape[1]
+    e0 = 0
+    for pt in parts:
+        nodes, e2n = pt.local_mesh(0.05)
+        l2g = pt.local_to_global()
+        assert np.array_equal(nodes, gnodes[:, l2g])  # bitwise, incl. the warp
+        ge = ge2n[e0:e0 + pt.n_elem].astype(np.int64)
+        assert np.array_equal(l2g[e2n.astype(np.int64)], ge)
+        e0 += pt.n_elem
+    for a, b in zip(parts[:-1], parts[1:]):
+        ga = a.local_to_global()[a.neighbors[b.rank]]
+        gb = b.local_to_global()[b.neighbors[a.rank]]
+        assert np.array_equal(ga, gb) and ga.size == a.Ny * a.Nz
+    with pytest.raises(ValueError):
+        SlabPartition(2, 3, 3, 2, 4, 0)
+
+
+def _dd_worker_hex(rank, world, port, mode, q):
+    """The overlapped step's protocol (DDPlan + dd_step_reference) on a
+    hexahedral slab / generic partition, hexahedral oracle stand-ins for the
+    two device operators, under gloo."""
+    import sys
+    for pth in (ROOT, os.path.join(ROOT, "oracle")):
+        if pth not in sys.path:
+            sys.path.insert(0, pth)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sem_oracle
+        from spectralelementmethod_amd import meshgen
+        from spectralelementmethod_amd.distributed import (DDPlan, GenericPartition, SlabPartition,
+                                                           dd_step_reference, partition_elements,
+                                                           torch_p2p_exchange)
+        gll = np.load(os.path.join(ROOT, "tests", "golden", "gll.npz"))
+        p, nex, ney, nez = 3, 5, 2, 2
+        half = gll["half_%d" % p]
+        gnodes, ge2n = meshgen.structured_cube(nex, ney, nez, p, warp=0.05)
+        u_glob = np.random.default_rng(6).standard_normal(gnodes.shape[1])
+        y_glob = sem_oracle.HexPoissonProblem(gnodes, ge2n, half).apply(u_glob)
+        if mode == "slab":
+            part = SlabPartition(nex, ney, nez, p, world, rank)
+            nodes, e2n = part.local_mesh(0.05)
+        else:
+            part = GenericPartition(ge2n, partition_elements(ge2n, gnodes, world, "sfc"), world,
+                                    rank)
+            e2n, nodes = part.e2n_local, gnodes[:, part.l2g]
+        plan = DDPlan(e2n, nodes.shape[1], part.neighbors, 1, part.owned)
+        op_i = sem_oracle.HexPoissonProblem(nodes[:, plan.iface_nodes], plan.e2n_iface, half)
+        op_b = sem_oracle.HexPoissonProblem(nodes, e2n[plan.interior_elems], half) \
+            if plan.interior_elems.size else None
+        l2g = part.local_to_global()
+        u = torch.from_numpy(u_glob[l2g].copy())
+        y = dd_step_reference(
+            plan, u, lambda uc: torch.from_numpy(op_i.apply(uc.numpy())),
+            lambda ul: torch.from_numpy(op_b.apply(ul.numpy())),
+            lambda send, peers, counts: torch_p2p_exchange(send, peers, counts))
+        err = np.abs(y.numpy() - y_glob[l2g]).max() / np.abs(y_glob).max()
+        own = torch.from_numpy(np.asarray(plan.not_owned == 0))
+        d = torch.sum(u[own] * y[own]).reshape(1)
+        dist.all_reduce(d)
+        q.put((rank, err, d.item(), float(np.dot(u_glob, y_glob)), plan.exchanged_per_direction,
+               plan.iface_elems.size, plan.interior_elems.size))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,mode", [(2, "slab"), (3, "slab"), (2, "generic")])
+def test_overlapped_protocol_hex_gloo(world, mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dd_worker_hex, args=(r, world, port, mode, q))
+             for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    for rank, err, d, d_ref, nx, n_if, n_in in res:
+        assert err < 1e-14, (rank, err)
+        assert abs(d - d_ref) <= 1e-12 * abs(d_ref)
+        assert nx > 0 and n_if > 0
+
+
+def test_ddplan_hex_slabs():
+    """DDPlan on hexahedral slabs: one element layer per shared face is the
+    interface, the shared faces are touched by interface elements only."""
+    from spectralelementmethod_amd.distributed import DDPlan, SlabPartition
+    for rank in range(3):
+        part = SlabPartition(9, 3, 2, 2, 3, rank)
+        nodes, e2n = part.local_mesh()
+        pl = DDPlan(e2n, part.n_nodes, part.neighbors, 1, part.owned)
+        assert pl.iface_elems.size == len(part.neighbors) * part.ney * part.nez
+        assert np.array_equal(pl.iface_nodes[pl.e2n_iface], e2n[pl.iface_elems])
+        iface = np.concatenate(list(part.neighbors.values()))
+        assert not np.isin(iface, e2n[pl.interior_elems]).any()
+        assert pl.exchanged_per_direction == len(part.neighbors) * part.face
+        assert pl.not_owned.sum() == (part.face if rank > 0 else 0)

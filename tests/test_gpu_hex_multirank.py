@@ -1,0 +1,147 @@
+"""GPU tests of row N3: hexahedral meshes across ranks through the native
+decomposition (csrc/sem_dd.hip, hexahedral contexts from sem_ctx_create_nd).
+
+As in test_gpu_multirank.py, several ranks share the box's one device and
+the interface sum goes through the caller-supplied transport (TorchTransport
+over gloo; RCCL refuses two ranks on one GPU).  Everything else is the
+production step: the interface elements (a hexahedral context over the
+rank's own numbering) on the side stream, pack, exchange, the interior
+elements on the caller's stream, the finish kernel.  The reference loop this
+splits is the serial ``for cell in self._mesh.cells``
+(sem/discrete.py:189-209) over its N-D tensor layer
+(sem/basis_functions.py:626-650).
+
+Tolerances: every rank's action equals the single-GPU hexahedral action on
+its nodes to 1e-12 relative (only the summation order at the shared face
+differs) and the oracle's (HexPoissonProblem) to 1e-10; the diagonal to
+1e-12; the PCG over the decomposition the single-GPU solve to 1e-9."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda", 0)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _hex_worker(rank, world, port, mode, p, nex, ney, nez, q):
+    import sys
+    for pth in (ROOT, os.path.join(ROOT, "oracle")):
+        if pth not in sys.path:
+            sys.path.insert(0, pth)
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sem_oracle
+        from spectralelementmethod_amd import meshgen
+        from spectralelementmethod_amd.distributed import (GenericPartition, OverlappedOperator,
+                                                           SlabPartition, partition_elements)
+        from spectralelementmethod_amd.operators import SEMOperator
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        gnodes, ge2n = meshgen.structured_cube(nex, ney, nez, p, warp=0.05)
+        if mode == "slab":
+            part = SlabPartition(nex, ney, nez, p, world, rank)
+            nodes, e2n = part.local_mesh(0.05)
+        else:  # Morton curve through the hexahedra's centroids
+            part = GenericPartition(ge2n, partition_elements(ge2n, gnodes, world, "sfc"), world,
+                                    rank)
+            e2n, nodes = part.e2n_local, gnodes[:, part.l2g]
+        l2g_np = part.local_to_global().astype(np.int64)
+        l2g = torch.from_numpy(l2g_np).to(dev)
+        op = OverlappedOperator(p, nodes, e2n, part.neighbors, 1, dev, owned=part.owned,
+                                transport="torch", world=world, rank=rank)
+        full = SEMOperator(p, ge2n, gnodes, device=dev)
+        g = torch.Generator(device=dev).manual_seed(31)
+        u_glob = torch.randn(full.ndof, dtype=torch.float64, device=dev, generator=g)
+        y_full = full.apply(u_glob)
+        y_ref = y_full[l2g]
+        u = u_glob[l2g].contiguous()
+        y = torch.full_like(u, 7.0)
+        errs = []
+        for _ in range(3):  # repeated steps reuse the buffers and the side stream
+            op.step(u, y)
+            errs.append(((y - y_ref).norm() / y_ref.norm()).item())
+        gll = np.load(os.path.join(ROOT, "tests", "golden", "gll.npz"))
+        ref = sem_oracle.HexPoissonProblem(gnodes, ge2n, gll["half_%d" % p]).apply(
+            u_glob.cpu().numpy())[l2g_np]
+        err_oracle = float(np.linalg.norm(y.cpu().numpy() - ref) / np.linalg.norm(ref))
+        d = op.diag()
+        d_ref = full.diag()[l2g]
+        err_diag = ((d - d_ref).norm() / d_ref.norm()).item()
+        # device-resident PCG over the decomposition vs the single-GPU solve
+        X = torch.from_numpy(gnodes).to(dev)
+        xs_g = torch.sin(0.5 * np.pi * X[0]) * torch.cos(0.5 * np.pi * X[1]) + X[0] * X[2]
+        on_g = (X.abs() - 1).abs().min(dim=0).values < 1e-9
+        b = full.apply(xs_g)
+        x_single = torch.where(on_g, xs_g, torch.zeros_like(xs_g))
+        x_single, its1, _ = full.pcg_solve(b, x_single, on_g, rtol=1e-12)
+        xs, on = xs_g[l2g], on_g[l2g]
+        x = torch.where(on, xs, torch.zeros_like(xs))
+        x, its, rel = op.pcg_solve(b[l2g].contiguous(), x, on, rtol=1e-12, check_every=4)
+        err_pcg = ((x - x_single[l2g]).norm() / x_single[l2g].norm()).item()
+        info = op.dd_info()
+        q.put((rank, max(errs), err_oracle, err_diag, err_pcg, its, its1, op.transport,
+               op.n_iface_elem, op.n_interior_elem, info["event_fence"],
+               op.plan_info().get("ndim")))
+        op.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world, *args):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hex_worker, args=(r, world, port) + args) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    try:
+        res = [q.get(timeout=180) for _ in range(world)]
+    finally:
+        for pr in procs:
+            pr.join(timeout=60)
+    for pr in procs:
+        assert pr.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("world,mode,p,nex,ney,nez", [(2, "slab", 8, 6, 3, 2),
+                                                      (3, "slab", 4, 9, 3, 3),
+                                                      (4, "slab", 3, 10, 4, 3),
+                                                      (3, "sfc", 5, 4, 3, 3)])
+def test_hex_overlapped_ranks_on_one_gpu(gpu, world, mode, p, nex, ney, nez):
+    res = _run(world, mode, p, nex, ney, nez)
+    its_all = set()
+    for (rank, err, err_or, err_d, err_pcg, its, its1, tr, n_if, n_in, fence,
+         ndim) in res:
+        assert ndim == 3
+        assert tr == "torch-host" and fence == "system"
+        assert err < 1e-12, (rank, err)
+        assert err_or < 1e-10, (rank, err_or)
+        assert err_d < 1e-12, (rank, err_d)
+        assert err_pcg < 1e-9, (rank, err_pcg)
+        assert n_if > 0
+        its_all.add(its)
+    assert len(its_all) == 1  # every rank ran the same iterations (global dots)

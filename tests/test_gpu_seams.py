@@ -272,3 +272,63 @@ def test_dd_split_finish_is_bitwise(gpu, monkeypatch, rank):
     assert out["1"][1]["split_finish"] and not out["0"][1]["split_finish"]
     assert out["1"][1]["seam_sum_in_finish"]
     assert torch.equal(out["1"][0], out["0"][0])
+
+
+@pytest.mark.parametrize("transport", ["loopback", "rccl_self"])
+def test_dd_event_fence_scope(gpu, monkeypatch, transport):
+    """The stream-join events carry the system-scope fence unless the
+    transport keeps every writer on this device (loopback, RCCL to self:
+    device scope by default); SEM_DD_EVENT_FENCE forces either scope, and the
+    step is bitwise the same under both."""
+    from spectralelementmethod_amd.distributed import OverlappedOperator, StripPartition
+    part = StripPartition(24, 112, 8, 4, 2)
+    nodes, e2n = part.local_mesh(0.05)
+    u = torch.from_numpy(np.random.default_rng(9).standard_normal(nodes.shape[1])).to(gpu)
+    out = {}
+    for scope in ("auto", "system", "device"):
+        if scope == "auto":
+            monkeypatch.delenv("SEM_DD_EVENT_FENCE", raising=False)
+        else:
+            monkeypatch.setenv("SEM_DD_EVENT_FENCE", scope)
+        op = OverlappedOperator(8, nodes, e2n, part.neighbors, 1, gpu, owned=part.owned,
+                                transport=transport, world=1, rank=0, decompose=True)
+        y = torch.full_like(u, 7.0)
+        for _ in range(3):
+            op.step(u, y)
+        torch.cuda.synchronize()
+        out[scope] = (y.clone(), op.dd_info()["event_fence"])
+        op.close()
+    assert out["auto"][1] == "device" and out["system"][1] == "system"
+    assert out["device"][1] == "device"
+    assert torch.equal(out["auto"][0], out["system"][0])
+    assert torch.equal(out["auto"][0], out["device"][0])
+
+
+@pytest.mark.parametrize("rank", [0, 1, 3])
+def test_dd_hex_slab_rank_equals_single_gpu_interior(gpu, rank):
+    """One rank of a hexahedral slab split (row N3) through sem_dd with the
+    RCCL-to-self timing transport (bench.py --dim 3 --time-rank): away from
+    the shared faces (where the loopback adds the rank's own values, not the
+    neighbour's) every node equals the single-GPU action of the whole cube."""
+    from spectralelementmethod_amd import meshgen
+    from spectralelementmethod_amd.distributed import OverlappedOperator, SlabPartition
+    from spectralelementmethod_amd.operators import SEMOperator
+    p, nex, ney, nez, world = 6, 12, 3, 3, 4
+    part = SlabPartition(nex, ney, nez, p, world, rank)
+    nodes, e2n = part.local_mesh(0.05)
+    gnodes, ge2n = meshgen.structured_cube(nex, ney, nez, p, warp=0.05)
+    u_glob = torch.from_numpy(np.random.default_rng(12).standard_normal(gnodes.shape[1])).to(gpu)
+    y_glob = SEMOperator(p, ge2n, gnodes, device=gpu).apply(u_glob)
+    l2g = torch.from_numpy(part.local_to_global()).to(gpu)
+    op = OverlappedOperator(p, nodes, e2n, part.neighbors, 1, gpu, owned=part.owned,
+                            transport="rccl_self", world=1, rank=0, decompose=True)
+    y = torch.full((op.ndof,), 7.0, dtype=torch.float64, device=gpu)
+    op.step(u_glob[l2g].contiguous(), y)
+    torch.cuda.synchronize()
+    inner = torch.ones(op.ndof, dtype=torch.bool, device=gpu)
+    for nb in part.neighbors.values():
+        inner[torch.from_numpy(nb).to(gpu)] = False
+    ref = y_glob[l2g]
+    assert ((y - ref)[inner].norm() / ref[inner].norm()).item() < 1e-12
+    assert op.dd_info()["event_fence"] == "device" and op.plan_info()["ndim"] == 3
+    op.close()

@@ -1,4 +1,4 @@
-"""Average PMC counters per dispatch from tools/gpu_counters.sh output."""
+"""Average PMC counters per dispatch from tools/archive/gpu_counters.sh output."""
 import collections
 import csv
 import glob

@@ -1,6 +1,6 @@
 #!/usr/bin/env python
 """One parameterised runner for the GPU calls (replaces round 3's per-call
-tools/r03/gpu_*.sh scripts).
+tools/archive/r03/gpu_*.sh scripts).
 
   python tools/gpu_steps.py OUTDIR "label|timeout_s|command" ["label|timeout_s|command" ...]
 
