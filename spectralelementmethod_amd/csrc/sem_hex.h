@@ -81,6 +81,27 @@ struct HexD {
   double d[N * N];  // d[q*N + a] = D[q][a]: row q of D
 };
 
+// Layout of the stored factors (G00, G01, G02, G11, G12, G22 per element
+// node) as three double2 pairs (00, 01), (02, 11), (12, 22).  SoA
+// (HEX_GSOA, default): per element and node row a, three planes of n^2
+// pairs, so one wave-instruction reads 64 lanes' pair j as one contiguous
+// 1 KiB run; AoS (SEM_HEX_GSOA=0): the node's three pairs side by side
+// (48 B per lane, each wave-instruction spread over 3 KiB).  Measured equal
+// at p = 4..10 and 1.5 % faster at p = 2.  Either way a
+// node row is 3 n^2 pairs.
+#ifndef SEM_HEX_GSOA
+#define SEM_HEX_GSOA 1
+#endif
+constexpr bool HEX_GSOA = SEM_HEX_GSOA != 0;
+template <int N>
+__host__ __device__ constexpr int64_t hex_g_off(int64_t e, int bc) {
+  return e * (int64_t)N * N * N * 3 + (HEX_GSOA ? bc : 3 * bc);
+}
+template <int N>
+__device__ __forceinline__ const double2* hex_g(const double* G, int64_t e, int bc) {
+  return reinterpret_cast<const double2*>(G) + hex_g_off<N>(e, bc);
+}
+
 // boundary-column index of (b, c) in [0, 4(n-1)), -1 for an interior column
 template <int N>
 __device__ __forceinline__ int hex_bcol(int b, int c) {
@@ -93,8 +114,8 @@ __device__ __forceinline__ int hex_bcol(int b, int c) {
 
 // Poisson stiffness action on hexahedra (MODE HEX_SET / HEX_ACC), or the
 // diagonal of the assembled operator (HEX_DIAG; u unused).  G: stored factors
-// [E][a][b*n + c][6], components (00, 01, 02, 11, 12, 22): a thread reads its
-// node's six as three 16-byte loads.
+// in the pair layout of hex_g (components 00, 01, 02, 11, 12, 22): a thread
+// reads its node's six as three 16-byte loads.
 #ifndef SEM_HEX_MIN_WAVES
 #define SEM_HEX_MIN_WAVES 4
 #endif
@@ -104,6 +125,7 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
                   const uint32_t* __restrict__ map, const double* __restrict__ G,
                   const double* __restrict__ gD, HexLaunch P, const HexD<N> Dk) {
   constexpr int N2 = N * N, N3 = N2 * N, S = hex_slots(N), T = hex_threads(N), NBC = hex_nbc(N);
+  constexpr int GROW = 3 * N2, GPAIR = HEX_GSOA ? N2 : 1;  // factor layout (hex_g)
   __shared__ double sD[N2];
   __shared__ double sU[S * N3];
   __shared__ double sA[S * N3];
@@ -154,7 +176,7 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
     uint32_t m[N];
 #pragma unroll
     for (int a = 0; a < N; ++a) m[a] = mn[a];
-    const double* g = G + ((int64_t)e * N3 + bc) * 6;
+    const double2* g = hex_g<N>(G, e, bc);
     double uc[MODE != HEX_DIAG ? N : 1];
     if (active) {
       if constexpr (MODE != HEX_DIAG) {
@@ -172,9 +194,9 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
         // diagonal: G00 of this column, G11 / G22 of the other threads' nodes
 #pragma unroll
         for (int a = 0; a < N; ++a) {
-          su[a * N2 + bc] = g[a * N2 * 6 + 0];
-          sa[a * N2 + bc] = g[a * N2 * 6 + 3];
-          sb[a * N2 + bc] = g[a * N2 * 6 + 5];
+          su[a * N2 + bc] = g[a * GROW].x;              // G00
+          sa[a * N2 + bc] = g[a * GROW + GPAIR].y;      // G11
+          sb[a * N2 + bc] = g[a * GROW + 2 * GPAIR].y;  // G22
         }
       }
     }
@@ -211,8 +233,8 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
             d1 = fma(dbr, su[a * N2 + r * N + c], d1);
             d2 = fma(dcr, su[a * N2 + b * N + r], d2);
           }
-          const double2* ga = reinterpret_cast<const double2*>(g + a * N2 * 6);
-          const double2 q0 = ga[0], q1 = ga[1], q2 = ga[2];
+          const double2* ga = g + a * GROW;
+          const double2 q0 = ga[0], q1 = ga[GPAIR], q2 = ga[2 * GPAIR];
           const double g00 = q0.x, g01 = q0.y, g02 = q1.x, g11 = q1.y, g12 = q2.x, g22 = q2.y;
           const double w0 = g00 * d0 + g01 * d1 + g02 * d2;
           sa[a * N2 + bc] = g01 * d0 + g11 * d1 + g12 * d2;
@@ -252,9 +274,10 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
         }
 #pragma unroll
         for (int a = 0; a < N; ++a) {
-          const double* ga = g + a * N2 * 6;
+          const double2* ga = g + a * GROW;
           const double daa = sD[a * N + a];
-          yv[a] += 2.0 * (daa * dbb * ga[1] + daa * dcc * ga[2] + dbb * dcc * ga[4]);
+          // G01, G02, G12
+          yv[a] += 2.0 * (daa * dbb * ga[0].y + daa * dcc * ga[GPAIR].x + dbb * dcc * ga[2 * GPAIR].x);
         }
       }
       __syncthreads();  // su / sa / sb are rewritten by the next element
@@ -327,6 +350,7 @@ __global__ void __launch_bounds__(hex_threads(N), hex_rows_min_waves(N))
   static_assert(MODE == HEX_SET || MODE == HEX_ACC, "row form: the action only");
   constexpr int N2 = N * N, N3 = N2 * N, S = hex_slots(N), T = hex_threads(N), NBC = hex_nbc(N);
   constexpr int SW = S * N2;  // one plane of the ring: [slot][b*n + c]
+  constexpr int GROW = 3 * N2, GPAIR = HEX_GSOA ? N2 : 1;  // factor layout (hex_g)
   __shared__ double sD[N2];
   __shared__ double sU[S * N3];
   __shared__ double sW[4 * SW];  // [row parity][w1, w2][slot][b*n + c]
@@ -368,7 +392,7 @@ __global__ void __launch_bounds__(hex_threads(N), hex_rows_min_waves(N))
     uint32_t m[N];
 #pragma unroll
     for (int a = 0; a < N; ++a) m[a] = mn[a];
-    const double* g = G + ((int64_t)e * N3 + bc) * 6;
+    const double2* g = hex_g<N>(G, e, bc);
     double uc[N];
     if (active) {
 #pragma unroll
@@ -397,8 +421,8 @@ __global__ void __launch_bounds__(hex_threads(N), hex_rows_min_waves(N))
           d1 = fma(sD[b * N + r], su[a * N2 + r * N + c], d1);
           d2 = fma(sD[c * N + r], su[a * N2 + b * N + r], d2);
         }
-        const double2* ga = reinterpret_cast<const double2*>(g + a * N2 * 6);
-        const double2 q0 = ga[0], q1 = ga[1], q2 = ga[2];
+        const double2* ga = g + a * GROW;
+        const double2 q0 = ga[0], q1 = ga[GPAIR], q2 = ga[2 * GPAIR];
         const double g00 = q0.x, g01 = q0.y, g02 = q1.x, g11 = q1.y, g12 = q2.x, g22 = q2.y;
         const double w0 = g00 * d0 + g01 * d1 + g02 * d2;
         w1p[bc] = g01 * d0 + g11 * d1 + g12 * d2;
@@ -485,7 +509,7 @@ __global__ void k_hex_seam_sum(double* __restrict__ y, const uint32_t* __restric
 // The transforms act on coordinates relative to the element's node (0,0,0)
 // (the constant is added back to x_phys) to keep the rounding of V^-1's
 // large alternating entries off the absolute position.  Outputs may be null:
-// GP [E][n^3][6] (the action's layout), x_phys [E][3][n^3], J / invJ
+// GP: the action's pair layout (hex_g), x_phys [E][3][n^3], J / invJ
 // [E][3][3][n^3], detJ / detJxW [E][n^3].  bad counts nodes with detJ <= 0.
 template <int N>
 __global__ void __launch_bounds__(hex_threads(N))
@@ -615,14 +639,14 @@ __global__ void __launch_bounds__(hex_threads(N))
         const double W = ((det * sw[a]) * sw[b]) * sw[c];
         const int64_t node = e * N3 + a * N2 + bc;
         if (GP) {
-          double2* gp = reinterpret_cast<double2*>(GP + node * 6);
+          double2* gp = reinterpret_cast<double2*>(GP) + hex_g_off<N>(e, bc) + a * (3 * N2);
           gp[0] = make_double2(
               W * (iJ[0][0] * iJ[0][0] + iJ[0][1] * iJ[0][1] + iJ[0][2] * iJ[0][2]),
               W * (iJ[0][0] * iJ[1][0] + iJ[0][1] * iJ[1][1] + iJ[0][2] * iJ[1][2]));
-          gp[1] = make_double2(
+          gp[HEX_GSOA ? N2 : 1] = make_double2(
               W * (iJ[0][0] * iJ[2][0] + iJ[0][1] * iJ[2][1] + iJ[0][2] * iJ[2][2]),
               W * (iJ[1][0] * iJ[1][0] + iJ[1][1] * iJ[1][1] + iJ[1][2] * iJ[1][2]));
-          gp[2] = make_double2(
+          gp[HEX_GSOA ? 2 * N2 : 2] = make_double2(
               W * (iJ[1][0] * iJ[2][0] + iJ[1][1] * iJ[2][1] + iJ[1][2] * iJ[2][2]),
               W * (iJ[2][0] * iJ[2][0] + iJ[2][1] * iJ[2][1] + iJ[2][2] * iJ[2][2]));
         }
@@ -662,7 +686,7 @@ __global__ void k_hex_assemble(const uint32_t* __restrict__ e2n, const double* _
     unsafeAtomicAdd(out + e2n[t], vals[t]);
 }
 
-// user factors [E][6][n^3] -> the action's layout [E][n^3][6]
+// user factors [E][6][n^3] -> the action's pair layout (hex_g)
 __global__ void k_hex_pack_geom(const double* __restrict__ G, int64_t n_elem, int n,
                                 double* __restrict__ GP) {
   const int64_t n2 = (int64_t)n * n, n3 = n2 * n;
@@ -673,7 +697,12 @@ __global__ void k_hex_pack_geom(const double* __restrict__ G, int64_t n_elem, in
     const int64_t rem = t - e * 6 * n3;
     const int comp = (int)(rem / n3);
     const int64_t node = rem - comp * n3;
-    GP[(e * n3 + node) * 6 + comp] = G[t];
+    if (HEX_GSOA) {  // [e][a][pair][bc][2]
+      const int64_t a = node / n2, bc = node - a * n2;
+      GP[(((e * n + a) * 3 + comp / 2) * n2 + bc) * 2 + (comp & 1)] = G[t];
+    } else {
+      GP[(e * n3 + node) * 6 + comp] = G[t];
+    }
   }
 }
 

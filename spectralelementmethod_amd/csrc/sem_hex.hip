@@ -34,7 +34,7 @@ struct HexState {
   uint32_t* d_zero = nullptr;  // unreferenced nodes (overwrite mode zeroes them)
   int64_t n_zero = 0;
   uint32_t* d_map = nullptr;   // the library's copy of the caller's map [E][n][n][n]
-  double* d_G = nullptr;       // stored factors [E][n^3][6]
+  double* d_G = nullptr;       // stored factors, 6 per element node (pair layout, sem_hex.h hex_g)
   bool have_G = false;
   // the action's kernel: k_hex_poisson (three-block, default) or k_hex_rows
   // (row form, SEM_HEX_ROWS=1; the diagonal always runs k_hex_poisson)

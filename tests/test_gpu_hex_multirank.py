@@ -114,14 +114,26 @@ def _run(world, *args):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_hex_worker, args=(r, world, port) + args) for r in range(world)]
+    procs = [ctx.Process(target=_hex_worker, args=(r, world, port) + args + (q,))
+             for r in range(world)]
     for pr in procs:
         pr.start()
     try:
-        res = [q.get(timeout=180) for _ in range(world)]
+        res = []
+        for _ in range(world):  # a rank that died cannot report: do not wait out the timeout
+            while True:
+                try:
+                    res.append(q.get(timeout=5))
+                    break
+                except Exception:
+                    if any(pr.exitcode not in (None, 0) for pr in procs):
+                        raise AssertionError("a rank exited: %s" % [pr.exitcode for pr in procs])
     finally:
         for pr in procs:
             pr.join(timeout=60)
+            if pr.is_alive():  # a peer of a failed rank, blocked in a collective
+                pr.kill()
+                pr.join()
     for pr in procs:
         assert pr.exitcode == 0
     return res
