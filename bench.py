@@ -315,33 +315,41 @@ def hex_parity_checks(op, y, u, part, p, warp, dev, world):
     def rel(a, b):
         return float(np.linalg.norm(a - b) / np.linalg.norm(b))
     t0 = time.perf_counter()
-    if world == 1:
+    ext = p > 10  # the extended-precision oracle, on blocks
+
+    def oracle(nodes, e2n, u_sub):
+        if ext:
+            return np.asarray(sem_oracle.hex_poisson_apply_extended(nodes, e2n, half, u_sub),
+                              dtype=np.float64)
+        return sem_oracle.HexPoissonProblem(nodes, e2n, half).apply(u_sub)
+    vs = ("oracle/sem_oracle.py hex_poisson_apply_extended (x87 extended precision; the "
+          "float64 transform is ill-conditioned above p = 10)" if ext else
+          "oracle/sem_oracle.py HexPoissonProblem")
+    if world == 1 and not ext:
         nodes, e2n = part.local_mesh(warp)
         ref = sem_oracle.HexPoissonProblem(nodes, e2n, half).apply(u.cpu().numpy())
         return {"rel_l2": rel(y.cpu().numpy(), ref), "tolerance": 1e-10,
                 "vs": "oracle/sem_oracle.py HexPoissonProblem (whole mesh)",
                 "oracle_sec": time.perf_counter() - t0}, None
     face = part.face
-    nl = part.ex1 - part.ex0
+    nl = part.ex1 - part.ex0  # (world 1 above p = 10: a block, not the whole mesh)
     c0 = part.ex0 + max(0, (nl - 2) // 2)
     c1 = min(part.ex1, c0 + 2)
     nodes, e2n, off = meshgen.structured_slab(part.nex, part.ney, part.nez, p, c0, c1, warp)
     loc = off - part.node_offset + np.arange(nodes.shape[1])
-    y_ref = sem_oracle.HexPoissonProblem(nodes, e2n, half).apply(
-        u[torch_index(loc, dev)].cpu().numpy())
+    y_ref = oracle(nodes, e2n, u[torch_index(loc, dev)].cpu().numpy())
     inner = np.arange(face, nodes.shape[1] - face)
     block = {"rel_l2": rel(y[torch_index(loc[inner], dev)].cpu().numpy(), y_ref[inner]),
              "tolerance": 1e-10, "nodes_checked": int(inner.size),
-             "block": "element layers [%d, %d) of the slab" % (c0, c1),
-             "vs": "oracle/sem_oracle.py HexPoissonProblem"}
+             "block": "element layers [%d, %d) of the slab" % (c0, c1), "vs": vs,
+             "oracle_sec": time.perf_counter() - t0}
     iface = None
     if part.rank < world - 1:
         c0 = part.ex1 - 1
         nodes, e2n, off = meshgen.structured_slab(part.nex, part.ney, part.nez, p, c0, c0 + 2,
                                                   warp)
         gids = off + np.arange(nodes.shape[1])
-        y_ref = sem_oracle.HexPoissonProblem(nodes, e2n, half).apply(
-            global_field_at(part, gids, dev).cpu().numpy())
+        y_ref = oracle(nodes, e2n, global_field_at(part, gids, dev).cpu().numpy())
         own = np.arange(face, (p + 1) * face)
         iface = {"rel_l2": rel(y[torch_index(gids[own] - part.node_offset, dev)].cpu().numpy(),
                                y_ref[own]),

@@ -116,7 +116,9 @@ void sem_ctx_destroy(sem_ctx* ctx);
  * sem/basis_functions.py:599-650; TensorQuadratureRule.xweight,
  * sem/quadratures.py:268-275; NCube, sem/geometry.py:32-216); only its 2x2
  * Jacobian inverse stops at 2-D (sem/mapping.py:110-111).  On a hexahedral
- * context (1 <= p <= 11, dpn = 1, Poisson):
+ * context (1 <= p <= 16, dpn = 1, Poisson; above p = 10 the equispaced ->
+ * GLL transform runs as compensated passes, above p = 12 the action runs the
+ * row form of the kernel by default):
  *   - element-local arrays are [n][n][n] in lexicographic (xi0, xi1, xi2)
  *     order, xi2 fastest; the map is uint32 [n_elem][n][n][n];
  *   - sem_geom_from_nodes takes nodes float64 [3][n_node] and stores the 6

@@ -39,7 +39,7 @@
 namespace semh {
 
 constexpr int HEX_MIN_N = 2;
-constexpr int HEX_MAX_N = 12;  // p <= 11
+constexpr int HEX_MAX_N = 17;  // p <= 16
 
 // element slots per workgroup: as many n x n thread tiles as fit in 256 threads
 constexpr int hex_slots(int n) { return 256 / (n * n) > 0 ? 256 / (n * n) : 1; }
@@ -119,8 +119,12 @@ __device__ __forceinline__ int hex_bcol(int b, int c) {
 #ifndef SEM_HEX_MIN_WAVES
 #define SEM_HEX_MIN_WAVES 4
 #endif
+// occupancy request: above p = 10 the register arrays (column of u, y, the
+// maps) exceed what four waves per SIMD allow, and one element slot per
+// workgroup leaves LDS the limit anyway
+constexpr int hex_min_waves(int n) { return n <= 11 ? SEM_HEX_MIN_WAVES : n <= 13 ? 2 : 1; }
 template <int N, int MODE>
-__global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
+__global__ void __launch_bounds__(hex_threads(N), hex_min_waves(N))
     k_hex_poisson(const double* __restrict__ u, double* __restrict__ y,
                   const uint32_t* __restrict__ map, const double* __restrict__ G,
                   const double* __restrict__ gD, HexLaunch P, const HexD<N> Dk) {
@@ -340,7 +344,7 @@ __global__ void __launch_bounds__(hex_threads(N), SEM_HEX_MIN_WAVES)
 // four waves per SIMD (<= 128 VGPRs) up to n = 9; above, the allocator
 // would spill at that bound, and three waves per SIMD are what the
 // three-block kernel gets there
-constexpr int hex_rows_min_waves(int n) { return n <= 9 ? 4 : n <= 11 ? 3 : 2; }
+constexpr int hex_rows_min_waves(int n) { return n <= 9 ? 4 : n <= 11 ? 3 : n <= 13 ? 2 : 1; }
 
 template <int N, int MODE>
 __global__ void __launch_bounds__(hex_threads(N), hex_rows_min_waves(N))
@@ -517,7 +521,8 @@ __global__ void __launch_bounds__(hex_threads(N))
                int64_t n_elem, const double* __restrict__ gV, const double* __restrict__ gD,
                const double* __restrict__ gw, double* __restrict__ GP, double* __restrict__ xph,
                double* __restrict__ Jo, double* __restrict__ iJo, double* __restrict__ dJo,
-               double* __restrict__ dJWo, unsigned long long* __restrict__ bad) {
+               double* __restrict__ dJWo, unsigned long long* __restrict__ bad,
+               const double* __restrict__ xrel) {
   constexpr int N2 = N * N, N3 = N2 * N, S = hex_slots(N), T = hex_threads(N);
   __shared__ double sV[N2], sD[N2], sw[N];
   __shared__ double sX[3][S * N3];
@@ -544,58 +549,68 @@ __global__ void __launch_bounds__(hex_threads(N))
     double* const sx2 = sX[2] + sl * N3;
     double* const sxk[3] = {sx0, sx1, sx2};
     if (active) {
-      const uint32_t* me = map + e * N3;
-      const uint32_t g0 = me[0];
+      const uint32_t g0 = map[e * N3];
 #pragma unroll
       for (int k = 0; k < 3; ++k) xr[k] = nodes[k * n_node + g0];
-      double xe[3][N];
+    }
+    if (xrel) {  // x_phys - x_phys(0,0,0) given (k_hex_eq2gll_pass, compensated)
+      if (active)
 #pragma unroll
-      for (int a = 0; a < N; ++a) {
-        const uint32_t gi = me[a * N2 + bc];
+        for (int k = 0; k < 3; ++k)
 #pragma unroll
-        for (int k = 0; k < 3; ++k) xe[k][a] = nodes[k * n_node + gi] - xr[k];
+          for (int a = 0; a < N; ++a) x[k][a] = xrel[(e * 3 + k) * N3 + a * N2 + bc];
+    } else {  // the three passes here (uniform branch: xrel is an argument)
+      if (active) {
+        const uint32_t* me = map + e * N3;
+        double xe[3][N];
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+          const uint32_t gi = me[a * N2 + bc];
+#pragma unroll
+          for (int k = 0; k < 3; ++k) xe[k][a] = nodes[k * n_node + gi] - xr[k];
+        }
+        // xi0: registers
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+          for (int a = 0; a < N; ++a) {
+            double v = 0.0;
+#pragma unroll
+            for (int r = 0; r < N; ++r) v = fma(sV[a * N + r], xe[k][r], v);
+            sxk[k][a * N2 + bc] = v;
+          }
       }
-      // xi0: registers
+      __syncthreads();
+      if (active) {  // xi1
 #pragma unroll
-      for (int k = 0; k < 3; ++k)
+        for (int k = 0; k < 3; ++k)
 #pragma unroll
-        for (int a = 0; a < N; ++a) {
-          double v = 0.0;
+          for (int a = 0; a < N; ++a) {
+            double v = 0.0;
 #pragma unroll
-          for (int r = 0; r < N; ++r) v = fma(sV[a * N + r], xe[k][r], v);
-          sxk[k][a * N2 + bc] = v;
-        }
-    }
-    __syncthreads();
-    if (active) {  // xi1
+            for (int r = 0; r < N; ++r) v = fma(sV[b * N + r], sxk[k][a * N2 + r * N + c], v);
+            x[k][a] = v;
+          }
+      }
+      __syncthreads();
+      if (active)
 #pragma unroll
-      for (int k = 0; k < 3; ++k)
+        for (int k = 0; k < 3; ++k)
 #pragma unroll
-        for (int a = 0; a < N; ++a) {
-          double v = 0.0;
+          for (int a = 0; a < N; ++a) sxk[k][a * N2 + bc] = x[k][a];
+      __syncthreads();
+      if (active) {  // xi2
 #pragma unroll
-          for (int r = 0; r < N; ++r) v = fma(sV[b * N + r], sxk[k][a * N2 + r * N + c], v);
-          x[k][a] = v;
-        }
-    }
-    __syncthreads();
-    if (active)
+        for (int k = 0; k < 3; ++k)
 #pragma unroll
-      for (int k = 0; k < 3; ++k)
+          for (int a = 0; a < N; ++a) {
+            double v = 0.0;
 #pragma unroll
-        for (int a = 0; a < N; ++a) sxk[k][a * N2 + bc] = x[k][a];
-    __syncthreads();
-    if (active) {  // xi2
-#pragma unroll
-      for (int k = 0; k < 3; ++k)
-#pragma unroll
-        for (int a = 0; a < N; ++a) {
-          double v = 0.0;
-#pragma unroll
-          for (int r = 0; r < N; ++r) v = fma(sV[c * N + r], sxk[k][a * N2 + b * N + r], v);
-          x[k][a] = v;  // x_phys relative to node (0,0,0)
-        }
-    }
+            for (int r = 0; r < N; ++r) v = fma(sV[c * N + r], sxk[k][a * N2 + b * N + r], v);
+            x[k][a] = v;  // x_phys relative to node (0,0,0)
+          }
+      }
+    }  // xrel
     __syncthreads();
     if (active)
 #pragma unroll
@@ -670,6 +685,74 @@ __global__ void __launch_bounds__(hex_threads(N))
     __syncthreads();  // sX is rewritten by the next element
   }
   if (nbad) atomicAdd(bad, nbad);
+}
+
+// The equispaced -> GLL transform above p = 10 (k_hex_geom's xrel input):
+// V_eq^-1 has entries up to ~170 at p = 16 (cond ~1e5) and J = D x_phys
+// amplifies the rounding of plain float64 sums by ~n^2/4, so, as on
+// quadrilaterals (k_geometry), every pass is a compensated dot
+// product (Ogita-Rump-Oishi Dot2, semk::dot2) on coordinates relative to the
+// element's node (0,0,0), the intermediate kept as hi + lo in global scratch
+// (setup only).  Layout of every array: [E][3][n^3], local node a*n^2 + b*n + c.
+// Pass 0: the relative element coordinates from the nodes and the map.
+template <int N>
+__global__ void k_hex_rel_coords(const double* __restrict__ nodes, int64_t n_node,
+                                 const uint32_t* __restrict__ map, int64_t n_elem,
+                                 double* __restrict__ out) {
+  constexpr int N3 = N * N * N;
+  const int64_t total = n_elem * 3 * N3;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t ek = t / N3, e = ek / 3;
+    const int node = (int)(t - ek * N3), k = (int)(ek - e * 3);
+    out[t] = nodes[k * n_node + map[e * N3 + node]] - nodes[k * n_node + map[e * N3]];
+  }
+}
+// One pass along axis AX (0: a, 1: b, 2: c): out = V_eq^-1 (vh + vl, an
+// inverse computed in extended precision) applied along AX to in = hi (+ lo),
+// compensated: s_hi + s_lo ~= sum_r (vh + vl)[m][r] (in_hi + in_lo)[r] to
+// about twice the working precision (Dot2 with both low parts folded in).
+template <int N>
+__device__ __forceinline__ void dot2x(const double* ah, const double* al, const double* bh,
+                                      const double* bl, int sb, double& hi, double& lo) {
+  double s = 0.0, c = 0.0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    double p, ep, es;
+    semk::two_prod(ah[i], bh[i * sb], p, ep);
+    semk::two_sum(s, p, s, es);
+    c += ep + es;
+    if (bl) c = fma(ah[i], bl[i * sb], c);
+    c = fma(al[i], bh[i * sb], c);
+  }
+  hi = s + c;
+  lo = c - (hi - s);
+}
+template <int N, int AX>
+__global__ void k_hex_eq2gll_pass(const double* __restrict__ in_hi, const double* __restrict__ in_lo,
+                                  double* __restrict__ out_hi, double* __restrict__ out_lo,
+                                  const double* __restrict__ vh, const double* __restrict__ vl,
+                                  int64_t n_blocks) {
+  constexpr int N2 = N * N, N3 = N2 * N;
+  constexpr int ST = AX == 0 ? N2 : AX == 1 ? N : 1;  // stride along the axis
+  __shared__ double sV[N2], sVl[N2];
+  for (int i = threadIdx.x; i < N2; i += blockDim.x) {
+    sV[i] = vh[i];
+    sVl[i] = vl[i];
+  }
+  __syncthreads();
+  const int64_t total = n_blocks * N3;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t blk = t / N3;
+    const int node = (int)(t - blk * N3);
+    const int m = AX == 0 ? node / N2 : AX == 1 ? (node / N) % N : node % N;
+    const int64_t line = blk * N3 + node - m * ST;  // the line's first node
+    double hi, lo;
+    dot2x<N>(&sV[m * N], &sVl[m * N], in_hi + line, in_lo ? in_lo + line : nullptr, ST, hi, lo);
+    out_hi[t] = hi;
+    if (out_lo) out_lo[t] = lo;
+  }
 }
 
 __global__ void k_hex_zero(double* __restrict__ y, const uint32_t* __restrict__ idx, int64_t n) {

@@ -34,6 +34,7 @@ struct HexState {
   uint32_t* d_zero = nullptr;  // unreferenced nodes (overwrite mode zeroes them)
   int64_t n_zero = 0;
   uint32_t* d_map = nullptr;   // the library's copy of the caller's map [E][n][n][n]
+  double* d_vx = nullptr;      // V_eq^-1 hi, lo (extended-precision inverse, p >= 11)
   double* d_G = nullptr;       // stored factors, 6 per element node (pair layout, sem_hex.h hex_g)
   bool have_G = false;
   // the action's kernel: k_hex_poisson (three-block, default) or k_hex_rows
@@ -60,6 +61,12 @@ struct HexState {
 };
 
 namespace {
+
+#define SEM_TRY_RC(expr) \
+  do {                     \
+    int _rc = (expr);      \
+    if (_rc) return _rc;   \
+  } while (0)
 
 int hex_check_order(int n) {
   if (n < semh::HEX_MIN_N || n > semh::HEX_MAX_N)
@@ -436,16 +443,107 @@ int launch_hex_apply(sem_ctx* c, int mode, const double* u, double* y, hipStream
   return SEM_OK;
 }
 
+// from this many nodes per line (p >= 11) the equispaced -> GLL transform
+// runs as three compensated passes (k_hex_eq2gll_pass) before k_hex_geom:
+// float64 sums lose 7e-12 (p = 12) to 1e-8 (p = 16) of the action against
+// the extended-precision oracle (oracle
+// hex_poisson_apply_extended); at p <= 10 the plain passes stay (4.7e-13)
+constexpr int HEX_DOT2_MIN_N = 12;
+
+// V_eq^-1 as hi + lo doubles, from V_eq built and inverted in x87 extended
+// precision on the GLL nodes of the context's basis: the float64 inverse the
+// caller passes is itself off by ~cond(V_eq) eps (1e-11 at p = 16), which the
+// compensated passes would otherwise carry into x_phys.  Only for the standard
+// GLL basis (the baked table reproduces the context's D bit for bit);
+// otherwise hi = the caller's inverse, lo = 0.
+int eq2gll_hilo(sem_ctx* c, double* hi, double* lo) {
+  const int n = c->n;
+  std::vector<double> xn(n), bw(n), qw(n), D((size_t)n * n);
+  bool gll = sem::gll_table(c->p, xn.data(), bw.data(), qw.data()) == SEM_OK;
+  if (gll) {
+    sem::diff_matrix(n, xn.data(), bw.data(), D.data());
+    gll = std::memcmp(D.data(), c->hD, sizeof(double) * n * n) == 0;
+  }
+  if (!gll) {
+    HIP_TRY(hipMemcpy(hi, c->d_Vinv, sizeof(double) * n * n, hipMemcpyDeviceToHost));
+    for (int i = 0; i < n * n; ++i) lo[i] = 0.0;
+    return SEM_OK;
+  }
+  std::vector<long double> a((size_t)n * 2 * n, 0.0L);
+  for (int i = 0; i < n; ++i) {
+    const long double x = -1.0L + 2.0L * i / (long double)(n - 1);
+    int hit = -1;
+    long double sum = 0.0L;
+    for (int j = 0; j < n && hit < 0; ++j) {
+      const long double d = x - (long double)xn[j];
+      if (d == 0.0L) hit = j;
+      else sum += (long double)bw[j] / d;
+    }
+    for (int j = 0; j < n; ++j)
+      a[(size_t)i * 2 * n + j] =
+          hit >= 0 ? (j == hit ? 1.0L : 0.0L) : ((long double)bw[j] / (x - (long double)xn[j])) / sum;
+    a[(size_t)i * 2 * n + n + i] = 1.0L;
+  }
+  for (int col = 0; col < n; ++col) {  // Gauss-Jordan, partial pivoting
+    int piv = col;
+    for (int r = col + 1; r < n; ++r)
+      if (fabsl(a[(size_t)r * 2 * n + col]) > fabsl(a[(size_t)piv * 2 * n + col])) piv = r;
+    if (piv != col)
+      for (int j = 0; j < 2 * n; ++j) std::swap(a[(size_t)col * 2 * n + j], a[(size_t)piv * 2 * n + j]);
+    const long double dg = a[(size_t)col * 2 * n + col];
+    for (int j = 0; j < 2 * n; ++j) a[(size_t)col * 2 * n + j] /= dg;
+    for (int r = 0; r < n; ++r) {
+      if (r == col) continue;
+      const long double f = a[(size_t)r * 2 * n + col];
+      for (int j = 0; j < 2 * n; ++j) a[(size_t)r * 2 * n + j] -= f * a[(size_t)col * 2 * n + j];
+    }
+  }
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      const long double v = a[(size_t)i * 2 * n + n + j];
+      hi[i * n + j] = (double)v;
+      lo[i * n + j] = (double)(v - (long double)hi[i * n + j]);
+    }
+  return SEM_OK;
+}
+
 template <int N>
 int launch_hex_geom(sem_ctx* c, const double* nodes, double* GP, double* xph, double* J,
                     double* iJ, double* dJ, double* dJW, hipStream_t st) {
   HexState* H = c->hex;
-  constexpr int S = semh::hex_slots(N);
+  constexpr int S = semh::hex_slots(N), N3 = N * N * N;
   const int64_t nb = std::min<int64_t>((c->n_elem + S - 1) / S, 16384);
+  double* buf[4] = {nullptr, nullptr, nullptr, nullptr};
+  const double* xrel = nullptr;
+  if constexpr (N >= HEX_DOT2_MIN_N) {
+    // relative coordinates R, then R -> (A, Al) -> (R, X) -> A along xi0, xi1, xi2
+    const int64_t total = c->n_elem * 3 * N3;
+    if (!H->d_vx) HIP_TRY(hipMalloc(&H->d_vx, 2 * N * N * sizeof(double)));
+    {
+      std::vector<double> vx(2 * N * N);
+      SEM_TRY_RC(eq2gll_hilo(c, vx.data(), vx.data() + N * N));
+      HIP_TRY(hipMemcpy(H->d_vx, vx.data(), vx.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
+    for (double*& b : buf) HIP_TRY(hipMallocAsync((void**)&b, total * sizeof(double), st));
+    const dim3 g(grid_for(total, 256, 16384)), bl(256);
+    const double *vh = H->d_vx, *vl = H->d_vx + N * N;
+    hipLaunchKernelGGL(semh::k_hex_rel_coords<N>, g, bl, 0, st, nodes, c->n_node, H->d_map,
+                       c->n_elem, buf[0]);
+    hipLaunchKernelGGL((semh::k_hex_eq2gll_pass<N, 0>), g, bl, 0, st, buf[0], nullptr, buf[1],
+                       buf[2], vh, vl, c->n_elem * 3);
+    hipLaunchKernelGGL((semh::k_hex_eq2gll_pass<N, 1>), g, bl, 0, st, buf[1], buf[2], buf[0],
+                       buf[3], vh, vl, c->n_elem * 3);
+    hipLaunchKernelGGL((semh::k_hex_eq2gll_pass<N, 2>), g, bl, 0, st, buf[0], buf[3], buf[1],
+                       nullptr, vh, vl, c->n_elem * 3);
+    HIP_TRY(hipGetLastError());
+    xrel = buf[1];
+  }
   hipLaunchKernelGGL(semh::k_hex_geom<N>, dim3((unsigned)nb), dim3(semh::hex_threads(N)), 0, st,
                      nodes, c->n_node, H->d_map, c->n_elem, c->d_Vinv, c->d_D, c->d_w, GP, xph, J,
-                     iJ, dJ, dJW, c->d_bad);
+                     iJ, dJ, dJW, c->d_bad, xrel);
   HIP_TRY(hipGetLastError());
+  for (double* b : buf)
+    if (b) HIP_TRY(hipFreeAsync(b, st));
   return SEM_OK;
 }
 
@@ -462,9 +560,14 @@ int launch_hex_geom(sem_ctx* c, const double* nodes, double* GP, double* xph, do
     case 10: rc = FN<10>(__VA_ARGS__); break;   \
     case 11: rc = FN<11>(__VA_ARGS__); break;   \
     case 12: rc = FN<12>(__VA_ARGS__); break;   \
+    case 13: rc = FN<13>(__VA_ARGS__); break;   \
+    case 14: rc = FN<14>(__VA_ARGS__); break;   \
+    case 15: rc = FN<15>(__VA_ARGS__); break;   \
+    case 16: rc = FN<16>(__VA_ARGS__); break;   \
+    case 17: rc = FN<17>(__VA_ARGS__); break;   \
     default: rc = fail(SEM_E_NOTIMPL, "hexahedral order out of range"); break; \
   }
-static_assert(semh::HEX_MAX_N == 12, "HEX_DISPATCH lists n = 2..12");
+static_assert(semh::HEX_MAX_N == 17, "HEX_DISPATCH lists n = 2..17");
 
 // workgroups of the element kernel resident per CU (LDS and VGPR bound)
 template <int N>
@@ -491,6 +594,13 @@ int need_map(const sem_ctx* c) {
 
 namespace semh {
 
+// the row form by default where the three-block kernel's LDS
+// (3 S n^3 doubles) exceeds 64 KiB: n >= 14
+static bool hex_rows_default(int n) {
+  const int64_t lds = 8 * (3 * (int64_t)hex_slots(n) * n * n * n + (int64_t)n * n);
+  return lds > 65536;
+}
+
 int ctx_init(sem_ctx* c) {
   int rc = hex_check_order(c->n);
   if (rc) return rc;
@@ -503,8 +613,10 @@ int ctx_init(sem_ctx* c) {
   // the row form only on request (SEM_HEX_ROWS=1): with the z-merge in both
   // kernels the three-block kernel is as fast or faster at every order
   // measured (p = 2 / 4 / 6, DESIGN.md §4.9, profiles/r05/hex/zmerge_w1/)
+  // and above p = 12, where the three-block kernel's 3 n^3 doubles of LDS
+  // would leave one workgroup (of one element slot) per CU
   const char* re = std::getenv("SEM_HEX_ROWS");
-  c->hex->rows = re && std::atoi(re) != 0;
+  c->hex->rows = re ? std::atoi(re) != 0 : hex_rows_default(c->n);
   const char* ze = std::getenv("SEM_HEX_ZMERGE");
   c->hex->zmerge = HEX_ZMERGE && !(ze && std::atoi(ze) == 0);
   return SEM_OK;
@@ -515,6 +627,7 @@ void ctx_free(sem_ctx* c) {
   c->hex->free_plan();
   (void)hipFree(c->hex->d_map);
   (void)hipFree(c->hex->d_G);
+  (void)hipFree(c->hex->d_vx);
   delete c->hex;
   c->hex = nullptr;
 }

@@ -2637,11 +2637,19 @@ struct GeomShape {
 
 // Error-free transformations for the compensated equispaced->GLL transform:
 // a*b = p + e exactly, a + b = s + e exactly (round to nearest, no fast-math).
+// Contraction is off inside them: hipcc's default -ffp-contract=fast would
+// otherwise fuse the rounded product p of two_prod into the following
+// two_sum's addition (s = s' + a*b as one fma), so that s no longer adds the
+// p whose error e describes and the compensation is silently lost (the
+// hexahedral p = 14 geometry measured exactly the plain-float64 error,
+// 1.34e-10 of the action against the extended-precision oracle).
 __device__ __forceinline__ void two_prod(double a, double b, double& p, double& e) {
+#pragma clang fp contract(off)
   p = a * b;
   e = fma(a, b, -p);
 }
 __device__ __forceinline__ void two_sum(double a, double b, double& s, double& e) {
+#pragma clang fp contract(off)
   s = a + b;
   const double bb = s - a;
   e = (a - (s - bb)) + (b - bb);

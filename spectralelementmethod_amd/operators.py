@@ -114,7 +114,7 @@ class SEMOperator(object):
     Parameters
     ----------
     p : int
-        Polynomial order (1..16 on quadrilaterals, 1..11 on hexahedra).
+        Polynomial order (1..16 on quadrilaterals and on hexahedra).
     e2n : array-like uint32 [n_elem, p+1, p+1] or [n_elem, p+1, p+1, p+1]
         Element -> global node map (lexicographic, sem/discrete.py:1044); a
         4-D map makes a hexahedral operator (include/sem_hip.h
