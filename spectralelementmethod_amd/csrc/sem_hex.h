@@ -694,18 +694,23 @@ __global__ void __launch_bounds__(hex_threads(N))
 // product (Ogita-Rump-Oishi Dot2, semk::dot2) on coordinates relative to the
 // element's node (0,0,0), the intermediate kept as hi + lo in global scratch
 // (setup only).  Layout of every array: [E][3][n^3], local node a*n^2 + b*n + c.
-// Pass 0: the relative element coordinates from the nodes and the map.
+// Pass 0: the relative element coordinates from the nodes and the map, as
+// the exact difference hi + lo (two_sum): the rounding of a float64
+// difference alone is amplified by cond(V_eq) (9e-11 of x_phys at p = 14).
 template <int N>
 __global__ void k_hex_rel_coords(const double* __restrict__ nodes, int64_t n_node,
                                  const uint32_t* __restrict__ map, int64_t n_elem,
-                                 double* __restrict__ out) {
+                                 double* __restrict__ out, double* __restrict__ out_lo) {
   constexpr int N3 = N * N * N;
   const int64_t total = n_elem * 3 * N3;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t ek = t / N3, e = ek / 3;
     const int node = (int)(t - ek * N3), k = (int)(ek - e * 3);
-    out[t] = nodes[k * n_node + map[e * N3 + node]] - nodes[k * n_node + map[e * N3]];
+    double hi, lo;
+    semk::two_sum(nodes[k * n_node + map[e * N3 + node]], -nodes[k * n_node + map[e * N3]], hi, lo);
+    out[t] = hi;
+    out_lo[t] = lo;
   }
 }
 // One pass along axis AX (0: a, 1: b, 2: c): out = V_eq^-1 (vh + vl, an

@@ -516,7 +516,7 @@ int launch_hex_geom(sem_ctx* c, const double* nodes, double* GP, double* xph, do
   double* buf[4] = {nullptr, nullptr, nullptr, nullptr};
   const double* xrel = nullptr;
   if constexpr (N >= HEX_DOT2_MIN_N) {
-    // relative coordinates R, then R -> (A, Al) -> (R, X) -> A along xi0, xi1, xi2
+    // relative coordinates (R, Rl), then -> (A, Al) -> (R, Rl) -> A along xi0, xi1, xi2
     const int64_t total = c->n_elem * 3 * N3;
     if (!H->d_vx) HIP_TRY(hipMalloc(&H->d_vx, 2 * N * N * sizeof(double)));
     {
@@ -528,8 +528,8 @@ int launch_hex_geom(sem_ctx* c, const double* nodes, double* GP, double* xph, do
     const dim3 g(grid_for(total, 256, 16384)), bl(256);
     const double *vh = H->d_vx, *vl = H->d_vx + N * N;
     hipLaunchKernelGGL(semh::k_hex_rel_coords<N>, g, bl, 0, st, nodes, c->n_node, H->d_map,
-                       c->n_elem, buf[0]);
-    hipLaunchKernelGGL((semh::k_hex_eq2gll_pass<N, 0>), g, bl, 0, st, buf[0], nullptr, buf[1],
+                       c->n_elem, buf[0], buf[3]);
+    hipLaunchKernelGGL((semh::k_hex_eq2gll_pass<N, 0>), g, bl, 0, st, buf[0], buf[3], buf[1],
                        buf[2], vh, vl, c->n_elem * 3);
     hipLaunchKernelGGL((semh::k_hex_eq2gll_pass<N, 1>), g, bl, 0, st, buf[1], buf[2], buf[0],
                        buf[3], vh, vl, c->n_elem * 3);

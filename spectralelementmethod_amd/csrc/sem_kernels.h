@@ -2730,10 +2730,12 @@ __global__ void __launch_bounds__(GeomShape<N>::THREADS)
     x0[0] = sx[el][0][0];
     x0[1] = sx[el][1][0];
     for (int c = 0; c < 2; ++c) {
-      double xr[N];
-      for (int i = 0; i < N; ++i) xr[i] = sx[el][c][i * N + nq] - x0[c];
+      // the exact difference hi + lo (two_sum): the rounding of a float64
+      // difference alone is amplified by cond(V_eq)
+      double xr[N], xrl[N];
+      for (int i = 0; i < N; ++i) two_sum(sx[el][c][i * N + nq], -x0[c], xr[i], xrl[i]);
       double hi, lo;
-      dot2<N>(&sV[m * N], 1, xr, nullptr, 1, hi, lo);
+      dot2<N>(&sV[m * N], 1, xr, xrl, 1, hi, lo);
       st[el][c][node] = hi;
       stl[el][c][node] = lo;
     }
