@@ -2720,10 +2720,12 @@ __global__ void __launch_bounds__(GeomShape<N>::THREADS)
   // is translation invariant (V_eq reproduces constants) and J = D x_phys
   // then no longer cancels the O(1) offset against O(h) variations.
   // Both passes are compensated dot products (dot2, the intermediate kept as
-  // hi + lo): Vinv has entries up to ~170 at p = 16 (cond(V_eq) ~ 1e5), and
-  // J = D x_phys amplifies the rounding of plain float64 sums by ~n^2/4;
-  // measured on CPU emulation at p = 16: 6.8e-11 -> 1.2e-11 rel-L2 of the
-  // action against the extended-precision oracle.
+  // hi + lo) on the exact relative coordinates (two_sum): Vinv has entries
+  // up to ~170 at p = 16 (cond(V_eq) ~ 1e5), and J = D x_phys amplifies the
+  // rounding of plain float64 sums by ~n^2/4; cfg4 p = 16 on the device:
+  // 4.9e-11 -> 2.9e-12 rel-L2 of the action against the extended-precision
+  // oracle (the rounds 3-5 passes had their compensation
+  // fused away by contraction, see two_prod).
   double x0[2] = {0.0, 0.0};
   const bool given = XGin || XEin;  // x_phys given: no transform
   if (act && !given) {
