@@ -12,7 +12,9 @@ region.
   python bench.py [--gpus N] [--steps K] [--warmup W] [--p 8] [--nex 1024] [--ney 1024]
                   [--scaling strong|weak] [--op poisson|axisym_stokes|axisym_ns|pcg]
   python bench.py --dim 3 [--p 8] [--hex-ne 27] [--hex-nex L] [--gpus N]
-                  (hexahedra; N ranks = slabs of element layers along x, bench_hex)
+                  [--hex-decomp block|slab]
+                  (hexahedra, bench_hex; N ranks = boxes on a near-cubic rank grid,
+                  or slabs of element layers along x)
 
 --gpus N without a launcher: this process starts N rank processes (before
 touching the GPU) and waits for them; under torchrun (WORLD_SIZE set) each
@@ -286,26 +288,81 @@ def cpu_baseline_hex(p, warp, budget_s=20.0, workers=16):
 
 
 def _hex_partition(args, world, rank):
-    """The hexahedral workload split into `world` slabs of element layers
-    along x (distributed.SlabPartition, row N3): --hex-ne^3 warped hexahedra
-    (--hex-nex layers along x if given); --scaling weak gives every rank that
-    many layers."""
-    from spectralelementmethod_amd.distributed import SlabPartition
+    """The hexahedral workload split over `world` ranks (row N3): --hex-ne^3
+    warped hexahedra (--hex-nex elements along x if given).  --hex-decomp
+    block (default): boxes on the distributed.block_grid(world) rank grid
+    (BlockPartition; 2 x 2 x 2 at 8 ranks); slab: slabs of element layers
+    along x (SlabPartition).  --scaling weak multiplies the mesh by the rank
+    grid, so every rank keeps the one-GPU mesh."""
+    from spectralelementmethod_amd.distributed import BlockPartition, SlabPartition, block_grid
     ne = args.hex_ne
-    nex = args.hex_nex or ne
+    nex, ney, nez = args.hex_nex or ne, ne, ne
+    if args.hex_decomp == "slab" or world == 1:
+        if args.scaling == "weak":
+            nex *= world
+        return SlabPartition(nex, ney, nez, args.p, world, rank)
+    grid = block_grid(world)
     if args.scaling == "weak":
-        nex *= world
-    return SlabPartition(nex, ne, ne, args.p, world, rank)
+        nex, ney, nez = nex * grid[0], ney * grid[1], nez * grid[2]
+    return BlockPartition(nex, ney, nez, args.p, grid, rank)
+
+
+def _hex_ranges(part):
+    """Element ranges per axis of a rank's part (slab or box)."""
+    if hasattr(part, "ranges"):
+        return [tuple(r) for r in part.ranges]
+    return [(part.ex0, part.ex1), (0, part.ney), (0, part.nez)]
+
+
+def _hex_desc(part):
+    r = _hex_ranges(part)
+    kind = "box" if hasattr(part, "ranges") else "slab"
+    return "%s %s" % (kind, " x ".join("[%d,%d)" % a for a in r))
+
+
+def _hex_gid_to_local(part, gids):
+    """Local node ids of global ids that lie in the rank's node box."""
+    p = part.p
+    r = _hex_ranges(part)
+    shape = [(b - a) * p + 1 for a, b in r]
+    iz = gids % part.Nz
+    iy = (gids // part.Nz) % part.Ny
+    ix = gids // (part.Nz * part.Ny)
+    lx, ly, lz = ix - r[0][0] * p, iy - r[1][0] * p, iz - r[2][0] * p
+    assert (lx >= 0).all() and (lx < shape[0]).all() and (ly >= 0).all() and \
+        (ly < shape[1]).all() and (lz >= 0).all() and (lz < shape[2]).all()
+    return (lx * shape[1] + ly) * shape[2] + lz
+
+
+def _hex_sub_box(part, box, keep_lo_x=True):
+    """Nodes of the element box `box` (3 element ranges) whose value the box's
+    elements alone determine: along each axis the box's first and last node
+    index are dropped unless they lie on the mesh boundary (or, with
+    keep_lo_x False, the first x index is always dropped)."""
+    p = part.p
+    Ns = ((part.nex * p + 1), part.Ny, part.Nz)
+    keep = []
+    for a, (c0, c1) in enumerate(box):
+        idx = np.arange(c0 * p, c1 * p + 1)
+        m = np.ones(idx.size, dtype=bool)
+        if (c0 > 0) or (a == 0 and not keep_lo_x):
+            m[0] = False
+        if c1 * p < Ns[a] - 1:
+            m[-1] = False
+        keep.append(m)
+    return (keep[0][:, None, None] & keep[1][None, :, None] & keep[2][None, None, :]).ravel()
 
 
 def hex_parity_checks(op, y, u, part, p, warp, dev, world):
     """Parity of the timed hexahedral output against the NumPy oracle
-    (HexPoissonProblem).  One rank: the whole mesh.  Several ranks: (a) two
-    element layers in the middle of the rank's slab, compared on the inner
-    node layers of the block; (b) the two layers across the rank's right
-    face, [ex1 - 1, ex1 + 1) (the neighbour's u regenerated from the global
-    field), compared on this rank's node layers of the block, the last being
-    the shared face whose value exists only after the exchange."""
+    (HexPoissonProblem).  One rank: the whole mesh.  Several ranks: (a) a box
+    of two elements per axis in the middle of the rank's part, compared on
+    the nodes the box's elements alone determine; (b) the two element layers
+    across the rank's +x face, [ex1 - 1, ex1 + 1) (x two elements in the
+    middle of the rank's y/z range for a box, the whole y/z extent for a
+    slab; the neighbour's u regenerated from the global field), compared on
+    this rank's nodes of that box, the last x layer being the shared face
+    whose value exists only after the exchange."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import sem_oracle
     from spectralelementmethod_amd import meshgen
@@ -331,31 +388,41 @@ def hex_parity_checks(op, y, u, part, p, warp, dev, world):
         return {"rel_l2": rel(y.cpu().numpy(), ref), "tolerance": 1e-10,
                 "vs": "oracle/sem_oracle.py HexPoissonProblem (whole mesh)",
                 "oracle_sec": time.perf_counter() - t0}, None
-    face = part.face
-    nl = part.ex1 - part.ex0  # (world 1 above p = 10: a block, not the whole mesh)
-    c0 = part.ex0 + max(0, (nl - 2) // 2)
-    c1 = min(part.ex1, c0 + 2)
-    nodes, e2n, off = meshgen.structured_slab(part.nex, part.ney, part.nez, p, c0, c1, warp)
-    loc = off - part.node_offset + np.arange(nodes.shape[1])
+    rng = _hex_ranges(part)  # (world 1 above p = 10: a block, not the whole mesh)
+    slab = not hasattr(part, "ranges")
+
+    def middle(a):
+        r0, r1 = rng[a]
+        if slab and a > 0:
+            return (r0, r1)
+        c0 = r0 + max(0, (r1 - r0 - 2) // 2)
+        return (c0, min(r1, c0 + 2))
+    box = [middle(0), middle(1), middle(2)]
+    nodes, e2n, gids = meshgen.structured_box(part.nex, part.ney, part.nez, p, *box, warp=warp)
+    loc = _hex_gid_to_local(part, gids)
     y_ref = oracle(nodes, e2n, u[torch_index(loc, dev)].cpu().numpy())
-    inner = np.arange(face, nodes.shape[1] - face)
+    inner = np.flatnonzero(_hex_sub_box(part, box))
     block = {"rel_l2": rel(y[torch_index(loc[inner], dev)].cpu().numpy(), y_ref[inner]),
              "tolerance": 1e-10, "nodes_checked": int(inner.size),
-             "block": "element layers [%d, %d) of the slab" % (c0, c1), "vs": vs,
+             "block": "elements %s of the rank's %s" % (
+                 " x ".join("[%d,%d)" % b for b in box), _hex_desc(part)), "vs": vs,
              "oracle_sec": time.perf_counter() - t0}
     iface = None
-    if part.rank < world - 1:
-        c0 = part.ex1 - 1
-        nodes, e2n, off = meshgen.structured_slab(part.nex, part.ney, part.nez, p, c0, c0 + 2,
-                                                  warp)
-        gids = off + np.arange(nodes.shape[1])
+    if rng[0][1] < part.nex:
+        c0 = rng[0][1] - 1
+        box = [(c0, c0 + 2), middle(1), middle(2)]
+        nodes, e2n, gids = meshgen.structured_box(part.nex, part.ney, part.nez, p, *box,
+                                                  warp=warp)
         y_ref = oracle(nodes, e2n, global_field_at(part, gids, dev).cpu().numpy())
-        own = np.arange(face, (p + 1) * face)
-        iface = {"rel_l2": rel(y[torch_index(gids[own] - part.node_offset, dev)].cpu().numpy(),
-                               y_ref[own]),
+        sel = _hex_sub_box(part, box, keep_lo_x=False)
+        sel &= (gids // (part.Ny * part.Nz)) <= rng[0][1] * p  # this rank's x layers
+        own = np.flatnonzero(sel)
+        face = int(((gids // (part.Ny * part.Nz))[own] == rng[0][1] * p).sum())
+        iface = {"rel_l2": rel(y[torch_index(_hex_gid_to_local(part, gids[own]),
+                                             dev)].cpu().numpy(), y_ref[own]),
                  "tolerance": 1e-10, "nodes_checked": int(own.size), "interface_nodes": face,
-                 "block": "element layers [%d, %d) across the face shared with rank %d" % (
-                     c0, c0 + 2, part.rank + 1)}
+                 "block": "elements %s across the rank's +x face" % (
+                     " x ".join("[%d,%d)" % b for b in box))}
     return block, iface
 
 
@@ -384,8 +451,8 @@ def bench_hex(args):
     part = _hex_partition(args, world, rank)
     t0 = time.time()
     nodes, e2n = part.local_mesh(args.warp)
-    log("rank %d: hex slab %d layers of %dx%dx%d p=%d: %d elements, %d nodes (%.1fs)" % (
-        rank, part.ex1 - part.ex0, part.nex, part.ney, part.nez, p, e2n.shape[0],
+    log("rank %d: hex %s of %dx%dx%d p=%d: %d elements, %d nodes (%.1fs)" % (
+        rank, _hex_desc(part), part.nex, part.ney, part.nez, p, e2n.shape[0],
         nodes.shape[1], time.time() - t0))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -466,13 +533,17 @@ def bench_hex(args):
         "config": {
             "workload": "poisson hex p=%d, %dx%dx%d hexahedra%s (rows N2/N3, north_star "
                         "'quad/hex')" % (p, part.nex, part.ney, part.nez,
-                                         " in %d slabs" % world if world > 1 else ""),
+                                         (" in %d %s" % (world, "boxes %s" % "x".join(
+                                             str(g) for g in part.grid) if hasattr(part, "grid")
+                                             else "slabs")) if world > 1 else ""),
             "p": p, "ndim": 3, "geometry": "stored", "n_elem_global": part.nex * part.ney *
             part.nez, "n_elem_per_gpu": E, "ndof_global": ndof_global, "ndof_per_gpu": n_nodes,
             "ranks_seen": world,
             "parallelism": "single GPU" if world == 1 else (
-                "slabs of element layers along x x%d; interface elements on a side stream, "
-                "face exchange (transport %s) overlapped with the interior elements" % (
+                "%s x%d; interface elements on a side stream, shared-node exchange "
+                "(transport %s) overlapped with the interior elements" % (
+                    ("boxes on a %s rank grid" % "x".join(str(g) for g in part.grid))
+                    if hasattr(part, "grid") else "slabs of element layers along x",
                     world, op.transport)),
             "per_rank_ms_per_step": per_rank_ms,
             "exchange_bytes_per_step_per_rank": 2 * op.exchange_bytes,
@@ -783,6 +854,9 @@ def main():
     ap.add_argument("--hex-nex", type=int, default=None,
                     help="--dim 3: element layers along x (the slab axis; default --hex-ne), "
                          "per rank with --scaling weak")
+    ap.add_argument("--hex-decomp", choices=["block", "slab"], default="block",
+                    help="--dim 3 on N ranks: boxes on a near-cubic rank grid (block) or "
+                         "slabs of element layers along x (slab)")
     args = ap.parse_args()
 
     if args.cpu_baseline_only:  # child process: no GPU
@@ -1218,7 +1292,7 @@ def time_rank(args):
         "rank": R, "of_ranks": N, "p": p,
         "mesh": ("%dx%dx%d hexahedra (%s scaling)" % (part.nex, part.ney, part.nez, args.scaling)
                  if hexa else "%dx%d" % (args.nex, args.ney)),
-        "strip_elements": ("%d x %d x %d" % (part.ex1 - part.ex0, part.ney, part.nez) if hexa
+        "strip_elements": (_hex_desc(part) if hexa
                            else "%d x %d" % (part.ex1 - part.ex0, part.ney)), "ndof_rank": ndof,
         "exchange_bytes_per_step": 2 * exch_bytes,
         "peers": sorted(part.neighbors), "interface_elements": iface_elems,
@@ -1246,6 +1320,8 @@ def global_random_field(part, dpn, kind, ndof, dev):
     if kind != 0:
         g = torch.Generator(device=dev).manual_seed(1234)
         return torch.randn(ndof, dtype=torch.float64, device=dev, generator=g)
+    if not hasattr(part, "node_offset"):  # a box: not one contiguous global range
+        return global_field_at(part, part.local_to_global(), dev)
     # the strip's nodes are the contiguous global range [node_offset, +n_nodes)
     g = torch.Generator(device=dev).manual_seed(1234)
     n_glob = part.global_nodes

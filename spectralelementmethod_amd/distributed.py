@@ -128,6 +128,94 @@ class SlabPartition(object):
         return self.node_offset + np.arange(self.n_nodes, dtype=np.int64)
 
 
+def _split(n, parts):
+    base, extra = divmod(n, parts)
+    sizes = [base + (1 if r < extra else 0) for r in range(parts)]
+    return np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+
+
+def block_grid(world):
+    """px x py x pz = world with the factors as equal as possible (8 -> 2 x 2
+    x 2, 4 -> 2 x 2 x 1, 6 -> 3 x 2 x 1), the largest along x."""
+    best = None
+    for px in range(1, world + 1):
+        if world % px:
+            continue
+        for py in range(1, world // px + 1):
+            if (world // px) % py:
+                continue
+            pz = world // px // py
+            g = tuple(sorted((px, py, pz), reverse=True))
+            key = (max(g) - min(g), -g[0])
+            if best is None or key < best[0]:
+                best = (key, g)
+    return best[1]
+
+
+class BlockPartition(object):
+    """Hexahedral boxes of a structured nex x ney x nez cube on a px x py x
+    pz grid of ranks (rank = (rx * py + ry) * pz + rz): each rank's elements
+    are a box, its nodes the box's node box, numbered locally x-major as in
+    the cube (meshgen.structured_box).  Against SlabPartition a box exposes
+    fewer interface elements per element at the price of more peers (faces,
+    edges and corners: up to 26): at 27^3 over 8 ranks 2 x 2 x 2 boxes of
+    13-14 elements per side put about a fifth of a rank's elements on its
+    interface, 8 slabs two thirds.  Shared nodes are listed per peer in
+    global-id order on both sides; a shared node belongs to the lowest rank
+    holding it."""
+
+    def __init__(self, nex, ney, nez, p, grid, rank):
+        px, py, pz = (int(g) for g in grid)
+        self.world = world = px * py * pz
+        if not (0 <= rank < world):
+            raise ValueError("bad world/rank")
+        if nex < px or ney < py or nez < pz:
+            raise ValueError("fewer elements than ranks along an axis")
+        self.nex, self.ney, self.nez, self.p, self.rank, self.dpn = nex, ney, nez, p, rank, 1
+        self.grid = (px, py, pz)
+        cuts = [_split(nex, px), _split(ney, py), _split(nez, pz)]
+
+        def box(q):  # element ranges of rank q
+            c = np.unravel_index(q, (px, py, pz))
+            return [(int(cuts[a][c[a]]), int(cuts[a][c[a] + 1])) for a in range(3)]
+        self.ranges = box(rank)
+        self.Ny, self.Nz = ney * p + 1, nez * p + 1
+        nb = [(e0 * p, e1 * p) for e0, e1 in self.ranges]  # inclusive node ranges
+        self.shape = tuple(b - a + 1 for a, b in nb)
+        self.n_nodes = int(np.prod(self.shape))
+        self.n_elem = int(np.prod([e1 - e0 for e0, e1 in self.ranges]))
+        self.neighbors = {}
+        self.owned = np.ones(self.n_nodes, dtype=bool)
+        for q in range(world):
+            if q == rank:
+                continue
+            qb = [(e0 * p, e1 * p) for e0, e1 in box(q)]
+            inter = [(max(a[0], b[0]), min(a[1], b[1])) for a, b in zip(nb, qb)]
+            if any(lo > hi for lo, hi in inter):
+                continue
+            ax = [np.arange(lo, hi + 1) - nb[a][0] for a, (lo, hi) in enumerate(inter)]
+            loc = ((ax[0][:, None, None] * self.shape[1] + ax[1][None, :, None]) * self.shape[2]
+                   + ax[2][None, None, :]).ravel()
+            self.neighbors[q] = loc
+            if q < rank:
+                self.owned[loc] = False
+
+    @property
+    def global_nodes(self):
+        return (self.nex * self.p + 1) * self.Ny * self.Nz
+
+    def local_mesh(self, warp=0.0):
+        nodes, e2n, _ = meshgen.structured_box(self.nex, self.ney, self.nez, self.p,
+                                               *self.ranges, warp=warp)
+        return nodes, e2n
+
+    def local_to_global(self):
+        (x0, x1), (y0, y1), (z0, z1) = [(e0 * self.p, e1 * self.p) for e0, e1 in self.ranges]
+        ix, iy, iz = np.arange(x0, x1 + 1), np.arange(y0, y1 + 1), np.arange(z0, z1 + 1)
+        return ((ix[:, None, None] * self.Ny + iy[None, :, None]) * self.Nz
+                + iz[None, None, :]).ravel()
+
+
 def partition_elements(e2n, nodes, world, method="sfc"):
     """Element -> rank assignment of an arbitrary mesh in equal contiguous
     pieces of a locality-preserving element order:

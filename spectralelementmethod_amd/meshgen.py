@@ -119,6 +119,37 @@ def structured_slab(nex, ney, nez, p, ex0, ex1, warp=0.0, lo=-1.0, hi=1.0):
     return nodes, _element_map3(ex1 - ex0, ney, nez, p, Ny, Nz), ix0 * Ny * Nz
 
 
+def structured_box(nex, ney, nez, p, rx, ry, rz, warp=0.0, lo=-1.0, hi=1.0):
+    """The element box rx x ry x rz (half-open element ranges per axis) of
+    ``structured_cube(nex, ney, nez, p, warp, lo, hi)`` with its nodes
+    numbered locally (x-major, z fastest, as in the cube).  Coordinates are
+    slices of the same global linspaces with the same warp expression, so a
+    node shared by two boxes has bit-identical coordinates in both.  Returns
+    nodes [3, n_local], e2n [E_local, n, n, n] and the global node ids
+    [n_local]."""
+    (ex0, ex1), (ey0, ey1), (ez0, ez1) = rx, ry, rz
+    for (a, b), m in ((rx, nex), (ry, ney), (rz, nez)):
+        if not (0 <= a < b <= m):
+            raise ValueError("bad element range [%d, %d) of %d" % (a, b, m))
+    Nx, Ny, Nz = nex * p + 1, ney * p + 1, nez * p + 1
+    if Nx * Ny * Nz >= 2 ** 32:
+        raise ValueError("mesh too large for a uint32 element map")
+    ix = np.arange(ex0 * p, ex1 * p + 1)
+    iy = np.arange(ey0 * p, ey1 * p + 1)
+    iz = np.arange(ez0 * p, ez1 * p + 1)
+    X, Y, Z = np.meshgrid(np.linspace(lo, hi, Nx)[ix], np.linspace(lo, hi, Ny)[iy],
+                          np.linspace(lo, hi, Nz)[iz], indexing="ij")
+    if warp:
+        s = warp * np.sin(np.pi * X) * np.sin(np.pi * Y) * np.sin(np.pi * Z)
+        X = X + s
+        Y = Y + 0.5 * s
+        Z = Z - s
+    nodes = np.stack([X.ravel(), Y.ravel(), Z.ravel()])
+    e2n = _element_map3(ex1 - ex0, ey1 - ey0, ez1 - ez0, p, iy.size, iz.size)
+    gids = ((ix[:, None, None] * Ny + iy[None, :, None]) * Nz + iz[None, None, :]).ravel()
+    return nodes, e2n, gids
+
+
 def extrude(nodes2, e2n2, nez, p, z0=0.0, z1=1.0):
     """Sweep a quad mesh (nodes2 [2, N2], e2n2 [E2, n, n]) along z in nez
     uniform layers of order-p elements over [z0, z1].  Node (i2, kz) -> id

@@ -348,6 +348,53 @@ def test_slab_partition_bookkeeping():
         SlabPartition(2, 3, 3, 2, 4, 0)
 
 
+def test_block_partition_bookkeeping():
+    """BlockPartition (hexahedral boxes on a rank grid): element and
+    owned-node counts add up to the cube, every pair of ranks agrees on its
+    shared nodes (faces, edges, corners) in global numbering, and every box's
+    local mesh is the global cube's nodes and element map at its global ids,
+    bit for bit."""
+    from spectralelementmethod_amd import meshgen
+    from spectralelementmethod_amd.distributed import BlockPartition, block_grid
+    assert block_grid(8) == (2, 2, 2) and block_grid(4) == (2, 2, 1)
+    assert block_grid(2) == (2, 1, 1) and block_grid(1) == (1, 1, 1)
+    assert block_grid(12) == (3, 2, 2)
+    nex, ney, nez, p = 5, 4, 3, 2
+    gnodes, ge2n = meshgen.structured_cube(nex, ney, nez, p, warp=0.05)
+    gpos = {tuple(r): i for i, r in enumerate(ge2n.reshape(ge2n.shape[0], -1)[:, [0, -1]])}
+    for grid in [(2, 2, 2), (3, 2, 1), (1, 1, 3), (2, 1, 1)]:
+        world = int(np.prod(grid))
+        parts = [BlockPartition(nex, ney, nez, p, grid, r) for r in range(world)]
+        assert sum(pt.n_elem for pt in parts) == nex * ney * nez
+        assert sum(int(pt.owned.sum()) for pt in parts) == gnodes.shape[1]
+        seen = set()
+        for pt in parts:
+            nodes, e2n = pt.local_mesh(0.05)
+            l2g = pt.local_to_global()
+            assert np.array_equal(nodes, gnodes[:, l2g])  # bitwise, incl. the warp
+            ge = l2g[e2n.astype(np.int64)].reshape(e2n.shape[0], -1)
+            for row in ge:  # every local element is a global element, once
+                k = gpos[(row[0], row[-1])]
+                assert np.array_equal(row, ge2n[k].ravel()) and k not in seen
+                seen.add(k)
+            for q, loc in pt.neighbors.items():
+                ga = l2g[loc]
+                gb = parts[q].local_to_global()[parts[q].neighbors[pt.rank]]
+                assert np.array_equal(ga, gb) and np.all(np.diff(ga) > 0)
+            # a node is shared with exactly the ranks whose node boxes hold it
+            cnt = np.zeros(pt.n_nodes, dtype=np.int64)
+            for loc in pt.neighbors.values():
+                cnt[loc] += 1
+            holders = np.zeros(gnodes.shape[1], dtype=np.int64)
+            for o in parts:
+                holders[o.local_to_global()] += 1
+            assert np.array_equal(cnt + 1, holders[l2g])
+        assert len(seen) == ge2n.shape[0]
+    assert len(BlockPartition(nex, ney, nez, p, (2, 2, 2), 0).neighbors) == 7  # faces+edges+corner
+    with pytest.raises(ValueError):
+        BlockPartition(1, 3, 3, 2, (2, 1, 1), 0)
+
+
 def _dd_worker_hex(rank, world, port, mode, q):
     """The overlapped step's protocol (DDPlan + dd_step_reference) on a
     hexahedral slab / generic partition, hexahedral oracle stand-ins for the
@@ -362,9 +409,10 @@ def _dd_worker_hex(rank, world, port, mode, q):
     try:
         import sem_oracle
         from spectralelementmethod_amd import meshgen
-        from spectralelementmethod_amd.distributed import (DDPlan, GenericPartition, SlabPartition,
-                                                           dd_step_reference, partition_elements,
-                                                           torch_p2p_exchange)
+        from spectralelementmethod_amd.distributed import (BlockPartition, DDPlan,
+                                                           GenericPartition, SlabPartition,
+                                                           block_grid, dd_step_reference,
+                                                           partition_elements, torch_p2p_exchange)
         gll = np.load(os.path.join(ROOT, "tests", "golden", "gll.npz"))
         p, nex, ney, nez = 3, 5, 2, 2
         half = gll["half_%d" % p]
@@ -373,6 +421,9 @@ def _dd_worker_hex(rank, world, port, mode, q):
         y_glob = sem_oracle.HexPoissonProblem(gnodes, ge2n, half).apply(u_glob)
         if mode == "slab":
             part = SlabPartition(nex, ney, nez, p, world, rank)
+            nodes, e2n = part.local_mesh(0.05)
+        elif mode == "block":
+            part = BlockPartition(nex, ney, nez, p, block_grid(world), rank)
             nodes, e2n = part.local_mesh(0.05)
         else:
             part = GenericPartition(ge2n, partition_elements(ge2n, gnodes, world, "sfc"), world,
@@ -398,7 +449,8 @@ def _dd_worker_hex(rank, world, port, mode, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,mode", [(2, "slab"), (3, "slab"), (2, "generic")])
+@pytest.mark.parametrize("world,mode", [(2, "slab"), (3, "slab"), (2, "generic"), (4, "block"),
+                                        (8, "block")])
 def test_overlapped_protocol_hex_gloo(world, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
