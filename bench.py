@@ -13,8 +13,8 @@ region.
                   [--scaling strong|weak] [--op poisson|axisym_stokes|axisym_ns|pcg]
   python bench.py --dim 3 [--p 8] [--hex-ne 27] [--hex-nex L] [--gpus N]
                   [--hex-decomp block|slab]
-                  (hexahedra, bench_hex; N ranks = boxes on a near-cubic rank grid,
-                  or slabs of element layers along x)
+                  (hexahedra, bench_hex; N ranks = slabs of element layers along x,
+                  or boxes on a near-cubic rank grid)
 
 --gpus N without a launcher: this process starts N rank processes (before
 touching the GPU) and waits for them; under torchrun (WORLD_SIZE set) each
@@ -290,9 +290,10 @@ def cpu_baseline_hex(p, warp, budget_s=20.0, workers=16):
 def _hex_partition(args, world, rank):
     """The hexahedral workload split over `world` ranks (row N3): --hex-ne^3
     warped hexahedra (--hex-nex elements along x if given).  --hex-decomp
-    block (default): boxes on the distributed.block_grid(world) rank grid
-    (BlockPartition; 2 x 2 x 2 at 8 ranks); slab: slabs of element layers
-    along x (SlabPartition).  --scaling weak multiplies the mesh by the rank
+    slab (default): slabs of element layers along x (SlabPartition); block:
+    boxes on the distributed.block_grid(world) rank grid (BlockPartition;
+    2 x 2 x 2 at 8 ranks; ahead of slabs from about 54^3 on, behind them at
+    27^3).  --scaling weak multiplies the mesh by the rank
     grid, so every rank keeps the one-GPU mesh."""
     from spectralelementmethod_amd.distributed import BlockPartition, SlabPartition, block_grid
     ne = args.hex_ne
@@ -854,9 +855,9 @@ def main():
     ap.add_argument("--hex-nex", type=int, default=None,
                     help="--dim 3: element layers along x (the slab axis; default --hex-ne), "
                          "per rank with --scaling weak")
-    ap.add_argument("--hex-decomp", choices=["block", "slab"], default="block",
-                    help="--dim 3 on N ranks: boxes on a near-cubic rank grid (block) or "
-                         "slabs of element layers along x (slab)")
+    ap.add_argument("--hex-decomp", choices=["block", "slab"], default="slab",
+                    help="--dim 3 on N ranks: slabs of element layers along x (slab) or "
+                         "boxes on a near-cubic rank grid (block)")
     args = ap.parse_args()
 
     if args.cpu_baseline_only:  # child process: no GPU
