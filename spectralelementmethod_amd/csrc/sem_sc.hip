@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <string>
 
 #include "sem_internal.h"
@@ -184,86 +185,111 @@ __global__ void k_band_fill(int64_t n, int KU, int W, const int64_t* __restrict_
     }
 }
 
-// One workgroup: the elimination is a chain of n dependent steps; each step
-// (pivot search over kl + 1 entries, row swap over KU + 1 columns, rank-1
-// update of a kl x KU block) is spread over the workgroup.  The multipliers
-// replace column j below the diagonal (LAPACK's in-place L), so any kl fits.  b is eliminated
-// alongside; then the column-oriented back substitution (U's column j above
-// the diagonal is contiguous in this layout).  info = j + 1 for an exactly
-// zero pivot in column j (LAPACK's convention), 0 otherwise.
-__global__ void __launch_bounds__(BLU)
-    k_band_lu_solve(int64_t n, int kl, int KU, int W, double* __restrict__ AB,
-                    double* __restrict__ b, double* __restrict__ x, int* __restrict__ info) {
-  __shared__ double s_val[BLU];
-  __shared__ int s_idx[BLU];
+// The elimination is a chain of n dependent steps.  Step j: the pivot
+// search over the kl + 1 entries of column j (fixed order: the largest
+// |a|, the lowest row on ties), the row swap over KU + 1 columns, the
+// multipliers (they replace column j below the diagonal, LAPACK's in-place
+// L, so any kl fits) and b's update -- band_pivot, one workgroup -- then
+// the rank-1 update of the kl x KU block below and right of the pivot --
+// band_update.  b is eliminated alongside; then the column-oriented back
+// substitution (U's column j above the diagonal is contiguous in this
+// layout).  info = j + 1 for an exactly zero pivot in column j (LAPACK's
+// convention), 0 otherwise.
+//
+// Two schedules, bitwise the same result (every entry gets the same fma in
+// the same order of steps; tests/test_gpu_facade.py):
+//  * narrow bands: the whole chain in one workgroup (k_band_lu_solve), the
+//    update spread over its 1024 threads -- 2.8 us per step at kl = ku = 8
+//    at any n, 6.6 at 64, but the update is one CU's work: 62 us per step at
+//    kl = ku = 256, 452 us at 1024 (profiles/r06/band_lu_timing.json);
+//  * wide bands (kl * (kl + ku) >= SEM_BAND_STEP_MIN, default 12288, or
+//    SEM_BAND_LU_STEPS=1): two launches per step on the caller's stream,
+//    band_pivot in one workgroup and band_update over the whole device,
+//    then the back substitution in one workgroup -- 7.1-7.4 us per step
+//    (launch-bound) from kl = ku = 8 to 256, 15.6 at 1024.
+__device__ __forceinline__ bool band_pivot(int64_t n, int kl, int KU, int W,
+                                           double* __restrict__ AB, double* __restrict__ b,
+                                           int* __restrict__ info, int64_t j, double* s_val,
+                                           int* s_idx) {
   const int tid = threadIdx.x;
-  for (int64_t j = 0; j < n; ++j) {
-    const int64_t ilast = min<int64_t>(n - 1, j + kl);
-    const int nr = (int)(ilast - j);  // rows below the diagonal
-    double best = -1.0;
-    int bi = 0;
-    for (int r = tid; r <= nr; r += BLU) {
-      const double a = fabs(AB[j * W + r + KU]);
-      if (a > best) {
-        best = a;
-        bi = r;
+  const int64_t ilast = min<int64_t>(n - 1, j + kl);
+  const int nr = (int)(ilast - j);  // rows below the diagonal
+  double best = -1.0;
+  int bi = 0;
+  for (int r = tid; r <= nr; r += BLU) {
+    const double a = fabs(AB[j * W + r + KU]);
+    if (a > best) {
+      best = a;
+      bi = r;
+    }
+  }
+  s_val[tid] = best;
+  s_idx[tid] = bi;
+  __syncthreads();
+  for (int o = BLU / 2; o > 0; o >>= 1) {
+    if (tid < o) {
+      const double v2 = s_val[tid + o];
+      const int i2 = s_idx[tid + o];
+      if (v2 > s_val[tid] || (v2 == s_val[tid] && i2 < s_idx[tid])) {
+        s_val[tid] = v2;
+        s_idx[tid] = i2;
       }
-    }
-    s_val[tid] = best;
-    s_idx[tid] = bi;
-    __syncthreads();
-    for (int o = BLU / 2; o > 0; o >>= 1) {
-      if (tid < o) {
-        const double v2 = s_val[tid + o];
-        const int i2 = s_idx[tid + o];
-        if (v2 > s_val[tid] || (v2 == s_val[tid] && i2 < s_idx[tid])) {
-          s_val[tid] = v2;
-          s_idx[tid] = i2;
-        }
-      }
-      __syncthreads();
-    }
-    const double pv = s_val[0];
-    const int p = s_idx[0];
-    if (!(pv > 0.0)) {  // exactly zero (or NaN) pivot column
-      if (tid == 0) *info = (int)(j + 1);
-      return;           // uniform: every thread read the same s_val[0]
-    }
-    const int64_t klast = min<int64_t>(n - 1, j + KU);
-    if (p != 0) {
-      for (int64_t k = j + tid; k <= klast; k += BLU) {
-        double* a = AB + k * W + (j - k + KU);
-        const double t = a[0];
-        a[0] = a[p];
-        a[p] = t;
-      }
-      if (tid == 0) {
-        const double t = b[j];
-        b[j] = b[j + p];
-        b[j + p] = t;
-      }
-    }
-    __syncthreads();
-    const double inv = 1.0 / AB[j * W + KU];
-    const double bj = b[j];
-    double* lcol = AB + j * W + KU;  // (j + r, j) at lcol[r]
-    for (int r = 1 + tid; r <= nr; r += BLU) {
-      const double l = lcol[r] * inv;
-      lcol[r] = l;
-      b[j + r] = fma(-l, bj, b[j + r]);
-    }
-    __syncthreads();
-    // A(j + r, k) -= l_r A(j, k) for r in [1, nr], k in (j, klast]
-    const int nc = (int)(klast - j);
-    const int64_t tot = (int64_t)nr * nc;
-    for (int64_t t = tid; t < tot; t += BLU) {
-      const int c = 1 + (int)(t / nr), r = 1 + (int)(t % nr);
-      double* col = AB + (j + c) * W + (KU - c);  // (i, j + c) at col[i - j]
-      col[r] = fma(-lcol[r], col[0], col[r]);
     }
     __syncthreads();
   }
-  // back substitution, column-oriented: x_j = b_j / U_jj, then b_i -= U_ij x_j
+  const double pv = s_val[0];
+  const int p = s_idx[0];
+  if (!(pv > 0.0)) {  // exactly zero (or NaN) pivot column
+    if (tid == 0) *info = (int)(j + 1);
+    return false;     // uniform: every thread read the same s_val[0]
+  }
+  const int64_t klast = min<int64_t>(n - 1, j + KU);
+  if (p != 0) {
+    for (int64_t k = j + tid; k <= klast; k += BLU) {
+      double* a = AB + k * W + (j - k + KU);
+      const double t = a[0];
+      a[0] = a[p];
+      a[p] = t;
+    }
+    if (tid == 0) {
+      const double t = b[j];
+      b[j] = b[j + p];
+      b[j + p] = t;
+    }
+  }
+  __syncthreads();
+  const double inv = 1.0 / AB[j * W + KU];
+  const double bj = b[j];
+  double* lcol = AB + j * W + KU;  // (j + r, j) at lcol[r]
+  for (int r = 1 + tid; r <= nr; r += BLU) {
+    const double l = lcol[r] * inv;
+    lcol[r] = l;
+    b[j + r] = fma(-l, bj, b[j + r]);
+  }
+  return true;
+}
+
+// A(j + r, j + c) -= l_r A(j, j + c) for r in [1, nr], c in [1, nc]: entries
+// t0, t0 + stride, ... of the nr x nc block, r fastest (a column of the
+// block is contiguous in the band layout)
+__device__ __forceinline__ void band_update(int64_t n, int kl, int KU, int W,
+                                            double* __restrict__ AB, int64_t j, int64_t t0,
+                                            int64_t stride) {
+  const int nr = (int)(min<int64_t>(n - 1, j + kl) - j);
+  const int nc = (int)(min<int64_t>(n - 1, j + KU) - j);
+  const double* lcol = AB + j * W + KU;
+  const int64_t tot = (int64_t)nr * nc;
+  for (int64_t t = t0; t < tot; t += stride) {
+    const int c = 1 + (int)(t / nr), r = 1 + (int)(t % nr);
+    double* col = AB + (j + c) * W + (KU - c);  // (i, j + c) at col[i - j]
+    col[r] = fma(-lcol[r], col[0], col[r]);
+  }
+}
+
+__device__ __forceinline__ void band_backsub(int64_t n, int KU, int W,
+                                             const double* __restrict__ AB,
+                                             double* __restrict__ b, double* __restrict__ x) {
+  const int tid = threadIdx.x;
   for (int64_t j = n - 1; j >= 0; --j) {
     const double xj = b[j] / AB[j * W + KU];
     __syncthreads();  // every thread read b[j] before it can change again
@@ -272,7 +298,58 @@ __global__ void __launch_bounds__(BLU)
     for (int64_t i = i0 + tid; i < j; i += BLU) b[i] = fma(-AB[j * W + (i - j + KU)], xj, b[i]);
     __syncthreads();
   }
-  if (tid == 0) *info = 0;
+}
+
+__global__ void __launch_bounds__(BLU)
+    k_band_lu_solve(int64_t n, int kl, int KU, int W, double* __restrict__ AB,
+                    double* __restrict__ b, double* __restrict__ x, int* __restrict__ info) {
+  __shared__ double s_val[BLU];
+  __shared__ int s_idx[BLU];
+  for (int64_t j = 0; j < n; ++j) {
+    if (!band_pivot(n, kl, KU, W, AB, b, info, j, s_val, s_idx)) return;
+    __syncthreads();
+    band_update(n, kl, KU, W, AB, j, threadIdx.x, BLU);
+    __syncthreads();
+  }
+  band_backsub(n, KU, W, AB, b, x);
+  if (threadIdx.x == 0) *info = 0;
+}
+
+// the wide-band schedule: one launch of each per step, then k_band_backsub;
+// a step after a zero pivot does nothing (info is set)
+__global__ void __launch_bounds__(BLU)
+    k_band_step_pivot(int64_t n, int kl, int KU, int W, double* __restrict__ AB,
+                      double* __restrict__ b, int* __restrict__ info, int64_t j) {
+  __shared__ double s_val[BLU];
+  __shared__ int s_idx[BLU];
+  if (*info) return;  // uniform
+  band_pivot(n, kl, KU, W, AB, b, info, j, s_val, s_idx);
+}
+
+constexpr int BLU_UPD = 256;
+__global__ void __launch_bounds__(BLU_UPD)
+    k_band_step_update(int64_t n, int kl, int KU, int W, double* __restrict__ AB,
+                       const int* __restrict__ info, int64_t j) {
+  if (*info) return;  // uniform
+  band_update(n, kl, KU, W, AB, j, (int64_t)blockIdx.x * BLU_UPD + threadIdx.x,
+              (int64_t)gridDim.x * BLU_UPD);
+}
+
+__global__ void __launch_bounds__(BLU)
+    k_band_backsub(int64_t n, int KU, int W, const double* __restrict__ AB,
+                   double* __restrict__ b, double* __restrict__ x, const int* __restrict__ info) {
+  if (*info) return;  // uniform
+  band_backsub(n, KU, W, AB, b, x);
+}
+
+bool band_steps(int kl, int KU) {
+  if (const char* e = getenv("SEM_BAND_LU_STEPS")) {
+    if (e[0] == '0') return false;
+    if (e[0] == '1') return true;
+  }
+  int64_t lim = 12288;
+  if (const char* e = getenv("SEM_BAND_STEP_MIN")) lim = atoll(e);
+  return (int64_t)kl * KU >= lim;
 }
 
 }  // namespace
@@ -329,7 +406,25 @@ int sem_band_lu_solve(int64_t n, int kl, int ku, const int64_t* d_rowptr, const 
   const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(k_band_fill, dim3(grid), dim3(256), 0, st, n, KU, W, d_rowptr, d_colind, d_val,
                      AB);
-  hipLaunchKernelGGL(k_band_lu_solve, dim3(1), dim3(BLU), 0, st, n, kl, KU, W, AB, b, d_x, d_info);
+  if (band_steps(kl, KU)) {
+    HIP_TRY(hipMemsetAsync(d_info, 0, sizeof(int), st));
+    for (int64_t j = 0; j < n; ++j) {
+      const int64_t nr = std::min<int64_t>(n - 1, j + kl) - j;
+      const int64_t nc = std::min<int64_t>(n - 1, j + KU) - j;
+      hipLaunchKernelGGL(k_band_step_pivot, dim3(1), dim3(BLU), 0, st, n, kl, KU, W, AB, b, d_info,
+                         j);
+      const int64_t tot = nr * nc;
+      if (tot > 0) {
+        const int g = (int)std::min<int64_t>((tot + BLU_UPD - 1) / BLU_UPD, 2048);
+        hipLaunchKernelGGL(k_band_step_update, dim3(g), dim3(BLU_UPD), 0, st, n, kl, KU, W, AB,
+                           d_info, j);
+      }
+    }
+    hipLaunchKernelGGL(k_band_backsub, dim3(1), dim3(BLU), 0, st, n, KU, W, AB, b, d_x, d_info);
+  } else {
+    hipLaunchKernelGGL(k_band_lu_solve, dim3(1), dim3(BLU), 0, st, n, kl, KU, W, AB, b, d_x,
+                       d_info);
+  }
   HIP_TRY(hipGetLastError());
   int h_info = 0;
   HIP_TRY(hipMemcpyAsync(&h_info, d_info, sizeof(int), hipMemcpyDeviceToHost, st));

@@ -278,6 +278,55 @@ def test_band_lu_solve_wide_band():
     assert rel_l2(x, ref) < 1e-9
 
 
+def test_band_lu_step_schedule_is_bitwise():
+    """The wide-band schedule of sem_band_lu_solve (two launches per
+    elimination step, the rank-1 update over the whole device) against the
+    one-workgroup kernel: bitwise the same solution (every entry gets the
+    same fma in the same step order), on a pivoting band (kl = 37) and an
+    uneven one (kl = 90, ku = 20); an exactly singular matrix gives NaN and
+    the MatrixRankWarning on both schedules."""
+    import os
+    from scipy import sparse
+    from scipy.sparse import linalg as spla
+    from scipy.sparse.linalg import MatrixRankWarning
+    from spectralelementmethod_amd.discrete import band_lu_solve
+    rng = np.random.default_rng(13)
+    dev = torch.device("cuda", 0)
+    old = os.environ.get("SEM_BAND_LU_STEPS")
+    try:
+        for n, kl, ku in [(1500, 37, 37), (1200, 90, 20)]:
+            offs = list(range(-kl, ku + 1))
+            A = sparse.diags([rng.standard_normal(n - abs(k)) for k in offs], offs,
+                             format="lil")
+            A.setdiag(1e-3 * rng.standard_normal(n))
+            A = A.tocsr()
+            b = rng.standard_normal(n)
+            xs = {}
+            for mode in ("0", "1"):
+                os.environ["SEM_BAND_LU_STEPS"] = mode
+                xs[mode] = band_lu_solve(A, b, dev)
+            assert np.array_equal(xs["0"], xs["1"])
+            if kl == ku:
+                assert rel_l2(xs["1"], spla.spsolve(A.tocsc(), b)) < 1e-10
+            else:  # ill-conditioned: backward stable, as partial pivoting is
+                x = xs["1"]
+                res = np.linalg.norm(A @ x - b) / (abs(A).max() * np.linalg.norm(x) * n)
+                assert res < 1e-14, res
+        S = A.toarray()
+        S[7, :] = 0.0
+        S[:, 7] = 0.0
+        S = sparse.csr_matrix(S)
+        for mode in ("0", "1"):
+            os.environ["SEM_BAND_LU_STEPS"] = mode
+            with pytest.warns(MatrixRankWarning):
+                assert np.isnan(band_lu_solve(S, b, dev)).all()
+    finally:
+        if old is None:
+            os.environ.pop("SEM_BAND_LU_STEPS", None)
+        else:
+            os.environ["SEM_BAND_LU_STEPS"] = old
+
+
 def test_static_condensation_nonsymmetric_device_solve():
     """The condensed exterior system of non-symmetric local systems (the
     shape of the axisymmetric Stokes / Navier-Stokes block the squirmer

@@ -58,5 +58,13 @@ def run(n, bw, dev, check=True):
 if __name__ == "__main__":
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    for n, bw in [(2000, 8), (20000, 8), (200000, 8), (20000, 64), (20000, 256), (5000, 1024)]:
-        run(n, bw, dev, check=n * bw <= 5_000_000)
+    # both schedules (SEM_BAND_LU_STEPS 0: one workgroup; 1: two launches per step)
+    for mode in ("0", "1"):
+        os.environ["SEM_BAND_LU_STEPS"] = mode
+        print(json.dumps({"schedule": "one workgroup" if mode == "0" else "launches per step"}),
+              flush=True)
+        for n, bw in [(2000, 8), (20000, 8), (20000, 32), (20000, 48), (20000, 64),
+                      (20000, 96), (20000, 128), (20000, 256), (5000, 1024)]:
+            if mode == "0" and bw >= 1024:
+                n = 2000
+            run(n, bw, dev, check=n * bw <= 5_000_000)
