@@ -136,7 +136,8 @@ void sem_ctx_destroy(sem_ctx* ctx);
  *     cap, [7] launch positions, [8] sub-chains, [9] seam nodes, [10] slotted
  *     writes, [11] plain stores, [12] threads per workgroup, [13] 3, [14]
  *     geometry ready, [15] action kernel (1 row form, 0 three-block),
- *     [16] xi2 faces merged in LDS (z-merge). */
+ *     [16] xi2 faces merged in LDS (z-merge), [17] xi1 faces merged in LDS
+ *     too (y-merge): slots per row of the workgroup's slot grid, 0 = off. */
 int sem_ctx_create_nd(sem_ctx** out, int ndim, int p, int64_t n_elem, int64_t n_node, int dpn,
                       int device);
 

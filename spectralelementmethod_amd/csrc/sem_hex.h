@@ -72,6 +72,22 @@ enum { HEX_SET = 0, HEX_ACC = 1, HEX_DIAG = 2 };
 #endif
 constexpr bool HEX_ZMERGE = SEM_HEX_ZMERGE != 0;
 
+// y-merge (three-block kernel, with the z-merge): the S slots of a
+// workgroup form a Y x Z grid (Z = hex_grid_z(n) slots along xi2 per row, Y
+// rows along xi1; Y = 1 when S is prime), and slot s hands its xi1 = 0 face
+// to slot s - Z when that face IS slot s - Z's xi1 = n-1 face at every chain
+// step (cflag bit 3, checked by the planner), through the w2 block.  Columns
+// a slot already handed over in the z-merge (c = 0) stay out of the y-merge
+// on both sides.  p = 1 / 2 / 3 / 4 / 7: 8 x 8, 4 x 7, 4 x 4, 2 x 5, 2 x 2
+// slots; on by default at p <= 3 (sem_hex.hip ctx_init), SEM_HEX_YMERGE=1 / 0
+// in the environment forces it.
+constexpr int hex_grid_z(int n) {
+  int z = hex_slots(n);
+  for (int y = 2; y * y <= hex_slots(n); ++y)
+    if (hex_slots(n) % y == 0) z = hex_slots(n) / y;
+  return z;
+}
+
 // D as a kernel argument: the wave-uniform coefficients of the
 // register-direction contractions (row a of D, for d0 = D u and y += D^T w0
 // along xi0) are read with scalar loads (SGPR operands) instead of LDS
@@ -159,10 +175,23 @@ __global__ void __launch_bounds__(hex_threads(N), hex_min_waves(N))
   // chain step); the merged node then has one writer fewer
   const bool give = (cf & 4) && c == 0;
   [[maybe_unused]] const bool take = active && c == N - 1 && s + 1 < S && (P.cflag[w * S + s + 1] & 4);
+  // y-merge: slot s hands its xi1 = 0 face (b = 0) to slot s - GZ, except
+  // the column it already handed over in the z-merge (or whose receiver did)
+  constexpr int GZ = hex_grid_z(N);
+  constexpr bool YM = ZM && GZ < S;
+  [[maybe_unused]] bool ygive = false, ytake = false;
+  if constexpr (YM) {
+    ygive = (cf & 8) && b == 0 && s >= GZ &&
+            !(c == 0 && ((cf & 4) || (P.cflag[w * S + s - GZ] & 4)));
+    if (active && b == N - 1 && s + GZ < S) {
+      const uint8_t cg = P.cflag[w * S + s + GZ];
+      ytake = (cg & 8) && !(c == 0 && ((cg & 4) || (cf & 4)));
+    }
+  }
   [[maybe_unused]] bool wg_merge = false;
   if constexpr (ZM)
 #pragma unroll
-    for (int t = 1; t < S; ++t) wg_merge |= (P.cflag[w * S + t] & 4) != 0;
+    for (int t = 1; t < S; ++t) wg_merge |= (P.cflag[w * S + t] & 12) != 0;
   double* const face = P.slot + P.face_base + (int64_t)(w * S + sl) * 2 * N2 + bc;
   __syncthreads();  // sD
   double carry = 0.0;
@@ -296,12 +325,23 @@ __global__ void __launch_bounds__(hex_threads(N), hex_min_waves(N))
       if (take)
 #pragma unroll
         for (int a = 0; a < N; ++a) yv[a] += sA[sl * N2 + a * N + b];
-      // the diagonal writes sA (G11) at the top of the next step before any
-      // barrier: every take must have read the merged face first (the
-      // action writes sA only after that step's first barrier)
+      if constexpr (YM) {
+        // after this thread's z-take: a column that received the z-merged
+        // face passes it on (the edge node of four slots ends in one column)
+        if (ygive)
+#pragma unroll
+          for (int a = 0; a < N; ++a) sB[(sl - GZ) * N2 + a * N + c] = yv[a];
+        __syncthreads();
+        if (ytake)
+#pragma unroll
+          for (int a = 0; a < N; ++a) yv[a] += sB[sl * N2 + a * N + c];
+      }
+      // the diagonal writes sA / sB (G11 / G22) at the top of the next step
+      // before any barrier: every take must have read the merged faces first
+      // (the action writes them only after that step's first barrier)
       if constexpr (MODE == HEX_DIAG) __syncthreads();
     }
-    if (active && !give) {
+    if (active && !give && !ygive) {
       if (k > 0) yv[0] += carry;
       const bool last = k == L - 1;
       if (!last) carry = yv[N - 1];

@@ -43,6 +43,9 @@ struct HexState {
   // xi2 faces between the slots of a workgroup summed in LDS (both kernels;
   // SEM_HEX_ZMERGE=0 turns it off)
   bool zmerge = false;
+  // xi1 faces between the rows of a workgroup's slot grid too (three-block
+  // kernel only; SEM_HEX_YMERGE=0 turns it off)
+  bool ymerge = false;
   // diagnostics (sem_plan_info)
   int64_t n_chains = 0, n_subchains = 0, chain_len = 0, n_direct = 0;
 
@@ -119,8 +122,19 @@ struct HexPlanHost {
   int64_t n_slot = 0, face_base = 0, n_chains = 0, n_sub = 0, lc = 0, n_direct = 0;
 };
 
+// hash of an element face given as n^2 entries at f[i * stride1 + j * stride2]
+uint64_t face_hash_strided(const uint32_t* f, int n, int stride1, int stride2) {
+  uint64_t h = 0x9E3779B97F4A7C15ull;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      h ^= f[i * stride1 + j * stride2] + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+      h *= 0xBF58476D1CE4E5B9ull;
+    }
+  return h ^ (h >> 31);
+}
+
 int hex_build_plan(const std::vector<uint32_t>& h, int64_t E, int64_t n_node, int N,
-                   int64_t resident, bool zmerge, HexPlanHost& P) {
+                   int64_t resident, bool zmerge, bool ymerge, HexPlanHost& P) {
   const int N2 = N * N;
   const int64_t N3 = (int64_t)N2 * N;
   const int S = semh::hex_slots(N), NBC = semh::hex_nbc(N);
@@ -174,8 +188,18 @@ int hex_build_plan(const std::vector<uint32_t>& h, int64_t E, int64_t n_node, in
   //    729 workgroups in one generation -- 0.271 against 0.278 ms per step
   //    for the round's first rule (lc = 3, 2.85 generations) and 0.275 /
   //    0.288 / 0.305 for lc = 5 / 4 / 7 (profiles/r05/hex/chain_length/).
+  //    A workgroup also pays a fixed start (D into LDS, its flags, the
+  //    first map rows) worth about one element step: cost = generations x
+  //    (sub-chain length + 1).  Without that term the rule took sub-chains
+  //    of one element at p = 1 / 3 / 6 / 7 (~1e7 DOF, many generations
+  //    either way): 1.431 / 0.418 / 0.285 / 0.268 ms per step against 1.193
+  //    / 0.397 / 0.277 / 0.258 with it (sub-chains of 12 / 14 / 8 / 15);
+  //    the other orders keep their plan (profiles/r06/hex_chain_start/).
+  //    SEM_HEX_CHAIN_START sets the term.
   int64_t lc = 1;
   {
+    double start = 1.0;
+    if (const char* e = std::getenv("SEM_HEX_CHAIN_START")) start = std::atof(e);
     double best = 0.0;
     for (int64_t c = 1; c <= 16; ++c) {
       int64_t nsub = 0, maxlen = 0;
@@ -187,7 +211,7 @@ int hex_build_plan(const std::vector<uint32_t>& h, int64_t E, int64_t n_node, in
       }
       const int64_t nwg = (nsub + S - 1) / S;
       const int64_t gens = resident > 0 ? (nwg + resident - 1) / resident : 1;
-      const double cost = (double)gens * (double)maxlen;
+      const double cost = (double)gens * ((double)maxlen + start);
       if (c == 1 || cost <= best) {
         best = cost;
         lc = c;
@@ -230,42 +254,138 @@ int hex_build_plan(const std::vector<uint32_t>& h, int64_t E, int64_t n_node, in
     for (size_t i = 0; i < idx.size(); ++i) sorted[i] = sub[idx[i]];
     sub.swap(sorted);
   }
-  // 5. workgroups of S equal-length sub-chains
-  std::vector<int64_t> sub_wg(sub.size()), sub_slot(sub.size());
+  // 5. workgroups of S equal-length sub-chains.  With the y-merge the S
+  //    slots form a GY x GZ grid: row r of a workgroup is GZ sub-chains that
+  //    follow each other along xi2 (xi2 = n-1 face of one = xi2 = 0 face of
+  //    the next at every step), row r + 1 the xi1-neighbours of row r.  A
+  //    workgroup whose first row cannot be completed (mesh edge, irregular
+  //    numbering) takes the next free sub-chains of its length in order, as
+  //    without the y-merge; so does the rest of a grid that ends early.
+  const int GZ = semh::hex_grid_z(N), GY = S / GZ;
+  const bool grid = zmerge && ymerge && GY >= 2;
+  const size_t nsub = sub.size();
+  // same-length neighbour along xi2 (kind 0) / xi1 (kind 1): its face 0
+  // equals my face n-1 at every step
+  auto face_ptr = [&](int64_t e, int kind, int side, int& st1, int& st2) -> const uint32_t* {
+    // kind 0: xi2 face c = side: entries (a, b) at a*N2 + b*N; kind 1: xi1
+    // face b = side: entries (a, c) at a*N2 + c
+    if (kind == 0) {
+      st1 = N2;
+      st2 = N;
+      return &h[e * N3 + side];
+    }
+    st1 = N2;
+    st2 = 1;
+    return &h[e * N3 + (int64_t)side * N];
+  };
+  auto same_faces = [&](int64_t i, int64_t j, int kind) -> bool {
+    if (sub[i].len != sub[j].len) return false;
+    for (int64_t k = 0; k < sub[i].len; ++k) {
+      int a1, a2, b1, b2;
+      const uint32_t* f1 = face_ptr(order[sub[i].start + k], kind, N - 1, a1, a2);
+      const uint32_t* f2 = face_ptr(order[sub[j].start + k], kind, 0, b1, b2);
+      for (int x = 0; x < N; ++x)
+        for (int y = 0; y < N; ++y)
+          if (f1[x * a1 + y * a2] != f2[x * b1 + y * b2]) return false;
+    }
+    return true;
+  };
+  std::vector<int64_t> nbr[2];
+  if (grid)
+    for (int kind = 0; kind < 2; ++kind) {
+      nbr[kind].assign(nsub, -1);
+      std::unordered_map<uint64_t, int64_t> head;
+      head.reserve(nsub * 2);
+      for (size_t j = 0; j < nsub; ++j) {
+        int s1, s2;
+        const uint32_t* f = face_ptr(order[sub[j].start], kind, 0, s1, s2);
+        auto it = head.emplace(face_hash_strided(f, N, s1, s2), (int64_t)j);
+        if (!it.second) it.first->second = -1;  // ambiguous
+      }
+      for (size_t i = 0; i < nsub; ++i) {
+        int s1, s2;
+        const uint32_t* f = face_ptr(order[sub[i].start], kind, N - 1, s1, s2);
+        auto it = head.find(face_hash_strided(f, N, s1, s2));
+        if (it == head.end() || it->second < 0 || it->second == (int64_t)i) continue;
+        if (same_faces((int64_t)i, it->second, kind)) nbr[kind][i] = it->second;
+      }
+    }
+  std::vector<int64_t> sub_wg(nsub, -1), sub_slot(nsub, -1);
+  std::vector<uint8_t> grid_wg;
   int64_t pos = 0;
-  for (size_t i = 0; i < sub.size();) {
-    const int64_t len = sub[i].len;
-    size_t j = i;
-    while (j < sub.size() && j - i < (size_t)S && sub[j].len == len) ++j;
+  size_t cur = 0;  // first sub-chain not yet placed
+  std::vector<int64_t> slots(S);
+  while (true) {
+    while (cur < nsub && sub_wg[cur] >= 0) ++cur;
+    if (cur >= nsub) break;
+    const int64_t len = sub[cur].len;
     const int64_t w = (int64_t)P.wg_off.size();
+    std::fill(slots.begin(), slots.end(), -1);
+    int filled = 0;
+    bool is_grid = false;
+    if (grid) {
+      int64_t rs = (int64_t)cur;
+      for (int r = 0; r < GY && rs >= 0; ++r) {
+        int64_t x = rs;
+        int zi = 0;
+        for (; zi < GZ && x >= 0; ++zi) {
+          bool taken = sub_wg[x] >= 0 || sub[x].len != len;
+          for (int t = 0; t < filled + zi && !taken; ++t) taken = slots[t] == x;
+          if (taken) break;
+          slots[filled + zi] = x;
+          x = zi + 1 < GZ ? nbr[0][x] : x;
+        }
+        if (zi < GZ) {  // incomplete row: drop it
+          for (int t = filled; t < filled + zi; ++t) slots[t] = -1;
+          break;
+        }
+        filled += GZ;
+        rs = nbr[1][slots[filled - GZ]];
+      }
+      is_grid = filled >= 2 * GZ;
+      if (!is_grid) {
+        std::fill(slots.begin(), slots.end(), -1);
+        filled = 0;
+      }
+    }
+    // the rest: the next free sub-chains of this length, in order
+    for (size_t j = cur; j < nsub && filled < S && sub[j].len == len; ++j) {
+      if (sub_wg[j] >= 0) continue;
+      bool taken = false;
+      for (int t = 0; t < filled && !taken; ++t) taken = slots[t] == (int64_t)j;
+      if (!taken) slots[filled++] = (int64_t)j;
+    }
     if (pos > 0x7FFFFFFFll - len * S) return fail(SEM_E_INVALID, "hex plan: too many elements");
     P.wg_off.push_back((int)pos);
     P.wg_len.push_back((int)len);
+    grid_wg.push_back(is_grid ? 1 : 0);
     for (int64_t k = 0; k < len; ++k)
-      for (int s = 0; s < S; ++s) {
-        const size_t si = i + s;
-        P.elist.push_back(si < j ? (int)order[sub[si].start + k] : -1);
+      for (int s = 0; s < S; ++s)
+        P.elist.push_back(slots[s] >= 0 ? (int)order[sub[slots[s]].start + k] : -1);
+    for (int s = 0; s < S; ++s)
+      if (slots[s] >= 0) {
+        sub_wg[slots[s]] = w;
+        sub_slot[slots[s]] = s;
       }
-    for (size_t si = i; si < j; ++si) {
-      sub_wg[si] = w;
-      sub_slot[si] = (int64_t)(si - i);
-    }
     pos += len * S;
-    i = j;
   }
   const int64_t n_wg = (int64_t)P.wg_off.size(), n_pos = pos;
   P.cmask.assign(n_pos, 0ull);
   P.cflag.assign(n_wg * S, 0);
   // 5b. z-merge: slot s of a workgroup hands its xi2 = 0 face to slot s-1
   //     when, at every chain step, that face IS slot s-1's xi2 = n-1 face
-  //     node for node (same (a, b)); the kernel sums it in LDS
-  std::vector<uint8_t> zm(n_wg * S, 0);
+  //     node for node (same (a, b)); the kernel sums it in LDS.  In a grid
+  //     workgroup only within a row.  y-merge: slot s hands its xi1 = 0 face
+  //     to slot s - GZ likewise (same (a, c)).
+  std::vector<uint8_t> zm(n_wg * S, 0), ym(n_wg * S, 0);
+  auto elem_at = [&](int64_t w, int64_t k, int s) { return P.elist[P.wg_off[w] + k * S + s]; };
   if (zmerge)
     for (int64_t w = 0; w < n_wg; ++w)
       for (int s = 1; s < S; ++s) {
+        if (grid_wg[w] && s % GZ == 0) continue;
         bool ok = true;
         for (int64_t k = 0; k < P.wg_len[w] && ok; ++k) {
-          const int e1 = P.elist[P.wg_off[w] + k * S + s - 1], e2 = P.elist[P.wg_off[w] + k * S + s];
+          const int e1 = elem_at(w, k, s - 1), e2 = elem_at(w, k, s);
           if (e1 < 0 || e2 < 0) {
             ok = false;
             break;
@@ -276,8 +396,31 @@ int hex_build_plan(const std::vector<uint32_t>& h, int64_t E, int64_t n_node, in
         }
         zm[w * S + s] = ok ? 1 : 0;
       }
-  // a thread whose face is merged emits no write of its own
-  auto merged = [&](int64_t w, int64_t s, int c) { return c == 0 && zm[w * S + s]; };
+  if (grid)
+    for (int64_t w = 0; w < n_wg; ++w) {
+      if (!grid_wg[w]) continue;
+      for (int s = GZ; s < S; ++s) {
+        bool ok = true;
+        for (int64_t k = 0; k < P.wg_len[w] && ok; ++k) {
+          const int e1 = elem_at(w, k, s - GZ), e2 = elem_at(w, k, s);
+          if (e1 < 0 || e2 < 0) {
+            ok = false;
+            break;
+          }
+          const uint32_t* m1 = &h[(int64_t)e1 * N3];
+          const uint32_t* m2 = &h[(int64_t)e2 * N3];
+          for (int a = 0; a < N && ok; ++a)
+            for (int c = 0; c < N && ok; ++c) ok = m1[a * N2 + (N - 1) * N + c] == m2[a * N2 + c];
+        }
+        ym[w * S + s] = ok ? 1 : 0;
+      }
+    }
+  // a thread whose column is handed over emits no write of its own (the
+  // kernel's give / ygive, sem_hex.h)
+  auto merged = [&](int64_t w, int64_t s, int b, int c) {
+    if (c == 0 && zm[w * S + s]) return true;
+    return b == 0 && ym[w * S + s] && !(c == 0 && zm[w * S + s - GZ]);
+  };
   // 6. events per node
   std::vector<uint8_t> cnt(n_node, 0);
   auto bump = [&](uint32_t g) {
@@ -289,7 +432,7 @@ int hex_build_plan(const std::vector<uint32_t>& h, int64_t E, int64_t n_node, in
       const uint32_t* me = &h[order[sub[i].start + k] * N3];
       const int amax = (k == len - 1) ? N : N - 1;
       for (int64_t t = 0; t < (int64_t)amax * N2; ++t)
-        if (!merged(sub_wg[i], sub_slot[i], (int)(t % N))) bump(me[t]);
+        if (!merged(sub_wg[i], sub_slot[i], (int)((t / N) % N), (int)(t % N))) bump(me[t]);
     }
   }
   // 7. face flags, column masks
@@ -310,6 +453,7 @@ int hex_build_plan(const std::vector<uint32_t>& h, int64_t E, int64_t n_node, in
       if (cnt[tl[j]] > 1) f |= 2;
     }
     if (zm[sub_wg[i] * S + sub_slot[i]]) f |= 4;
+    if (ym[sub_wg[i] * S + sub_slot[i]]) f |= 8;
     P.cflag[sub_wg[i] * S + sub_slot[i]] = f;
     for (int64_t k = 0; k < len; ++k) {
       const int64_t p = P.wg_off[sub_wg[i]] + k * S + sub_slot[i];
@@ -318,7 +462,7 @@ int hex_build_plan(const std::vector<uint32_t>& h, int64_t E, int64_t n_node, in
       for (int b = 0; b < N; ++b)
         for (int c = 0; c < N; ++c) {
           const int bcol = bcol_of(b, c);
-          if (bcol < 0 || merged(sub_wg[i], sub_slot[i], c)) continue;
+          if (bcol < 0 || merged(sub_wg[i], sub_slot[i], b, c)) continue;
           for (int a = 0; a < N; ++a) {
             if (a == N - 1 && k < len - 1) continue;
             if (a == 0 && k == 0 && (f & 1)) continue;
@@ -350,7 +494,7 @@ int hex_build_plan(const std::vector<uint32_t>& h, int64_t E, int64_t n_node, in
         for (int b = 0; b < N; ++b)
           for (int c = 0; c < N; ++c) {
             const int bc = b * N + c, bcol = bcol_of(b, c);
-            if (merged(w, s, c)) continue;
+            if (merged(w, s, b, c)) continue;
             const bool colslot = bcol >= 0 && ((mask >> bcol) & 1ull);
             for (int a = 0; a < N; ++a) {
               if (a == N - 1 && k < len - 1) continue;
@@ -619,6 +763,14 @@ int ctx_init(sem_ctx* c) {
   c->hex->rows = re ? std::atoi(re) != 0 : hex_rows_default(c->n);
   const char* ze = std::getenv("SEM_HEX_ZMERGE");
   c->hex->zmerge = HEX_ZMERGE && !(ze && std::atoi(ze) == 0);
+  // y-merge by default at n <= 4 (p <= 3), where it measured faster (p = 1 /
+  // 2 / 3: 1.530 -> 1.429, 0.589 -> 0.544, 0.430 -> 0.415 ms per step at
+  // ~1e7 DOF); at p = 4 / 7 its extra barrier per step outweighs the seams
+  // it removes (0.324 -> 0.328, 0.266 -> 0.275; profiles/r06/hex_ymerge/).
+  // SEM_HEX_YMERGE=1 / 0 forces it on / off.
+  const char* ye = std::getenv("SEM_HEX_YMERGE");
+  const bool ywant = ye ? std::atoi(ye) != 0 : c->n <= 4;
+  c->hex->ymerge = ywant && c->hex->zmerge && !c->hex->rows && hex_grid_z(c->n) < hex_slots(c->n);
   return SEM_OK;
 }
 
@@ -652,7 +804,7 @@ int set_map(sem_ctx* c, const uint32_t* d_e2n, hipStream_t st) {
   if (rc) return rc;
   const int64_t resident = (int64_t)std::max(c->n_cu, 1) * std::max(wpc, 1);
   HexPlanHost P;
-  rc = hex_build_plan(h, c->n_elem, c->n_node, N, resident, H->zmerge, P);
+  rc = hex_build_plan(h, c->n_elem, c->n_node, N, resident, H->zmerge, H->ymerge, P);
   if (rc) return rc;
   c->epoch++;
   c->map_epoch++;
@@ -791,13 +943,14 @@ int plan_info(const sem_ctx* c, int64_t* info, int n_info) {
   // length cap, [7] launch positions, [8] sub-chains, [9] seam nodes,
   // [10] slotted writes, [11] plain stores, [12] threads per workgroup,
   // [13] ndim (3), [14] geometry ready, [15] action kernel (1 row form,
-  // 0 three-block), [16] z-merge in the plan
+  // 0 three-block), [16] z-merge in the plan, [17] y-merge: slots per grid
+  // row (0: off)
   const int64_t v[] = {H->n_wg,        H->n_zero, 0,
                        1,              H->slots,  H->n_chains,
                        H->chain_len,   H->n_pos,  H->n_subchains,
                        H->n_seam,      H->n_seam_writes, H->n_direct,
                        H->threads,     3,         H->have_G ? 1 : 0,
-                       H->rows ? 1 : 0, H->zmerge ? 1 : 0};
+                       H->rows ? 1 : 0, H->zmerge ? 1 : 0, H->ymerge ? hex_grid_z(H->N) : 0};
   const int nv = (int)(sizeof(v) / sizeof(v[0]));
   for (int i = 0; i < n_info; ++i) info[i] = i < nv ? v[i] : 0;
   return SEM_OK;

@@ -164,6 +164,43 @@ def test_hex_kernel_forms_vs_oracle(sem, gll, monkeypatch, p, form):
         assert rel_l2(op.diag().cpu().numpy(), dref) < TOL
 
 
+@pytest.mark.parametrize("p,gy,gz", [(1, 8, 8), (2, 4, 7), (3, 4, 4), (4, 2, 5), (7, 2, 2)])
+def test_hex_ymerge_vs_oracle(sem, gll, monkeypatch, p, gy, gz):
+    """The y-merge (the workgroup's slots as a gy x gz grid, xi1 faces between
+    its rows summed in LDS as well as the xi2 faces within a row): action,
+    accumulate and diagonal against the oracle with it on and off, on a
+    warped mesh sized so that full grids, a grid cut short at the mesh edge
+    and the 1-D fallback all occur; fewer seam nodes with it on."""
+    from spectralelementmethod_amd import meshgen
+    nodes, e2n = meshgen.structured_cube(3, 2 * gy + 1, gz + 1, p, warp=0.05)
+    P = _oracle(gll, nodes, e2n, p)
+    rng = np.random.default_rng(40 + p)
+    u = rng.standard_normal(P.ndof)
+    y0 = rng.standard_normal(P.ndof)
+    ref = P.apply(u)
+    L = P.element_matrices()
+    dref = np.bincount(P.e2n.reshape(P.e2n.shape[0], -1).ravel(),
+                       weights=np.einsum("eii->ei", L).ravel(), minlength=P.ndof)
+    seams = {}
+    monkeypatch.setenv("SEM_HEX_ROWS", "0")
+    monkeypatch.setenv("SEM_HEX_ZMERGE", "1")
+    for ym in ("1", "0"):
+        monkeypatch.setenv("SEM_HEX_YMERGE", ym)
+        op = sem.SEMOperator(p, e2n, nodes)
+        info = op.plan_info()
+        assert info["ymerge"] == (ym == "1")
+        if ym == "1":
+            assert tuple(info["slot_grid"]) == (gy, gz)
+        seams[ym] = info["seam_nodes"]
+        y = op.apply(torch.from_numpy(u).cuda()).cpu().numpy()
+        assert rel_l2(y, ref) < TOL, ym
+        yt = torch.from_numpy(y0.copy()).cuda()
+        op.apply(torch.from_numpy(u).cuda(), out=yt, accumulate=True)
+        assert rel_l2(yt.cpu().numpy(), y0 + ref) < TOL, ym
+        assert rel_l2(op.diag().cpu().numpy(), dref) < TOL, ym
+    assert seams["1"] < seams["0"], seams
+
+
 def _permute_local(e2n, rng, frac=0.5):
     """Re-orient a fraction of the elements (swap / reverse local axes): the
     mesh is the same, the xi0 chains break wherever orientations differ."""

@@ -43,7 +43,11 @@ def _free_port():
 
 
 def _hex_worker(rank, world, port, mode, p, nex, ney, nez, q):
+    import faulthandler
     import sys
+    # a rank stuck for 120 s prints where it is (stderr) and exits: the parent
+    # then sees a dead rank instead of waiting out the test timeout
+    faulthandler.dump_traceback_later(120, exit=True)
     for pth in (ROOT, os.path.join(ROOT, "oracle")):
         if pth not in sys.path:
             sys.path.insert(0, pth)
