@@ -17,6 +17,7 @@ differs) and the oracle's (HexPoissonProblem) to 1e-10; the diagonal to
 1e-12; the PCG over the decomposition the single-GPU solve to 1e-9."""
 import os
 import socket
+import time
 
 import numpy as np
 import pytest
@@ -47,14 +48,27 @@ def _hex_worker(rank, world, port, mode, p, nex, ney, nez, q):
     import sys
     # a rank stuck for 120 s prints where it is (stderr) and exits: the parent
     # then sees a dead rank instead of waiting out the test timeout
-    faulthandler.dump_traceback_later(120, exit=True)
+    faulthandler.dump_traceback_later(float(os.environ.get("SEM_TEST_RANK_DEADLINE", "120")),
+                                      exit=True)
+    # eight ranks on one device besides the pytest process: two hardware
+    # queues per rank (the caller's stream and the side stream) instead of
+    # HIP's four (set before this process's first HIP call)
+    if world > 4:
+        os.environ["GPU_MAX_HW_QUEUES"] = "2"
     for pth in (ROOT, os.path.join(ROOT, "oracle")):
         if pth not in sys.path:
             sys.path.insert(0, pth)
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # an explicit collective timeout: with gloo's default (30 min) the
+    # 8-rank solve stalled in an all-reduce in 7 of 9 runs that followed
+    # other GPU tests in the same session (all ranks inside all_reduce,
+    # > 180 s; 6.5 s when run alone); with 60 s it passed every time
+    # (DESIGN.md §8).  A stuck collective now raises instead of hanging.
+    import datetime
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=60))
     try:
         import sem_oracle
         from spectralelementmethod_amd import meshgen
@@ -97,6 +111,9 @@ def _hex_worker(rank, world, port, mode, p, nex, ney, nez, q):
         d = op.diag()
         d_ref = full.diag()[l2g]
         err_diag = ((d - d_ref).norm() / d_ref.norm()).item()
+        # before the solve: a wrong action shows here even if the solve stalls
+        print("rank %d: action %s vs single GPU, %.2e vs oracle, diagonal %.2e" % (
+            rank, ["%.2e" % e for e in errs], err_oracle, err_diag), file=sys.stderr, flush=True)
         # device-resident PCG over the decomposition vs the single-GPU solve
         X = torch.from_numpy(gnodes).to(dev)
         xs_g = torch.sin(0.5 * np.pi * X[0]) * torch.cos(0.5 * np.pi * X[1]) + X[0] * X[2]
@@ -106,7 +123,11 @@ def _hex_worker(rank, world, port, mode, p, nex, ney, nez, q):
         x_single, its1, _ = full.pcg_solve(b, x_single, on_g, rtol=1e-12)
         xs, on = xs_g[l2g], on_g[l2g]
         x = torch.where(on, xs, torch.zeros_like(xs))
-        x, its, rel = op.pcg_solve(b[l2g].contiguous(), x, on, rtol=1e-12, check_every=4)
+        t_pcg = time.time()
+        x, its, rel = op.pcg_solve(b[l2g].contiguous(), x, on, rtol=1e-12, max_iter=4 * its1 + 100,
+                                   check_every=4)
+        print("rank %d: decomposed PCG %d iterations in %.2fs" % (rank, its, time.time() - t_pcg),
+              file=sys.stderr, flush=True)
         err_pcg = ((x - x_single[l2g]).norm() / x_single[l2g].norm()).item()
         info = op.dd_info()
         q.put((rank, max(errs), err_oracle, err_diag, err_pcg, its, its1, op.transport,
