@@ -1101,7 +1101,8 @@ def main():
             "kernel_family": plan["kernel"], "map_entry_bytes": map_bytes,
             "gpu_setup_sec": t_setup, "gpu_setup_sec_per_elem": t_setup / max(1, n_elem_local),
             "scatter_plan": {k: plan[k] for k in ("plan", "colours", "chains_per_colour", "rounds",
-                                                  "zero_list", "atomic_groups", "seam_nodes")},
+                                                  "zero_list", "atomic_groups", "seam_nodes",
+                                                  "map_patterns") if k in plan},
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -203,7 +203,11 @@ int sem_set_map_shared(sem_ctx* ctx, const uint32_t* d_e2n, const uint8_t* d_nod
  * bit for bit (csrc/deo_const.h; 16-bit maps) at an order where that is
  * measured faster; SEM_CONST_D=0 / 1 in the environment
  * turns it off / on at every order.
- * Writes min(n_info, 26) values. */
+ * [26] patterns of the 16-bit map's pattern table (0: one block of entries
+ * per group): groups whose entries repeat share one copy and the map stream
+ * shrinks to the per-row bases (SEM_MAP_PATTERNS=0 in the environment turns
+ * it off; built only for the orders whose kernels carry it, p = 8).
+ * Writes min(n_info, 27) values. */
 int sem_plan_info(sem_ctx* ctx, int64_t* info, int n_info);
 
 /* How the Poisson action obtains its geometric factors.

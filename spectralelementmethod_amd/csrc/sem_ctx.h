@@ -83,6 +83,8 @@ struct sem_ctx {
   uint16_t* d_map16 = nullptr;  // the same map as 16-bit row offsets (column kernel)
   uint32_t* d_mbase = nullptr;  // their per-(slot, row) 32-bit bases
   bool map16 = false;
+  bool map_pat = false;   // d_map16 is a pattern table (MapRef::pat)
+  int64_t n_map_pat = 0;
   int* d_epos = nullptr;         // element -> packed position slot * epw + k
   const uint32_t* d_e2n = nullptr;
   uint32_t* d_zero = nullptr;    // y entries no kernel stores first (unreferenced / first-atomic)

@@ -4,6 +4,8 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <unordered_map>
 
 #include "sem_ctx.h"
 
@@ -796,6 +798,54 @@ static bool build_map16(const Plan& P, int64_t n_elem, int n, int epw, int64_t n
   return wide * 16 <= filled;
 }
 
+// Pattern table of a 16-bit map (MapRef::pat, csrc/sem_kernels.h): every
+// group's block of n x lw entries (offsets and codes) deduplicated; the
+// table replaces m16 and each group's pattern id goes into bits 28-31 of its
+// bases 1..4.  Declined when an order's kernels lack the branch, when more
+// than 1 / 8 of the groups are distinct, or past 2^16 patterns.  On the
+// structured block layout a handful of layouts (which rows are carried,
+// slotted or merged) cover every group.
+static bool build_map_patterns(std::vector<uint16_t>& m16, std::vector<uint32_t>& mb, int n,
+                               int lw, int64_t n_slots, int64_t* n_pat) {
+  *n_pat = 0;
+  if (n < 5 || n > 31 || !((SEM_MAP_PATTERN_N >> n) & 1u) || SEM_MAP_TOUCH) return false;
+  const size_t blk = (size_t)n * lw;
+  std::unordered_map<uint64_t, std::vector<uint32_t>> seen;
+  std::vector<uint16_t> table;
+  std::vector<uint32_t> pid((size_t)n_slots, 0);
+  for (int64_t sl = 0; sl < n_slots; ++sl) {
+    if (mb[(size_t)sl * n] == M16_WIDE) continue;  // reads the 32-bit map
+    const uint16_t* e = &m16[(size_t)sl * blk];
+    uint64_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < blk; ++i) h = (h ^ e[i]) * 1099511628211ull;
+    auto& cand = seen[h];
+    uint32_t id = 0xFFFFFFFFu;
+    for (uint32_t c : cand)
+      if (std::memcmp(&table[(size_t)c * blk], e, blk * sizeof(uint16_t)) == 0) {
+        id = c;
+        break;
+      }
+    if (id == 0xFFFFFFFFu) {
+      id = (uint32_t)(table.size() / blk);
+      if (id >= 65536u || (int64_t)id * 8 > n_slots) return false;
+      table.insert(table.end(), e, e + blk);
+      cand.push_back(id);
+    }
+    pid[(size_t)sl] = id;
+  }
+  for (int64_t sl = 0; sl < n_slots; ++sl) {
+    if (mb[(size_t)sl * n] == M16_WIDE) continue;
+    for (int q = 0; q < 4; ++q) {
+      uint32_t& b = mb[(size_t)sl * n + 1 + q];
+      if (b & ~GID_MASK) return false;  // a node id past 2^28 (cannot happen: packed maps)
+      b |= ((pid[(size_t)sl] >> (4 * q)) & 15u) << 28;
+    }
+  }
+  *n_pat = (int64_t)(table.size() / blk);
+  m16.swap(table);
+  return true;
+}
+
 // ---------------------------------------------------------------------------
 // Element-level plan for the MFMA kernel (one element per wavefront, no
 // chains): elements are greedily coloured so that elements of one colour
@@ -1362,11 +1412,16 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
   c->d_map16 = nullptr;
   c->d_mbase = nullptr;
   c->map16 = false;
+  c->map_pat = false;
+  c->n_map_pat = 0;
   const char* m16env = std::getenv("SEM_MAP16");
   if (!mfma && !(m16env && std::atoi(m16env) == 0)) {
     std::vector<uint16_t> m16;
     std::vector<uint32_t> mb;
     if (build_map16(P, c->n_elem, n, c->epw, c->n_groups, m16, mb)) {
+      const char* pe = std::getenv("SEM_MAP_PATTERNS");
+      c->map_pat = c->dpn == 1 && !(pe && std::atoi(pe) == 0) &&
+                   build_map_patterns(m16, mb, n, c->epw * n, P.n_slots, &c->n_map_pat);
       HIP_TRY(hipMalloc(&c->d_map16, m16.size() * sizeof(uint16_t)));
       HIP_TRY(hipMemcpy(c->d_map16, m16.data(), m16.size() * sizeof(uint16_t),
                         hipMemcpyHostToDevice));
@@ -1439,30 +1494,31 @@ int sem_plan_info(sem_ctx* c, int64_t* info, int n_info) {
   if (!c || !info || n_info < 1) return fail(SEM_E_INVALID, "bad arguments");
   if (c->ndim == 3) return semh::plan_info(c, info, n_info);
   const int64_t nc = c->colour_start.empty() ? 0 : (int64_t)c->colour_start.size() - 1;
-  constexpr int NV = 8 + MAX_COLOURS + 1 + 1 + 1 + 1 + 1 + 1 + 1 + 2 + 1;
+  constexpr int NV = 8 + MAX_COLOURS + 1 + 1 + 1 + 1 + 1 + 1 + 1 + 2 + 1 + 1;
   int64_t vals[NV] = {c->n_groups, c->n_zero, c->n_atomic_groups, c->conforming ? 1 : 0,
                       c->epw,      nc,        c->rounds,          c->n_slots};
   for (int64_t q = 0; q < nc && q <= MAX_COLOURS; ++q)
     vals[8 + q] = c->colour_start[q + 1] - c->colour_start[q];
-  vals[NV - 9] = c->mfma ? SEM_KERNEL_MFMA : SEM_KERNEL_COLUMN;
-  vals[NV - 8] = c->map16 ? 2 : 4;  // bytes per packed map entry
+  vals[NV - 10] = c->mfma ? SEM_KERNEL_MFMA : SEM_KERNEL_COLUMN;
+  vals[NV - 9] = c->map16 ? 2 : 4;  // bytes per packed map entry
   // the geometry the Poisson action actually uses: nodal only once x_phys
   // per node exists (sem_set_geom installs stored factors); before any
   // geometry, the mode sem_geom_from_nodes will resolve to
   const bool eff_nodal = c->xg_valid ? true : (c->d_GP[0] ? false : nodal_mode(c));
-  vals[NV - 7] = eff_nodal ? SEM_GEOM_NODAL : SEM_GEOM_STORED;
+  vals[NV - 8] = eff_nodal ? SEM_GEOM_NODAL : SEM_GEOM_STORED;
   // plan: 0 chains (colour launches), 1 element-coloured chains, 2 elements
   // (MFMA kernel), 4 chains + seam sums (3 was the retired one-launch plan),
   // 5 elements + seam sums (n = 17 MFMA kernel)
-  vals[NV - 6] = c->mfma ? (c->seam ? 5 : 2) : (c->ecol ? 1 : (c->seam ? 4 : 0));
+  vals[NV - 7] = c->mfma ? (c->seam ? 5 : 2) : (c->ecol ? 1 : (c->seam ? 4 : 0));
   // the same for the axisymmetric Stokes block (dofs_per_node = 2)
   const bool axi_nodal =
       c->xg_axi ? true : (c->d_GP[1] ? false : nodal_mode_op(c, SEM_OP_AXISYM_STOKES));
-  vals[NV - 5] = c->dpn == 2 ? (axi_nodal ? SEM_GEOM_NODAL : SEM_GEOM_STORED) : 0;
-  vals[NV - 4] = c->seam ? c->n_seam : 0;  // seam nodes
-  vals[NV - 3] = c->blocks ? 1 : 0;          // block layout
-  vals[NV - 2] = c->row_carries;             // entries carried between rounds
-  vals[NV - 1] = c->const_d && c->map16 && !c->mfma ? 1 : 0;  // Poisson: D as constants
+  vals[NV - 6] = c->dpn == 2 ? (axi_nodal ? SEM_GEOM_NODAL : SEM_GEOM_STORED) : 0;
+  vals[NV - 5] = c->seam ? c->n_seam : 0;  // seam nodes
+  vals[NV - 4] = c->blocks ? 1 : 0;          // block layout
+  vals[NV - 3] = c->row_carries;             // entries carried between rounds
+  vals[NV - 2] = c->const_d && c->map16 && !c->mfma ? 1 : 0;  // Poisson: D as constants
+  vals[NV - 1] = c->map_pat ? c->n_map_pat : 0;  // map pattern table: patterns (0: off)
   for (int i = 0; i < n_info && i < NV; ++i) info[i] = vals[i];
   return SEM_OK;
 }

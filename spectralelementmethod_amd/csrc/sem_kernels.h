@@ -709,6 +709,12 @@ __device__ __forceinline__ void row_pass(double* L, int j, const DT& D, bool act
 // mesh), read with scalar loads -- 2 B instead of 4 per element node.  A
 // group with a wider row (e.g. one that wraps into the next element column)
 // is flagged and reads the 32-bit map instead (uniform branch per wave).
+// Pattern table (the PAT kernels, sem_ctx::map_pat): groups whose 16-bit
+// entries (offsets and codes) are the same share one copy -- on a structured
+// numbering every row's offsets are the same run and the codes follow a few
+// layouts -- so p16 holds [pattern][r][lane] and the group's pattern id sits
+// in bits 28-31 of its bases 1..4 (node ids are < 2^28): the per-group map
+// stream shrinks to the N bases.
 struct MapRef {
   const uint32_t* __restrict__ p32;  // [slot][r][lane] gid | code << 28
   const uint16_t* __restrict__ p16;  // [slot][r][lane] (gid - base) | code << 12
@@ -718,7 +724,17 @@ constexpr uint32_t M16_OFF_MASK = 0xFFFu;
 constexpr uint32_t M16_WIDE = 0xFFFFFFFFu;  // base[slot][0]: this group uses the 32-bit map
 constexpr int M16_CODE_SHIFT = 12;
 
-template <int N, bool M16 = false, bool LD = false>
+// orders with pattern-table (PAT) kernels (SEM_MAP_PATTERN_N, a bit per n;
+// the host builds a table only for these)
+#ifndef SEM_MAP_PATTERN_N
+#define SEM_MAP_PATTERN_N (1u << 9)
+#endif
+template <int N>
+struct PatternMap {
+  static constexpr bool value = N >= 5 && ((SEM_MAP_PATTERN_N >> N) & 1u);
+};
+
+template <int N, bool M16 = false, bool LD = false, bool PAT = false>
 __device__ __forceinline__ void load_map(const MapRef& m, int64_t g, int lane, bool in_wave,
                                          uint32_t (&raw)[N]) {
   constexpr int LW = Tile<N>::LW;
@@ -729,16 +745,32 @@ __device__ __forceinline__ void load_map(const MapRef& m, int64_t g, int lane, b
     // serialised two memory latencies and measured 8 % slower
     // padding lanes load a valid entry (lane clamped) and discard it: no
     // load under a branch
-    const uint16_t* mp = m.p16 + g * (int64_t)(N * LW) + (in_wave ? lane : LW - 1);
     const uint32_t* bp = m.base + g * N;  // g is wave-uniform: scalar loads
     uint32_t o[N], b[N];
+    if constexpr (PAT) {  // the pattern's entries follow the bases
 #pragma unroll
-    for (int r = 0; r < N; ++r) {
-      const uint32_t t = mp[r * LW];
-      o[r] = in_wave ? t : (W_SKIP << M16_CODE_SHIFT);
+      for (int r = 0; r < N; ++r) b[r] = bp[r];
+      const int64_t pid = (b[1] >> 28) | ((b[2] >> 28) << 4) | ((b[3] >> 28) << 8) |
+                          ((b[4] >> 28) << 12);
+      const uint16_t* mp = m.p16 + pid * (int64_t)(N * LW) + (in_wave ? lane : LW - 1);
+#pragma unroll
+      for (int r = 0; r < N; ++r) {
+        const uint32_t t = mp[r * LW];
+        o[r] = in_wave ? t : (W_SKIP << M16_CODE_SHIFT);
+      }
+    } else {
+      const uint16_t* mp = m.p16 + g * (int64_t)(N * LW) + (in_wave ? lane : LW - 1);
+#pragma unroll
+      for (int r = 0; r < N; ++r) {
+        const uint32_t t = mp[r * LW];
+        o[r] = in_wave ? t : (W_SKIP << M16_CODE_SHIFT);
+      }
+#pragma unroll
+      for (int r = 0; r < N; ++r) b[r] = bp[r];
     }
+    if constexpr (PAT)  // bases 1..4 carry the pattern id above the node id
 #pragma unroll
-    for (int r = 0; r < N; ++r) b[r] = bp[r];
+      for (int r = 1; r < 5; ++r) b[r] &= GID_MASK;
 #pragma unroll
     for (int r = 0; r < N; ++r)
       raw[r] = (b[r] + (o[r] & M16_OFF_MASK)) | ((o[r] >> M16_CODE_SHIFT) << CODE_SHIFT);
@@ -797,7 +829,8 @@ struct MapTouch {
 // (p = 0..N-1) of the lane's column j in v[], and the raw coded map entries.
 //   mapP[g][r][k*N + j] = map[e][r][j] | code,  GP[g][c][r][k*N + j] = G_c(e; r, j)
 // ---------------------------------------------------------------------------
-template <int N, bool M16, class Pre = NoWait, bool LD = false, class DT = DEO<N>>
+template <int N, bool M16, class Pre = NoWait, bool LD = false, bool PAT = false,
+          class DT = DEO<N>>
 __device__ __forceinline__ void poisson_group_stored(const MapRef& mref,
                                                      const double* __restrict__ GP,
                                                      const double* __restrict__ u, int64_t g,
@@ -815,7 +848,7 @@ __device__ __forceinline__ void poisson_group_stored(const MapRef& mref,
   constexpr bool SP = N >= SEM_LDS_SPLIT_STORED_N;
   const double* gp = GP + g * (int64_t)(3 * N * LW) + lane;
   double uc[N];
-  load_map<N, M16, LD>(mref, g, lane, in_wave, raw);
+  load_map<N, M16, LD, PAT>(mref, g, lane, in_wave, raw);
 #pragma unroll
   for (int r = 0; r < N; ++r) {
     uc[r] = u[raw[r] & GID_MASK];
@@ -1029,7 +1062,8 @@ __device__ __forceinline__ void nodal_laplacian(const double (&uc)[N], int j, do
 }
 
 // One group of the Poisson action with NODAL geometry (no prefetch).
-template <int N, bool M16, class Pre = NoWait, bool LD = false, class DT = DEO<N>>
+template <int N, bool M16, class Pre = NoWait, bool LD = false, bool PAT = false,
+          class DT = DEO<N>>
 __device__ __forceinline__ void poisson_group_nodal(const MapRef& mref,
                                                     const double2* __restrict__ XG,
                                                     const double* __restrict__ u, int64_t g,
@@ -1041,7 +1075,7 @@ __device__ __forceinline__ void poisson_group_nodal(const MapRef& mref,
                                                     double (&prev)[N], const Pre& pre = Pre(), const double* wp = nullptr) {
   double uc[N];
   double2 xc[N];
-  load_map<N, M16, LD>(mref, g, lane, in_wave, raw);
+  load_map<N, M16, LD, PAT>(mref, g, lane, in_wave, raw);
   gather_x<N>(XG, raw, j, xc);
 #if SEM_NODAL_EARLY_U
   gather_u<N>(u, raw, uc);
@@ -1323,7 +1357,8 @@ __device__ __forceinline__ double block_sum_fixed(double v, double* sh) {
   return s;
 }
 
-template <int N, bool NODAL, bool M16, bool SEAM = false, bool DOT = false, bool CD = false>
+template <int N, bool NODAL, bool M16, bool SEAM = false, bool DOT = false, bool CD = false,
+          bool PAT = false>
 __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODAL, SEAM, DOT, CD>::value))
     k_poisson_apply(const MapRef mref, const double* __restrict__ GP,
                     const double2* __restrict__ XG, const double* __restrict__ u,
@@ -1369,10 +1404,10 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, (PoissonMinWaves<N, NODA
     constexpr bool PRE = RmwPrefetch<N>::value > 0 && Pre::prefetch;
     constexpr bool LD = RawLaunder<N, DOT>::value;
     if constexpr (NODAL)
-      poisson_group_nodal<N, M16, Pre, LD>(mref, XG, u, g, lane, j, in_wave, L, LB, D, w, wj, raw,
+      poisson_group_nodal<N, M16, Pre, LD, PAT>(mref, XG, u, g, lane, j, in_wave, L, LB, D, w, wj, raw,
                                            v[0], y, accumulate, prev, pre, sp.w);
     else
-      poisson_group_stored<N, M16, Pre, LD>(mref, GP, u, g, lane, j, in_wave, L, D, raw, v[0], y,
+      poisson_group_stored<N, M16, Pre, LD, PAT>(mref, GP, u, g, lane, j, in_wave, L, D, raw, v[0], y,
                                             accumulate, prev, pre);
     SeamOut so;
     if constexpr (SEAM) so.base = sp.buf + sp.colour[chain] * sp.n_node;

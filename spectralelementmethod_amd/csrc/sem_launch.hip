@@ -26,6 +26,29 @@ void launch_chains(sem_ctx* c, int op_kind, bool nodal, const double* u, double*
   sp.dot = dot_part;
   sp.round_sync = c->round_sync ? 1 : 0;
   sp.w = c->d_w;
+  // 16-bit map as a pattern table (sem_ctx::map_pat): the PAT kernels, D as
+  // an argument (the host builds a table only at the orders PatternMap lists)
+  if constexpr (PatternMap<N>::value) {
+    if (c->map_pat && op_kind == SEM_OP_POISSON) {
+      const double* GP = nodal ? nullptr : c->d_GP[0];
+      const double2* XG = nodal ? c->d_XG : nullptr;
+      if (SEAM && dot_part) {
+        if (nodal)
+          hipLaunchKernelGGL((k_poisson_apply<N, true, true, SEAM, SEAM, false, true>), g, b, 0, st,
+                             mr, GP, XG, u, y, c0, c1, R, acc, D, w, sp);
+        else
+          hipLaunchKernelGGL((k_poisson_apply<N, false, true, SEAM, SEAM, false, true>), g, b, 0,
+                             st, mr, GP, XG, u, y, c0, c1, R, acc, D, w, sp);
+      } else if (nodal) {
+        hipLaunchKernelGGL((k_poisson_apply<N, true, true, SEAM, false, false, true>), g, b, 0, st,
+                           mr, GP, XG, u, y, c0, c1, R, acc, D, w, sp);
+      } else {
+        hipLaunchKernelGGL((k_poisson_apply<N, false, true, SEAM, false, false, true>), g, b, 0, st,
+                           mr, GP, XG, u, y, c0, c1, R, acc, D, w, sp);
+      }
+      return;
+    }
+  }
   // the standard GLL D as compile-time constants (16-bit maps: the
   // structured meshes; sem_ctx::const_d)
   if (c->const_d && c->map16 && op_kind == SEM_OP_POISSON) {

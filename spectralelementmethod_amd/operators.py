@@ -255,8 +255,8 @@ class SEMOperator(object):
 
     def plan_info(self):
         """Setup plan of the scatter (see include/sem_hip.h sem_plan_info)."""
-        info = (C.c_int64 * 26)()
-        _lib.check(self._lib.sem_plan_info(self._ctx, info, 26))
+        info = (C.c_int64 * 27)()
+        _lib.check(self._lib.sem_plan_info(self._ctx, info, 27))
         v = list(info)
         if self.ndim == 3:
             return dict(ndim=3, workgroups=v[0], zero_list=v[1], conforming=bool(v[3]),
@@ -281,7 +281,7 @@ class SEMOperator(object):
                     geometry_axisym=(None if self.dpn != 2 else
                                      "nodal" if v[21] == _lib.GEOM_NODAL else "stored"),
                     seam_nodes=v[22] if v[20] in (4, 5) else 0, blocks=bool(v[23]),
-                    row_carries=v[24], const_d=bool(v[25]))
+                    row_carries=v[24], const_d=bool(v[25]), map_patterns=v[26])
 
     # ------------------------------------------------------------------
     def compute_geometry(self, kind=POISSON, stream=None):
