@@ -75,15 +75,19 @@ def alg_bytes_s8d(kind, n_nodes, n_elem, p):
     return 32 * n_nodes + 60 * n_elem * n2
 
 
-def streamed_bytes(kind, n_nodes, n_elem, p, geometry, map_bytes):
+def streamed_bytes(kind, n_nodes, n_elem, p, geometry, map_bytes, map_patterns=0):
     """The least the kernel as built must stream: with NODAL geometry the
     factors are replaced by x_phys per global node (16 B) gathered like u;
-    map_bytes = 2: 16-bit packed map plus one uint32 base per group row."""
+    map_bytes = 2: 16-bit packed map plus one uint32 base per group row;
+    map_patterns > 0: the bases and the pattern table only."""
     n = p + 1
     n2 = n * n
     m = map_bytes * n_elem * n2
     if map_bytes == 2:
-        m += 4 * n * n_elem // (64 // n)
+        epw = 64 // n
+        m += 4 * n * n_elem // epw
+        if map_patterns:
+            m = 4 * n * n_elem // epw + 2 * map_patterns * n * epw * n
     if kind != "poisson":
         if geometry == "nodal":  # (psi, omega) read + written, x_phys read
             return 48 * n_nodes + m
@@ -1037,7 +1041,8 @@ def main():
     map_bytes = plan.get("map_entry_bytes", 4) if (
         plan["kernel"] == "column" and (kind == POISSON or geometry == "nodal")) else 4
     B = alg_bytes_s8d(kname, n_nodes_local, n_elem_local, p)
-    B_stream = streamed_bytes(kname, n_nodes_local, n_elem_local, p, geometry, map_bytes)
+    B_stream = streamed_bytes(kname, n_nodes_local, n_elem_local, p, geometry, map_bytes,
+                              plan.get("map_patterns", 0) if map_bytes == 2 else 0)
     F = alg_flops(kname, n_elem_local, p, geometry)
     achieved = B / kern_avg_s / 1e9
     traffic, traffic_src = None, args.traffic_json
