@@ -137,7 +137,10 @@ void sem_ctx_destroy(sem_ctx* ctx);
  *     writes, [11] plain stores, [12] threads per workgroup, [13] 3, [14]
  *     geometry ready, [15] action kernel (1 row form, 0 three-block),
  *     [16] xi2 faces merged in LDS (z-merge), [17] xi1 faces merged in LDS
- *     too (y-merge): slots per row of the workgroup's slot grid, 0 = off. */
+ *     too (y-merge): slots per row of the workgroup's slot grid, 0 = off,
+ *     [18] template map: every element's node ids are its first node's id +
+ *     one shared offset block, read as one base per element
+ *     (SEM_HEX_TMAP=0 turns it off). */
 int sem_ctx_create_nd(sem_ctx** out, int ndim, int p, int64_t n_elem, int64_t n_node, int dpn,
                       int device);
 

@@ -58,6 +58,12 @@ struct HexLaunch {
                                     // face of slot s-1's (z-merge: summed in LDS)
   double* slot;                     // column slots [pos][n][NBC], then face slots [n_wg*S][2][n^2]
   int64_t face_base;
+  // template map (the TM kernels): every element's node ids are its first
+  // node's id + one shared offset block -- a structured numbering -- so a
+  // thread keeps its column's n offsets in registers and reads one base per
+  // element instead of n map entries
+  const uint32_t* ebase = nullptr;  // [E] node id of local node (0, 0, 0)
+  const int* tmpl = nullptr;        // [n^3] offsets
 };
 
 enum { HEX_SET = 0, HEX_ACC = 1, HEX_DIAG = 2 };
@@ -139,7 +145,7 @@ __device__ __forceinline__ int hex_bcol(int b, int c) {
 // maps) exceed what four waves per SIMD allow, and one element slot per
 // workgroup leaves LDS the limit anyway
 constexpr int hex_min_waves(int n) { return n <= 11 ? SEM_HEX_MIN_WAVES : n <= 13 ? 2 : 1; }
-template <int N, int MODE>
+template <int N, int MODE, bool TM = false>
 __global__ void __launch_bounds__(hex_threads(N), hex_min_waves(N))
     k_hex_poisson(const double* __restrict__ u, double* __restrict__ y,
                   const uint32_t* __restrict__ map, const double* __restrict__ G,
@@ -198,9 +204,19 @@ __global__ void __launch_bounds__(hex_threads(N), hex_min_waves(N))
   // the element map of the next chain step is loaded one step ahead
   uint32_t mn[N];
   int en = active ? P.elist[base + s] : 0;
-  if (active) {
+  [[maybe_unused]] int toff[TM ? N : 1];
+  if constexpr (TM)
 #pragma unroll
-    for (int a = 0; a < N; ++a) mn[a] = map[(int64_t)en * N3 + a * N2 + bc];
+    for (int a = 0; a < N; ++a) toff[a] = P.tmpl[a * N2 + bc];
+  if (active) {
+    if constexpr (TM) {
+      const uint32_t eb = P.ebase[en];
+#pragma unroll
+      for (int a = 0; a < N; ++a) mn[a] = eb + (uint32_t)toff[a];
+    } else {
+#pragma unroll
+      for (int a = 0; a < N; ++a) mn[a] = map[(int64_t)en * N3 + a * N2 + bc];
+    }
   }
 #pragma unroll 1
   for (int k = 0; k < L; ++k) {
@@ -236,8 +252,14 @@ __global__ void __launch_bounds__(hex_threads(N), hex_min_waves(N))
     __syncthreads();
     if (active && k + 1 < L) {
       en = P.elist[pos + S];
+      if constexpr (TM) {
+        const uint32_t eb = P.ebase[en];
 #pragma unroll
-      for (int a = 0; a < N; ++a) mn[a] = map[(int64_t)en * N3 + a * N2 + bc];
+        for (int a = 0; a < N; ++a) mn[a] = eb + (uint32_t)toff[a];
+      } else {
+#pragma unroll
+        for (int a = 0; a < N; ++a) mn[a] = map[(int64_t)en * N3 + a * N2 + bc];
+      }
     }
     // The contractions run with the summation index outermost and NOT
     // unrolled, the node row a unrolled inside: every register array is

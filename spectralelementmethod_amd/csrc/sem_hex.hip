@@ -3,6 +3,7 @@
 // the C ABI entry points (sem_device.hip forwards a context created with
 // ndim = 3 here).  DESIGN.md §4.9 / §5.3.
 #include <cmath>
+#include <cstdint>
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
@@ -46,14 +47,23 @@ struct HexState {
   // xi1 faces between the rows of a workgroup's slot grid too (three-block
   // kernel only; SEM_HEX_YMERGE=0 turns it off)
   bool ymerge = false;
+  // template map (HexLaunch::ebase / tmpl; three-block kernel): every
+  // element's ids = its first node's id + one offset block (SEM_HEX_TMAP=0
+  // turns it off)
+  bool tmap = false;
+  uint32_t* d_ebase = nullptr;
+  int* d_tmpl = nullptr;
   // diagnostics (sem_plan_info)
   int64_t n_chains = 0, n_subchains = 0, chain_len = 0, n_direct = 0;
 
   void free_plan() {
     for (void* p : {(void*)d_wg_off, (void*)d_wg_len, (void*)d_elist, (void*)d_cmask,
                     (void*)d_cflag, (void*)d_slot, (void*)d_seam_gid, (void*)d_seam_ptr,
-                    (void*)d_seam_idx, (void*)d_zero})
+                    (void*)d_seam_idx, (void*)d_zero, (void*)d_ebase, (void*)d_tmpl})
       (void)hipFree(p);
+    d_ebase = nullptr;
+    d_tmpl = nullptr;
+    tmap = false;
     d_wg_off = d_wg_len = d_elist = nullptr;
     d_cmask = nullptr;
     d_cflag = nullptr;
@@ -554,7 +564,7 @@ template <int N>
 int launch_hex_apply(sem_ctx* c, int mode, const double* u, double* y, hipStream_t st) {
   HexState* H = c->hex;
   const semh::HexLaunch L{H->d_wg_off, H->d_wg_len, H->d_elist,   H->d_cmask,
-                          H->d_cflag,  H->d_slot,   H->face_base};
+                          H->d_cflag,  H->d_slot,   H->face_base, H->d_ebase, H->d_tmpl};
   const dim3 g((unsigned)H->n_wg), b(semh::hex_threads(N));
   semh::HexD<N> Dk;
   for (int i = 0; i < N * N; ++i) Dk.d[i] = c->hD[i];
@@ -564,6 +574,15 @@ int launch_hex_apply(sem_ctx* c, int mode, const double* u, double* y, hipStream
   else if (H->rows && mode == semh::HEX_ACC)
     hipLaunchKernelGGL((semh::k_hex_rows<N, semh::HEX_ACC>), g, b, 0, st, u, y, H->d_map, H->d_G,
                        c->d_D, L, Dk);
+  else if (H->tmap && mode == semh::HEX_SET)
+    hipLaunchKernelGGL((semh::k_hex_poisson<N, semh::HEX_SET, true>), g, b, 0, st, u, y,
+                       H->d_map, H->d_G, c->d_D, L, Dk);
+  else if (H->tmap && mode == semh::HEX_ACC)
+    hipLaunchKernelGGL((semh::k_hex_poisson<N, semh::HEX_ACC, true>), g, b, 0, st, u, y,
+                       H->d_map, H->d_G, c->d_D, L, Dk);
+  else if (H->tmap)
+    hipLaunchKernelGGL((semh::k_hex_poisson<N, semh::HEX_DIAG, true>), g, b, 0, st, u, y,
+                       H->d_map, H->d_G, c->d_D, L, Dk);
   else if (mode == semh::HEX_SET)
     hipLaunchKernelGGL((semh::k_hex_poisson<N, semh::HEX_SET>), g, b, 0, st, u, y, H->d_map,
                        H->d_G, c->d_D, L, Dk);
@@ -819,6 +838,31 @@ int set_map(sem_ctx* c, const uint32_t* d_e2n, hipStream_t st) {
       (rc = upload(&H->d_seam_ptr, P.seam_ptr)) || (rc = upload(&H->d_seam_idx, P.seam_idx)) ||
       (rc = upload(&H->d_zero, P.zero)))
     return rc;
+  // template map: one offset block shared by every element (structured
+  // numberings), three-block kernel only
+  {
+    const char* te = std::getenv("SEM_HEX_TMAP");
+    bool ok = !H->rows && c->n_elem > 0 && !(te && std::atoi(te) == 0);
+    std::vector<int> tmpl((size_t)N3);
+    std::vector<uint32_t> eb;
+    if (ok) {
+      for (int64_t i = 0; i < N3 && ok; ++i) {
+        const int64_t d = (int64_t)h[i] - (int64_t)h[0];
+        ok = d >= INT32_MIN && d <= INT32_MAX;
+        tmpl[(size_t)i] = (int)d;
+      }
+      eb.resize((size_t)c->n_elem);
+      for (int64_t e = 0; e < c->n_elem && ok; ++e) {
+        const uint32_t* me = &h[(size_t)e * N3];
+        eb[(size_t)e] = me[0];
+        for (int64_t i = 1; i < N3 && ok; ++i) ok = me[i] == me[0] + (uint32_t)tmpl[(size_t)i];
+      }
+    }
+    if (ok) {
+      if ((rc = upload(&H->d_ebase, eb)) || (rc = upload(&H->d_tmpl, tmpl))) return rc;
+      H->tmap = true;
+    }
+  }
   H->n_wg = (int64_t)P.wg_off.size();
   H->n_pos = (int64_t)P.elist.size();
   H->face_base = P.face_base;
@@ -944,13 +988,14 @@ int plan_info(const sem_ctx* c, int64_t* info, int n_info) {
   // [10] slotted writes, [11] plain stores, [12] threads per workgroup,
   // [13] ndim (3), [14] geometry ready, [15] action kernel (1 row form,
   // 0 three-block), [16] z-merge in the plan, [17] y-merge: slots per grid
-  // row (0: off)
+  // row (0: off), [18] template map
   const int64_t v[] = {H->n_wg,        H->n_zero, 0,
                        1,              H->slots,  H->n_chains,
                        H->chain_len,   H->n_pos,  H->n_subchains,
                        H->n_seam,      H->n_seam_writes, H->n_direct,
                        H->threads,     3,         H->have_G ? 1 : 0,
-                       H->rows ? 1 : 0, H->zmerge ? 1 : 0, H->ymerge ? hex_grid_z(H->N) : 0};
+                       H->rows ? 1 : 0, H->zmerge ? 1 : 0, H->ymerge ? hex_grid_z(H->N) : 0,
+                       H->tmap ? 1 : 0};
   const int nv = (int)(sizeof(v) / sizeof(v[0]));
   for (int i = 0; i < n_info; ++i) info[i] = i < nv ? v[i] : 0;
   return SEM_OK;

@@ -265,7 +265,7 @@ class SEMOperator(object):
                         plain_stores=v[11], threads=v[12], geometry="stored",
                         kernel="column", plan="chains-seams",
                         hex_kernel="rows" if v[15] else "three_block", zmerge=bool(v[16]),
-                        ymerge=bool(v[17]),
+                        ymerge=bool(v[17]), template_map=bool(v[18]),
                         slot_grid=(v[4] // v[17], v[17]) if v[17] else (1, v[4]))
         counts = [x for x in v[8:8 + v[5]]]
         while counts and counts[-1] == 0:

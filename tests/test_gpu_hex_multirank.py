@@ -50,11 +50,14 @@ def _hex_worker(rank, world, port, mode, p, nex, ney, nez, q):
     # then sees a dead rank instead of waiting out the test timeout
     faulthandler.dump_traceback_later(float(os.environ.get("SEM_TEST_RANK_DEADLINE", "120")),
                                       exit=True)
-    # eight ranks on one device besides the pytest process: two hardware
-    # queues per rank (the caller's stream and the side stream) instead of
-    # HIP's four (set before this process's first HIP call)
+    # eight ranks on one device besides the pytest process (which holds its
+    # own queues once earlier tests have used the GPU): one hardware queue
+    # per rank instead of HIP's four, so that every rank's queue stays
+    # resident; oversubscribed, the device time-slices the queues and the
+    # solve's per-iteration host syncs each wait for their slice (DESIGN.md
+    # §8).  Set before this process's first HIP call.
     if world > 4:
-        os.environ["GPU_MAX_HW_QUEUES"] = "2"
+        os.environ["GPU_MAX_HW_QUEUES"] = "1"
     for pth in (ROOT, os.path.join(ROOT, "oracle")):
         if pth not in sys.path:
             sys.path.insert(0, pth)
