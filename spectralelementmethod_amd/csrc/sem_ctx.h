@@ -292,7 +292,7 @@ struct PoissonLaunch {
 };
 template <int N>
 void launch_poisson_const_d(const PoissonLaunch& L, bool nodal, bool seam, bool dot,
-                            const WVec<N>& w);
+                            const WVec<N>& w, bool pat = false);
 // the seam sums of the seam plan (sem_device.hip); du / dot: also the u.y
 // partials of the seam nodes, one per block of seam_sum_blocks(c)
 int launch_seam_sum(sem_ctx* c, double* y, int acc, hipStream_t st, const double* du = nullptr,

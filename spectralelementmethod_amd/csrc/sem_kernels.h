@@ -725,9 +725,11 @@ constexpr uint32_t M16_WIDE = 0xFFFFFFFFu;  // base[slot][0]: this group uses th
 constexpr int M16_CODE_SHIFT = 12;
 
 // orders with pattern-table (PAT) kernels (SEM_MAP_PATTERN_N, a bit per n;
-// the host builds a table only for these)
+// the host builds a table only for these): every order from n = 5, where
+// the pattern id fits the bases 1..4 -- measured faster at p = 4 / 6 / 8 /
+// 10 / 12 / 14 / 16
 #ifndef SEM_MAP_PATTERN_N
-#define SEM_MAP_PATTERN_N (1u << 9)
+#define SEM_MAP_PATTERN_N 0x3FFE0u
 #endif
 template <int N>
 struct PatternMap {

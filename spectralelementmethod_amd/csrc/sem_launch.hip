@@ -29,7 +29,7 @@ void launch_chains(sem_ctx* c, int op_kind, bool nodal, const double* u, double*
   // 16-bit map as a pattern table (sem_ctx::map_pat): the PAT kernels, D as
   // an argument (the host builds a table only at the orders PatternMap lists)
   if constexpr (PatternMap<N>::value) {
-    if (c->map_pat && op_kind == SEM_OP_POISSON) {
+    if (c->map_pat && op_kind == SEM_OP_POISSON && !c->const_d) {
       const double* GP = nodal ? nullptr : c->d_GP[0];
       const double2* XG = nodal ? c->d_XG : nullptr;
       if (SEAM && dot_part) {
@@ -54,7 +54,7 @@ void launch_chains(sem_ctx* c, int op_kind, bool nodal, const double* u, double*
   if (c->const_d && c->map16 && op_kind == SEM_OP_POISSON) {
     const PoissonLaunch L{g,  b,  st, mr, nodal ? nullptr : c->d_GP[0], nodal ? c->d_XG : nullptr,
                           u,  y,  c0, c1, R, acc, sp};
-    launch_poisson_const_d<N>(L, nodal, SEAM, SEAM && dot_part, w);
+    launch_poisson_const_d<N>(L, nodal, SEAM, SEAM && dot_part, w, c->map_pat);
     return;
   }
   if constexpr (SEAM) {

@@ -16,8 +16,34 @@ namespace semd {
 
 template <int N>
 void launch_poisson_const_d(const PoissonLaunch& L, bool nodal, bool seam, bool dot,
-                            const WVec<N>& w) {
+                            const WVec<N>& w, bool pat) {
   const DEO<N> D{};  // unused by the constant-D instantiations
+  // the 16-bit map as a pattern table (MapRef, csrc/sem_kernels.h)
+  if constexpr (PatternMap<N>::value) {
+    if (pat) {
+#define SEM_CD_LAUNCH_PAT(NODAL, SEAM, DOT)                                                  \
+  hipLaunchKernelGGL((k_poisson_apply<N, NODAL, true, SEAM, DOT, true, true>), L.g, L.b, 0, L.st, \
+                     L.mr, L.GP, L.XG, L.u, L.y, L.c0, L.c1, L.rounds, L.acc, D, w, L.sp)
+      if (seam && dot) {
+        if (nodal)
+          SEM_CD_LAUNCH_PAT(true, true, true);
+        else
+          SEM_CD_LAUNCH_PAT(false, true, true);
+      } else if (seam) {
+        if (nodal)
+          SEM_CD_LAUNCH_PAT(true, true, false);
+        else
+          SEM_CD_LAUNCH_PAT(false, true, false);
+      } else {
+        if (nodal)
+          SEM_CD_LAUNCH_PAT(true, false, false);
+        else
+          SEM_CD_LAUNCH_PAT(false, false, false);
+      }
+#undef SEM_CD_LAUNCH_PAT
+      return;
+    }
+  }
 #define SEM_CD_LAUNCH(NODAL, SEAM, DOT)                                                       \
   hipLaunchKernelGGL((k_poisson_apply<N, NODAL, true, SEAM, DOT, true>), L.g, L.b, 0, L.st, L.mr, \
                      L.GP, L.XG, L.u, L.y, L.c0, L.c1, L.rounds, L.acc, D, w, L.sp)
@@ -41,7 +67,8 @@ void launch_poisson_const_d(const PoissonLaunch& L, bool nodal, bool seam, bool 
 }
 
 #define SEM_INSTANTIATE_CD(N)                                                               \
-  template void launch_poisson_const_d<N>(const PoissonLaunch&, bool, bool, bool, const WVec<N>&);
+  template void launch_poisson_const_d<N>(const PoissonLaunch&, bool, bool, bool, const WVec<N>&, \
+                                          bool);
 
 #if SEM_N_LO <= 2 && 2 <= SEM_N_HI
 SEM_INSTANTIATE_CD(2)
