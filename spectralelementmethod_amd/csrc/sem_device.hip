@@ -833,13 +833,16 @@ static bool build_map_patterns(std::vector<uint16_t>& m16, std::vector<uint32_t>
     }
     pid[(size_t)sl] = id;
   }
+  // bases 1..4 must have their top 4 bits free (node ids < 2^28: packed maps)
   for (int64_t sl = 0; sl < n_slots; ++sl) {
     if (mb[(size_t)sl * n] == M16_WIDE) continue;
-    for (int q = 0; q < 4; ++q) {
-      uint32_t& b = mb[(size_t)sl * n + 1 + q];
-      if (b & ~GID_MASK) return false;  // a node id past 2^28 (cannot happen: packed maps)
-      b |= ((pid[(size_t)sl] >> (4 * q)) & 15u) << 28;
-    }
+    for (int q = 1; q <= 4; ++q)
+      if (mb[(size_t)sl * n + q] & ~GID_MASK) return false;
+  }
+  for (int64_t sl = 0; sl < n_slots; ++sl) {
+    if (mb[(size_t)sl * n] == M16_WIDE) continue;
+    for (int q = 0; q < 4; ++q)
+      mb[(size_t)sl * n + 1 + q] |= ((pid[(size_t)sl] >> (4 * q)) & 15u) << 28;
   }
   *n_pat = (int64_t)(table.size() / blk);
   m16.swap(table);
