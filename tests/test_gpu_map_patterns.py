@@ -1,0 +1,55 @@
+"""The 16-bit map's pattern table (csrc/sem_device.hip build_map_patterns,
+the PAT kernels of csrc/sem_kernels.h): on a structured
+numbering the groups share a few entry patterns and the PAT kernels must
+give the per-group map's result bit for bit -- the entries they assemble
+are the same -- with D as an argument (p = 8) and as constants (p = 6, 16),
+nodal and stored geometry, overwrite and accumulate; a numbering whose
+groups are all distinct keeps the per-group map."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ops():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from spectralelementmethod_amd import operators
+    return operators
+
+
+@pytest.mark.parametrize("p,ne,geometry", [(8, 128, "nodal"), (8, 128, "stored"), (6, 128, "auto"),
+                                           (4, 200, "nodal"), (16, 40, "auto")])
+def test_map_patterns_bitwise(ops, monkeypatch, p, ne, geometry):
+    from spectralelementmethod_amd import meshgen
+    nodes, e2n = meshgen.structured_square(ne, ne + 3, p, warp=0.05)
+    u = torch.from_numpy(np.random.default_rng(p).standard_normal(nodes.shape[1])).cuda()
+    y0 = torch.from_numpy(np.random.default_rng(p + 1).standard_normal(nodes.shape[1])).cuda()
+    out = {}
+    for pat in ("1", "0"):
+        monkeypatch.setenv("SEM_MAP_PATTERNS", pat)
+        op = ops.SEMOperator(p, e2n, nodes, geometry=geometry)
+        info = op.plan_info()
+        if pat == "1":
+            assert 0 < info["map_patterns"] <= info["groups"] // 8, info
+        else:
+            assert info["map_patterns"] == 0
+        y = op.apply(u)
+        ya = y0.clone()
+        op.apply(u, out=ya, accumulate=True)
+        yd, d = op.apply_dot(u)  # the fused-dot (PCG) kernels
+        out[pat] = (y.cpu().numpy(), ya.cpu().numpy(), yd.cpu().numpy(), d.item())
+    for a, b in zip(out["1"], out["0"]):
+        assert np.array_equal(a, b)
+
+
+def test_map_patterns_declined_on_shuffled_elements(ops):
+    """Randomly ordered elements: the groups' entry blocks are all different
+    and the plan keeps the per-group 16-bit map (or the 32-bit one)."""
+    from spectralelementmethod_amd import meshgen
+    nodes, e2n = meshgen.structured_square(24, 24, 8, warp=0.05)
+    e2n = e2n[np.random.default_rng(3).permutation(e2n.shape[0])]
+    op = ops.SEMOperator(8, e2n, nodes)
+    assert op.plan_info()["map_patterns"] == 0
