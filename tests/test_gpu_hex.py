@@ -201,6 +201,31 @@ def test_hex_ymerge_vs_oracle(sem, gll, monkeypatch, p, gy, gz):
     assert seams["1"] < seams["0"], seams
 
 
+@pytest.mark.parametrize("p", [2, 5, 8])
+def test_hex_template_map_bitwise(sem, monkeypatch, p):
+    """The template map (one base per element, the column's offsets in
+    registers) gives the per-element map's action and diagonal bit for bit
+    on a structured cube; shuffled node ids keep the map."""
+    from spectralelementmethod_amd import meshgen
+    nodes, e2n = meshgen.structured_cube(5, 4, 3, p, warp=0.05)
+    u = torch.from_numpy(np.random.default_rng(p).standard_normal(nodes.shape[1])).cuda()
+    out = {}
+    monkeypatch.setenv("SEM_HEX_ROWS", "0")
+    for tm in ("1", "0"):
+        monkeypatch.setenv("SEM_HEX_TMAP", tm)
+        op = sem.SEMOperator(p, e2n, nodes)
+        assert op.plan_info()["template_map"] == (tm == "1")
+        out[tm] = (op.apply(u).cpu().numpy(), op.diag().cpu().numpy())
+    assert np.array_equal(out["1"][0], out["0"][0])
+    assert np.array_equal(out["1"][1], out["0"][1])
+    monkeypatch.delenv("SEM_HEX_TMAP")
+    perm = np.random.default_rng(1).permutation(nodes.shape[1])
+    inv = np.empty_like(perm)
+    inv[perm] = np.arange(perm.size)
+    op = sem.SEMOperator(p, inv[e2n.astype(np.int64)].astype(np.uint32), nodes[:, perm])
+    assert not op.plan_info()["template_map"]
+
+
 def _permute_local(e2n, rng, frac=0.5):
     """Re-orient a fraction of the elements (swap / reverse local axes): the
     mesh is the same, the xi0 chains break wherever orientations differ."""
