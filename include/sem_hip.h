@@ -209,7 +209,7 @@ int sem_set_map_shared(sem_ctx* ctx, const uint32_t* d_e2n, const uint8_t* d_nod
  * [26] patterns of the 16-bit map's pattern table (0: one block of entries
  * per group): groups whose entries repeat share one copy and the map stream
  * shrinks to the per-row bases (SEM_MAP_PATTERNS=0 in the environment turns
- * it off; built for p >= 4).
+ * it off; built for p >= 2).
  * Writes min(n_info, 27) values. */
 int sem_plan_info(sem_ctx* ctx, int64_t* info, int n_info);
 

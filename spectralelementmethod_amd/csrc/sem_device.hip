@@ -798,17 +798,20 @@ static bool build_map16(const Plan& P, int64_t n_elem, int n, int epw, int64_t n
   return wide * 16 <= filled;
 }
 
-// Pattern table of a 16-bit map (MapRef::pat, csrc/sem_kernels.h): every
+// Pattern table of a 16-bit map (the PAT kernels, csrc/sem_kernels.h): every
 // group's block of n x lw entries (offsets and codes) deduplicated; the
 // table replaces m16 and each group's pattern id goes into bits 28-31 of its
-// bases 1..4.  Declined when an order's kernels lack the branch, when more
-// than 1 / 8 of the groups are distinct, or past 2^16 patterns.  On the
+// bases 1..min(4, n - 1).  Declined when an order has no PAT kernels, when
+// more than 1 / 8 of the groups are distinct, or past 16^min(4, n - 1)
+// patterns.  On the
 // structured block layout a handful of layouts (which rows are carried,
 // slotted or merged) cover every group.
 static bool build_map_patterns(std::vector<uint16_t>& m16, std::vector<uint32_t>& mb, int n,
                                int lw, int64_t n_slots, int64_t* n_pat) {
   *n_pat = 0;
-  if (n < 5 || n > 31 || !((SEM_MAP_PATTERN_N >> n) & 1u) || SEM_MAP_TOUCH) return false;
+  if (n < 3 || n > 31 || !((SEM_MAP_PATTERN_N >> n) & 1u) || SEM_MAP_TOUCH) return false;
+  const int Q = std::min(4, n - 1);  // bases carrying the id (PatternMap::id_rows)
+  const uint32_t max_pat = 1u << (4 * Q);
   const size_t blk = (size_t)n * lw;
   std::unordered_map<uint64_t, std::vector<uint32_t>> seen;
   std::vector<uint16_t> table;
@@ -827,21 +830,21 @@ static bool build_map_patterns(std::vector<uint16_t>& m16, std::vector<uint32_t>
       }
     if (id == 0xFFFFFFFFu) {
       id = (uint32_t)(table.size() / blk);
-      if (id >= 65536u || (int64_t)id * 8 > n_slots) return false;
+      if (id >= max_pat || (int64_t)id * 8 > n_slots) return false;
       table.insert(table.end(), e, e + blk);
       cand.push_back(id);
     }
     pid[(size_t)sl] = id;
   }
-  // bases 1..4 must have their top 4 bits free (node ids < 2^28: packed maps)
+  // bases 1..Q must have their top 4 bits free (node ids < 2^28: packed maps)
   for (int64_t sl = 0; sl < n_slots; ++sl) {
     if (mb[(size_t)sl * n] == M16_WIDE) continue;
-    for (int q = 1; q <= 4; ++q)
+    for (int q = 1; q <= Q; ++q)
       if (mb[(size_t)sl * n + q] & ~GID_MASK) return false;
   }
   for (int64_t sl = 0; sl < n_slots; ++sl) {
     if (mb[(size_t)sl * n] == M16_WIDE) continue;
-    for (int q = 0; q < 4; ++q)
+    for (int q = 0; q < Q; ++q)
       mb[(size_t)sl * n + 1 + q] |= ((pid[(size_t)sl] >> (4 * q)) & 15u) << 28;
   }
   *n_pat = (int64_t)(table.size() / blk);

@@ -725,15 +725,17 @@ constexpr uint32_t M16_WIDE = 0xFFFFFFFFu;  // base[slot][0]: this group uses th
 constexpr int M16_CODE_SHIFT = 12;
 
 // orders with pattern-table (PAT) kernels (SEM_MAP_PATTERN_N, a bit per n;
-// the host builds a table only for these): every order from n = 5, where
-// the pattern id fits the bases 1..4 -- measured faster at p = 4 / 6 / 8 /
-// 10 / 12 / 14 / 16
+// the host builds a table only for these): every order from n = 3 --
+// measured faster at p = 4 / 6 / 8 / 10 / 12 / 14 / 16.  The
+// pattern id sits in the top 4 bits of bases 1..id_rows (min(4, n - 1)):
+// up to 16^id_rows patterns.
 #ifndef SEM_MAP_PATTERN_N
-#define SEM_MAP_PATTERN_N 0x3FFE0u
+#define SEM_MAP_PATTERN_N 0x3FFF8u
 #endif
 template <int N>
 struct PatternMap {
-  static constexpr bool value = N >= 5 && ((SEM_MAP_PATTERN_N >> N) & 1u);
+  static constexpr bool value = N >= 3 && ((SEM_MAP_PATTERN_N >> N) & 1u);
+  static constexpr int id_rows = N - 1 < 4 ? N - 1 : 4;
 };
 
 template <int N, bool M16 = false, bool LD = false, bool PAT = false>
@@ -752,8 +754,10 @@ __device__ __forceinline__ void load_map(const MapRef& m, int64_t g, int lane, b
     if constexpr (PAT) {  // the pattern's entries follow the bases
 #pragma unroll
       for (int r = 0; r < N; ++r) b[r] = bp[r];
-      const int64_t pid = (b[1] >> 28) | ((b[2] >> 28) << 4) | ((b[3] >> 28) << 8) |
-                          ((b[4] >> 28) << 12);
+      constexpr int Q = PatternMap<N>::id_rows;
+      int64_t pid = 0;
+#pragma unroll
+      for (int q = 1; q <= Q; ++q) pid |= (int64_t)(b[q] >> 28) << (4 * (q - 1));
       const uint16_t* mp = m.p16 + pid * (int64_t)(N * LW) + (in_wave ? lane : LW - 1);
 #pragma unroll
       for (int r = 0; r < N; ++r) {
@@ -770,9 +774,9 @@ __device__ __forceinline__ void load_map(const MapRef& m, int64_t g, int lane, b
 #pragma unroll
       for (int r = 0; r < N; ++r) b[r] = bp[r];
     }
-    if constexpr (PAT)  // bases 1..4 carry the pattern id above the node id
+    if constexpr (PAT)  // bases 1..Q carry the pattern id above the node id
 #pragma unroll
-      for (int r = 1; r < 5; ++r) b[r] &= GID_MASK;
+      for (int r = 1; r <= PatternMap<N>::id_rows; ++r) b[r] &= GID_MASK;
 #pragma unroll
     for (int r = 0; r < N; ++r)
       raw[r] = (b[r] + (o[r] & M16_OFF_MASK)) | ((o[r] >> M16_CODE_SHIFT) << CODE_SHIFT);
