@@ -1426,7 +1426,7 @@ int sem_set_map_shared(sem_ctx* c, const uint32_t* d_e2n, const uint8_t* d_node_
     std::vector<uint32_t> mb;
     if (build_map16(P, c->n_elem, n, c->epw, c->n_groups, m16, mb)) {
       const char* pe = std::getenv("SEM_MAP_PATTERNS");
-      c->map_pat = c->dpn == 1 && !(pe && std::atoi(pe) == 0) &&
+      c->map_pat = !(pe && std::atoi(pe) == 0) &&
                    build_map_patterns(m16, mb, n, c->epw * n, P.n_slots, &c->n_map_pat);
       HIP_TRY(hipMalloc(&c->d_map16, m16.size() * sizeof(uint16_t)));
       HIP_TRY(hipMemcpy(c->d_map16, m16.data(), m16.size() * sizeof(uint16_t),

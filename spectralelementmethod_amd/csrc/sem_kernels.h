@@ -1839,7 +1839,7 @@ __device__ __forceinline__ void axisym_group(const uint32_t* __restrict__ mapP,
 #ifndef SEM_AXI_EARLY_U
 #define SEM_AXI_EARLY_U 0
 #endif
-template <int N, bool M16>
+template <int N, bool M16, bool PAT = false>
 __device__ __forceinline__ void axisym_group_nodal(const MapRef& mref,
                                                    const double2* __restrict__ XG,
                                                    const double* __restrict__ u, int64_t g,
@@ -1848,7 +1848,7 @@ __device__ __forceinline__ void axisym_group_nodal(const MapRef& mref,
                                                    double wj, uint32_t (&raw)[N], double (&vo)[N],
                                                    double (&vp)[N]) {
   constexpr int RS = Tile<N>::RS;
-  load_map<N, M16>(mref, g, lane, in_wave, raw);
+  load_map<N, M16, false, PAT>(mref, g, lane, in_wave, raw);
   double2 xc[N];
   gather_x<N>(XG, raw, j, xc);
   const double2* u2 = reinterpret_cast<const double2*>(u);
@@ -2003,7 +2003,7 @@ __device__ __forceinline__ void axisym_group_nodal(const MapRef& mref,
 #ifndef SEM_AXI_FIELDS_FIRST
 #define SEM_AXI_FIELDS_FIRST 1
 #endif
-template <int N, bool M16>
+template <int N, bool M16, bool PAT = false>
 __device__ __forceinline__ void axisym_group_nodal3(const MapRef& mref,
                                                     const double2* __restrict__ XG,
                                                     const double* __restrict__ u, int64_t g,
@@ -2014,7 +2014,7 @@ __device__ __forceinline__ void axisym_group_nodal3(const MapRef& mref,
                                                     double (&vp)[N]) {
   constexpr int RS = Tile<N>::RS;
   constexpr bool SP = SEM_LDS_SPLIT_AXI;
-  load_map<N, M16>(mref, g, lane, in_wave, raw);
+  load_map<N, M16, false, PAT>(mref, g, lane, in_wave, raw);
   const double2* u2 = reinterpret_cast<const double2*>(u);
   double om[N], d0p[N], d0o[N];
   {
@@ -2117,7 +2117,7 @@ struct AxiNodal {
                                             : SEM_AXI_MIN_WAVES;
 };
 
-template <int N, bool M16, bool SEAM = false>
+template <int N, bool M16, bool SEAM = false, bool PAT = false>
 __global__ void __launch_bounds__(ChainWaves<N>::block, AxiNodal<N>::waves)
     k_axisym_nodal(const MapRef mref, const double2* __restrict__ XG, const double* __restrict__ u,
                    double* __restrict__ y, int64_t c0, int64_t c1, int rounds, int accumulate,
@@ -2143,10 +2143,10 @@ __global__ void __launch_bounds__(ChainWaves<N>::block, AxiNodal<N>::waves)
     uint32_t raw[N];
     double v[2][N];  // [0] omega row (y[2k]), [1] psi row (y[2k+1])
     if constexpr (AxiNodal<N>::fields_first)
-      axisym_group_nodal3<N, M16>(mref, XG, u, g, lane, j, in_wave, LP, LO,
+      axisym_group_nodal3<N, M16, PAT>(mref, XG, u, g, lane, j, in_wave, LP, LO,
                                   LO + T::TILE_SLOTS * T::ES, D, w, wj, raw, v[0], v[1]);
     else
-      axisym_group_nodal<N, M16>(mref, XG, u, g, lane, j, in_wave, LP, LO, D, w, wj, raw, v[0],
+      axisym_group_nodal<N, M16, PAT>(mref, XG, u, g, lane, j, in_wave, LP, LO, D, w, wj, raw, v[0],
                                  v[1]);
     SeamOut so;
     if constexpr (SEAM) so.base = sp.buf + sp.colour[chain] * sp.n_node * 2;

@@ -92,6 +92,13 @@ void launch_chains(sem_ctx* c, int op_kind, bool nodal, const double* u, double*
       hipLaunchKernelGGL((k_poisson_apply<N, false, false, SEAM>), g, b, 0, st, mr, GP, XG, u, y,
                          c0, c1, R, acc, D, w, sp);
   } else if (op_kind == SEM_OP_AXISYM_STOKES && nodal) {
+    if constexpr (PatternMap<N>::value) {
+      if (c->map_pat) {  // the 16-bit map as a pattern table
+        hipLaunchKernelGGL((k_axisym_nodal<N, true, SEAM, true>), g, b, 0, st, mr, c->d_XG, u, y,
+                           c0, c1, R, acc, D, w, sp);
+        return;
+      }
+    }
     if (c->map16)
       hipLaunchKernelGGL((k_axisym_nodal<N, true, SEAM>), g, b, 0, st, mr, c->d_XG, u, y, c0, c1,
                          R, acc, D, w, sp);
