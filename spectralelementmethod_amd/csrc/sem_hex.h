@@ -408,7 +408,7 @@ __global__ void __launch_bounds__(hex_threads(N), hex_min_waves(N))
 // three-block kernel gets there
 constexpr int hex_rows_min_waves(int n) { return n <= 9 ? 4 : n <= 11 ? 3 : n <= 13 ? 2 : 1; }
 
-template <int N, int MODE>
+template <int N, int MODE, bool TM = false>
 __global__ void __launch_bounds__(hex_threads(N), hex_rows_min_waves(N))
     k_hex_rows(const double* __restrict__ u, double* __restrict__ y,
                const uint32_t* __restrict__ map, const double* __restrict__ G,
@@ -447,9 +447,19 @@ __global__ void __launch_bounds__(hex_threads(N), hex_rows_min_waves(N))
   double carry = 0.0;
   uint32_t mn[N];
   int en = active ? P.elist[base + s] : 0;
-  if (active) {
+  [[maybe_unused]] int toff[TM ? N : 1];  // template map (HexLaunch::tmpl)
+  if constexpr (TM)
 #pragma unroll
-    for (int a = 0; a < N; ++a) mn[a] = map[(int64_t)en * N3 + a * N2 + bc];
+    for (int a = 0; a < N; ++a) toff[a] = P.tmpl[a * N2 + bc];
+  if (active) {
+    if constexpr (TM) {
+      const uint32_t eb = P.ebase[en];
+#pragma unroll
+      for (int a = 0; a < N; ++a) mn[a] = eb + (uint32_t)toff[a];
+    } else {
+#pragma unroll
+      for (int a = 0; a < N; ++a) mn[a] = map[(int64_t)en * N3 + a * N2 + bc];
+    }
   }
 #pragma unroll 1
   for (int k = 0; k < L; ++k) {
@@ -469,8 +479,14 @@ __global__ void __launch_bounds__(hex_threads(N), hex_rows_min_waves(N))
     __syncthreads();  // u complete; the previous element's ring / sX reads are done
     if (active && k + 1 < L) {
       en = P.elist[pos + S];
+      if constexpr (TM) {
+        const uint32_t eb = P.ebase[en];
 #pragma unroll
-      for (int a = 0; a < N; ++a) mn[a] = map[(int64_t)en * N3 + a * N2 + bc];
+        for (int a = 0; a < N; ++a) mn[a] = eb + (uint32_t)toff[a];
+      } else {
+#pragma unroll
+        for (int a = 0; a < N; ++a) mn[a] = map[(int64_t)en * N3 + a * N2 + bc];
+      }
     }
     double yv[N];
 #pragma unroll

@@ -47,7 +47,7 @@ struct HexState {
   // xi1 faces between the rows of a workgroup's slot grid too (three-block
   // kernel only; SEM_HEX_YMERGE=0 turns it off)
   bool ymerge = false;
-  // template map (HexLaunch::ebase / tmpl; three-block kernel): every
+  // template map (HexLaunch::ebase / tmpl; both kernel forms): every
   // element's ids = its first node's id + one offset block (SEM_HEX_TMAP=0
   // turns it off)
   bool tmap = false;
@@ -568,7 +568,13 @@ int launch_hex_apply(sem_ctx* c, int mode, const double* u, double* y, hipStream
   const dim3 g((unsigned)H->n_wg), b(semh::hex_threads(N));
   semh::HexD<N> Dk;
   for (int i = 0; i < N * N; ++i) Dk.d[i] = c->hD[i];
-  if (H->rows && mode == semh::HEX_SET)
+  if (H->rows && H->tmap && mode == semh::HEX_SET)
+    hipLaunchKernelGGL((semh::k_hex_rows<N, semh::HEX_SET, true>), g, b, 0, st, u, y, H->d_map,
+                       H->d_G, c->d_D, L, Dk);
+  else if (H->rows && H->tmap && mode == semh::HEX_ACC)
+    hipLaunchKernelGGL((semh::k_hex_rows<N, semh::HEX_ACC, true>), g, b, 0, st, u, y, H->d_map,
+                       H->d_G, c->d_D, L, Dk);
+  else if (H->rows && mode == semh::HEX_SET)
     hipLaunchKernelGGL((semh::k_hex_rows<N, semh::HEX_SET>), g, b, 0, st, u, y, H->d_map, H->d_G,
                        c->d_D, L, Dk);
   else if (H->rows && mode == semh::HEX_ACC)
@@ -839,10 +845,10 @@ int set_map(sem_ctx* c, const uint32_t* d_e2n, hipStream_t st) {
       (rc = upload(&H->d_zero, P.zero)))
     return rc;
   // template map: one offset block shared by every element (structured
-  // numberings), three-block kernel only
+  // numberings); both kernel forms and the diagonal
   {
     const char* te = std::getenv("SEM_HEX_TMAP");
-    bool ok = !H->rows && c->n_elem > 0 && !(te && std::atoi(te) == 0);
+    bool ok = c->n_elem > 0 && !(te && std::atoi(te) == 0);
     std::vector<int> tmpl((size_t)N3);
     std::vector<uint32_t> eb;
     if (ok) {

@@ -201,16 +201,18 @@ def test_hex_ymerge_vs_oracle(sem, gll, monkeypatch, p, gy, gz):
     assert seams["1"] < seams["0"], seams
 
 
+@pytest.mark.parametrize("rows", ["0", "1"])
 @pytest.mark.parametrize("p", [2, 5, 8])
-def test_hex_template_map_bitwise(sem, monkeypatch, p):
+def test_hex_template_map_bitwise(sem, monkeypatch, p, rows):
     """The template map (one base per element, the column's offsets in
     registers) gives the per-element map's action and diagonal bit for bit
-    on a structured cube; shuffled node ids keep the map."""
+    on a structured cube, in both kernel forms; shuffled node ids keep the
+    map."""
     from spectralelementmethod_amd import meshgen
     nodes, e2n = meshgen.structured_cube(5, 4, 3, p, warp=0.05)
     u = torch.from_numpy(np.random.default_rng(p).standard_normal(nodes.shape[1])).cuda()
     out = {}
-    monkeypatch.setenv("SEM_HEX_ROWS", "0")
+    monkeypatch.setenv("SEM_HEX_ROWS", rows)
     for tm in ("1", "0"):
         monkeypatch.setenv("SEM_HEX_TMAP", tm)
         op = sem.SEMOperator(p, e2n, nodes)
